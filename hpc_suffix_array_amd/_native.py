@@ -1,0 +1,147 @@
+"""ctypes binding of libsa_hip.so (include/sa_hip.h, include/suffix_array.h).
+
+The library is built in-tree by ``hpc_suffix_array_amd/csrc/Makefile`` into
+``hpc_suffix_array_amd/lib/libsa_hip.so``.  Loading it never touches the GPU;
+every compute entry point fails loudly (SAError) when no HIP device is
+present -- there is no CPU fallback anywhere in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG_DIR, "lib", "libsa_hip.so")
+CSRC = os.path.join(PKG_DIR, "csrc")
+
+SA_MAX_ROUNDS = 64
+KERNEL_KINDS = ["init", "hist_rank", "hist_keys", "scan", "scatter_rank", "scatter_keys",
+                "heads", "heads_scan", "rerank"]
+SA_K_COUNT = len(KERNEL_KINDS)
+
+# every symbol include/*.h declares
+DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_array",
+                  "build_lcp_array", "find_longest_repeated_substring", "is_valid_suffix_array"]
+EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", "sa_build_device",
+               "sa_build_ex", "sa_check_device", "sa_check", "sa_generate_text_device",
+               "sa_last_error", "sa_device_count", "sa_version"]
+
+
+class SAError(RuntimeError):
+    """A libsa_hip entry point returned an error code."""
+
+
+class SaOpts(ctypes.Structure):
+    _fields_ = [("profile", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+
+
+class SaStats(ctypes.Structure):
+    _fields_ = [
+        ("rounds", ctypes.c_int32),
+        ("n_kinds", ctypes.c_int32),
+        ("total_ms", ctypes.c_double),
+        ("h2d_ms", ctypes.c_double),
+        ("d2h_ms", ctypes.c_double),
+        ("round_ms", ctypes.c_double * SA_MAX_ROUNDS),
+        ("distinct", ctypes.c_uint64 * SA_MAX_ROUNDS),
+        ("passes", ctypes.c_int32 * SA_MAX_ROUNDS),
+        ("model_bytes", ctypes.c_uint64),
+        ("kern_ms", ctypes.c_double * SA_K_COUNT),
+        ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
+        ("kern_bytes", ctypes.c_uint64 * SA_K_COUNT),
+    ]
+
+    def to_dict(self) -> dict:
+        r = self.rounds
+        return {
+            "rounds": r,
+            "total_ms": self.total_ms,
+            "h2d_ms": self.h2d_ms,
+            "d2h_ms": self.d2h_ms,
+            "round_ms": list(self.round_ms[:r]),
+            "distinct": [int(x) for x in self.distinct[:r]],
+            "passes": list(self.passes[:r]),
+            "model_bytes": int(self.model_bytes),
+            "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
+                            "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},
+        }
+
+
+class SuffixArrayStruct(ctypes.Structure):
+    """SuffixArray of suffix_array.h:16-21 (32 bytes: str@0 n@8 sa@16 lcp@24)."""
+    _fields_ = [("str", ctypes.c_void_p), ("n", ctypes.c_int),
+                ("sa", ctypes.POINTER(ctypes.c_int)), ("lcp", ctypes.POINTER(ctypes.c_int))]
+
+
+_lib = None
+
+
+def build_library(force: bool = False) -> str:
+    """Compile libsa_hip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
+    if force or not os.path.exists(LIB_PATH):
+        subprocess.run(["make", "-s", "-C", CSRC], check=True)
+    return LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SAError(f"{LIB_PATH} is missing: run `make -C {CSRC}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, i32 = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int
+    L.sa_context_create.argtypes = [i32, u64, ctypes.POINTER(vp)]
+    L.sa_context_create.restype = i32
+    L.sa_context_destroy.argtypes = [vp]
+    L.sa_context_destroy.restype = None
+    L.sa_workspace_bytes.argtypes = [u64]
+    L.sa_workspace_bytes.restype = u64
+    L.sa_build_device.argtypes = [vp, vp, u64, vp, vp, ctypes.POINTER(SaOpts), ctypes.POINTER(SaStats)]
+    L.sa_build_device.restype = i32
+    L.sa_build_ex.argtypes = [vp, u64, vp, i32, ctypes.POINTER(SaOpts), ctypes.POINTER(SaStats)]
+    L.sa_build_ex.restype = i32
+    L.sa_check_device.argtypes = [vp, vp, u64, vp, vp]
+    L.sa_check_device.restype = i32
+    L.sa_check.argtypes = [vp, u64, vp, i32]
+    L.sa_check.restype = i32
+    L.sa_generate_text_device.argtypes = [vp, u64, u64, ctypes.c_char_p, ctypes.c_uint32, vp]
+    L.sa_generate_text_device.restype = i32
+    L.sa_last_error.argtypes = []
+    L.sa_last_error.restype = ctypes.c_char_p
+    L.sa_device_count.argtypes = []
+    L.sa_device_count.restype = i32
+    L.sa_version.argtypes = []
+    L.sa_version.restype = ctypes.c_char_p
+    P = ctypes.POINTER(SuffixArrayStruct)
+    L.create_suffix_array.argtypes = [ctypes.c_char_p, i32]
+    L.create_suffix_array.restype = P
+    L.destroy_suffix_array.argtypes = [P]
+    L.destroy_suffix_array.restype = None
+    L.build_suffix_array.argtypes = [P]
+    L.build_suffix_array.restype = None
+    L.build_lcp_array.argtypes = [P]
+    L.build_lcp_array.restype = None
+    L.find_longest_repeated_substring.argtypes = [P]
+    L.find_longest_repeated_substring.restype = vp
+    L.is_valid_suffix_array.argtypes = [P]
+    L.is_valid_suffix_array.restype = i32
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise SAError(f"{what}: {lib().sa_last_error().decode(errors='replace')} (code {rc})")
+    return rc
+
+
+def device_count() -> int:
+    return lib().sa_device_count()
+
+
+def require_device() -> None:
+    """Fail loudly when the HIP path cannot run (no silent fallback)."""
+    if device_count() <= 0:
+        raise SAError("no HIP device visible: libsa_hip builds suffix arrays on an MI355X only")

@@ -1,0 +1,186 @@
+"""Host-side mirror of the reference's suffix-array interface over libsa_hip.
+
+Reference interface (src/common/suffix_array.h:24-29, manber_myers.c):
+    create_suffix_array / build_suffix_array / build_lcp_array /
+    find_longest_repeated_substring / is_valid_suffix_array / destroy
+``SuffixArray`` below drives exactly those six C symbols of libsa_hip.so
+through ctypes (the drop-in boundary), with the same argument meaning and
+the same results.  ``build_suffix_array`` / ``check_suffix_array`` use the
+64-bit extended ABI (sa_build_ex / sa_check) and ``DeviceBuilder`` the
+device-resident one (sa_build_device) that bench.py times.
+
+Nothing here computes a suffix array on the CPU: every path runs the HIP
+kernels, and raises SAError when no GPU is visible.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import numpy as np
+
+from . import _native as N
+
+
+def _as_bytes_array(text) -> np.ndarray:
+    if isinstance(text, (bytes, bytearray, memoryview)):
+        return np.frombuffer(bytes(text), dtype=np.uint8)
+    if isinstance(text, str):
+        return np.frombuffer(text.encode("latin-1"), dtype=np.uint8)
+    return np.ascontiguousarray(text, dtype=np.uint8)
+
+
+def _opts(profile: bool) -> N.SaOpts:
+    o = N.SaOpts()
+    o.profile = 1 if profile else 0
+    return o
+
+
+def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False):
+    """Suffix array of ``text`` (bytes / uint8 array), built on the GPU.
+
+    Unsigned-byte order, end of string smallest (== the reference's order on
+    its valid domain, manber_myers.c:81-133).  Returns uint32 (width 4) or
+    int64 (width 8); with ``return_stats`` also the per-round statistics."""
+    t = _as_bytes_array(text)
+    n = int(t.size)
+    N.require_device()
+    out = np.empty(max(n, 1), dtype=np.uint32 if width == 4 else np.int64)
+    st = N.SaStats()
+    L = N.lib()
+    N.check(L.sa_build_ex(t.ctypes.data if n else None, n, out.ctypes.data, width,
+                          ctypes.byref(_opts(profile)), ctypes.byref(st)), "sa_build_ex")
+    out = out[:n]
+    return (out, st.to_dict()) if return_stats else out
+
+
+def check_suffix_array(text, sa) -> bool:
+    """O(n) GPU validity check (replaces is_valid_suffix_array, :184-202)."""
+    t = _as_bytes_array(text)
+    s = np.ascontiguousarray(sa)
+    if s.dtype not in (np.uint32, np.int32, np.int64):
+        s = s.astype(np.int64)
+    if s.size != t.size:
+        return False
+    N.require_device()
+    width = 8 if s.dtype == np.int64 else 4
+    r = N.check(N.lib().sa_check(t.ctypes.data if t.size else None, t.size,
+                                 s.ctypes.data if s.size else None, width), "sa_check")
+    return bool(r)
+
+
+class SuffixArray:
+    """The reference's SuffixArray object (suffix_array.h:16-21) driven
+    through the drop-in C symbols of libsa_hip.so.
+
+    >>> s = SuffixArray(b"banana"); s.build(); s.sa   -> [5, 3, 1, 0, 4, 2]
+    """
+
+    def __init__(self, text, n: Optional[int] = None):
+        raw = bytes(_as_bytes_array(text))
+        self.L = N.lib()
+        self.n = len(raw) if n is None else int(n)
+        self._buf = ctypes.create_string_buffer(raw, max(len(raw), self.n) + 1)
+        self.p = self.L.create_suffix_array(self._buf, self.n)     # manber_myers.c:51-69
+        if not self.p:
+            raise MemoryError("create_suffix_array returned NULL")
+
+    def build(self) -> None:
+        if self.n > 0:
+            N.require_device()
+        self.L.build_suffix_array(self.p)                           # :81-133
+
+    def build_lcp(self) -> None:
+        self.L.build_lcp_array(self.p)                              # :135-157
+
+    def longest_repeated_substring(self) -> Optional[bytes]:
+        r = self.L.find_longest_repeated_substring(self.p)          # :159-182
+        if not r:
+            return None
+        s = ctypes.string_at(r)
+        ctypes.CDLL(None).free(ctypes.c_void_p(r))
+        return s
+
+    def is_valid(self) -> bool:
+        if self.n > 0:
+            N.require_device()
+        return bool(self.L.is_valid_suffix_array(self.p))           # :184-202
+
+    @property
+    def text(self) -> bytes:
+        return ctypes.string_at(self.p.contents.str, self.n)
+
+    @property
+    def sa(self) -> np.ndarray:
+        if self.n == 0:
+            return np.zeros(0, dtype=np.int32)
+        return np.ctypeslib.as_array(self.p.contents.sa, shape=(self.n,)).copy()
+
+    @property
+    def lcp(self) -> np.ndarray:
+        if self.n == 0:
+            return np.zeros(0, dtype=np.int32)
+        return np.ctypeslib.as_array(self.p.contents.lcp, shape=(self.n,)).copy()
+
+    def close(self) -> None:
+        if getattr(self, "p", None):
+            self.L.destroy_suffix_array(self.p)                     # :71-78
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+
+class DeviceBuilder:
+    """Device-resident builder: text and SA live in HBM (torch tensors or raw
+    device pointers).  Holds one sa_context (workspace sized for max_n)."""
+
+    def __init__(self, max_n: int, device: int = 0):
+        N.require_device()
+        self.L = N.lib()
+        self.ctx = ctypes.c_void_p()
+        N.check(self.L.sa_context_create(device, max_n, ctypes.byref(self.ctx)), "sa_context_create")
+        self.device = device
+
+    @staticmethod
+    def _ptr(x) -> int:
+        return x if isinstance(x, int) else int(x.data_ptr())
+
+    def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False) -> dict:
+        """Build the SA of the n bytes at d_text into the n uint32 at d_sa."""
+        st = N.SaStats()
+        s = None if stream is None else ctypes.c_void_p(int(stream))
+        N.check(self.L.sa_build_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s,
+                                       ctypes.byref(_opts(profile)), ctypes.byref(st)), "sa_build_device")
+        return st.to_dict()
+
+    def generate_text(self, d_out, n: int, alphabet: bytes, seed: int = 1, stream=None) -> None:
+        """Fill n device bytes with the seeded splitmix64 text."""
+        s = None if stream is None else ctypes.c_void_p(int(stream))
+        N.check(self.L.sa_generate_text_device(self._ptr(d_out), n, seed, alphabet, len(alphabet), s),
+                "sa_generate_text_device")
+
+    def check(self, d_text, n: int, d_sa, stream=None) -> bool:
+        s = None if stream is None else ctypes.c_void_p(int(stream))
+        return bool(N.check(self.L.sa_check_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s),
+                            "sa_check_device"))
+
+    def close(self) -> None:
+        if self.ctx:
+            self.L.sa_context_destroy(self.ctx)
+            self.ctx = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,107 @@
+/*
+ * include/sa_hip.h -- extended 64-bit C ABI of libsa_hip.so.
+ *
+ * The reference has no 64-bit or device-resident entry point; these replace
+ * what its callers do around build_suffix_array (manber_myers.c:81-133):
+ *   sa_build_ex      -- host text in, host SA out (create+build of
+ *                       main_sequential.c:97-109 without the int n limit,
+ *                       SURVEY.md 8(b) "What the replacement exports" (2))
+ *   sa_build_device  -- text already resident in HBM, SA written to HBM
+ *                       (what bench.py times)
+ *   sa_check[_device]-- O(n) validity check replacing is_valid_suffix_array
+ *                       (manber_myers.c:184-202), SURVEY.md 8(b) (3)
+ * All functions return 0 on success or a negative SA_E* code; the text of
+ * the last error of the calling thread is available from sa_last_error().
+ * No torch types cross this boundary: plain pointers, sizes and a stream
+ * handle (hipStream_t passed as void*, NULL = the null stream).
+ */
+#ifndef SA_HIP_H
+#define SA_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SA_OK 0
+#define SA_E_INVALID (-1)   /* bad argument (NULL pointer, width, n too large) */
+#define SA_E_NOMEM (-2)     /* device or host allocation failed */
+#define SA_E_HIP (-3)       /* HIP runtime error (no device, launch failure) */
+#define SA_E_INTERNAL (-4)  /* internal consistency check failed */
+
+#define SA_MAX_ROUNDS 64
+
+/* kernel kinds timed when sa_opts.profile != 0 */
+enum sa_kernel_kind {
+    SA_K_INIT = 0,          /* text -> rank_1 */
+    SA_K_HIST_RANK = 1,     /* digit histogram, keys generated from ranks */
+    SA_K_HIST_KEYS = 2,     /* digit histogram over stored keys */
+    SA_K_SCAN = 3,          /* digit x chunk offset scan */
+    SA_K_SCATTER_RANK = 4,  /* stable scatter, keys generated from ranks */
+    SA_K_SCATTER_KEYS = 5,  /* stable scatter over stored (key, idx) */
+    SA_K_HEADS = 6,         /* group-head count per chunk */
+    SA_K_HEADS_SCAN = 7,    /* chunk scan of head counts, D_j */
+    SA_K_RERANK = 8,        /* dense rank -> rank[idx] scatter */
+    SA_K_COUNT = 9
+};
+
+typedef struct {
+    int32_t profile;        /* 1: time every launch with HIP events */
+    int32_t reserved[7];
+} sa_opts;
+
+typedef struct {
+    int32_t rounds;                      /* doubling rounds executed */
+    int32_t n_kinds;                     /* = SA_K_COUNT */
+    double total_ms;                     /* build time on the stream (HBM in -> HBM out) */
+    double h2d_ms, d2h_ms;               /* sa_build_ex only: PCIe copies */
+    double round_ms[SA_MAX_ROUNDS];      /* per doubling round */
+    uint64_t distinct[SA_MAX_ROUNDS];    /* D_j after round j */
+    int32_t passes[SA_MAX_ROUNDS];       /* radix passes in round j */
+    uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
+    double kern_ms[SA_K_COUNT];          /* profile only */
+    uint64_t kern_launches[SA_K_COUNT];  /* profile only */
+    uint64_t kern_bytes[SA_K_COUNT];     /* algorithmic bytes moved per kind */
+} sa_stats;
+
+typedef struct sa_context sa_context;
+
+/* Device workspace for texts of up to max_n symbols on `device`. */
+int sa_context_create(int device, uint64_t max_n, sa_context** out);
+void sa_context_destroy(sa_context* ctx);
+/* bytes of device memory a context for max_n needs */
+uint64_t sa_workspace_bytes(uint64_t max_n);
+
+/* d_text: n bytes in device memory; d_sa: n uint32 in device memory.
+ * n <= 2^32 - 1.  Enqueued on `stream`; returns after the SA is complete
+ * (one 4-byte D_j read-back per round synchronises the stream). */
+int sa_build_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint32_t* d_sa,
+                    void* stream, const sa_opts* opts, sa_stats* stats);
+
+/* Host in, host out.  sa_width is 4 (int32/uint32) or 8 (int64). */
+int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width,
+                const sa_opts* opts, sa_stats* stats);
+
+/* O(n) check on the GPU: 1 valid, 0 invalid, <0 error. */
+int sa_check_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa,
+                    void* stream);
+int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width);
+
+/* Seeded synthetic text in device memory: the splitmix64 generator of
+ * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
+ * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */
+int sa_generate_text_device(uint8_t* d_out, uint64_t n, uint64_t seed, const uint8_t* alphabet,
+                            uint32_t sigma, void* stream);
+
+const char* sa_last_error(void);
+/* number of visible HIP devices (0 when none; never aborts) */
+int sa_device_count(void);
+/* library build identification, e.g. "sa_hip gfx950 <date>" */
+const char* sa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SA_HIP_H */

@@ -1,0 +1,94 @@
+"""CPU tests of the drop-in boundary: libsa_hip.so loads without a GPU,
+exports every symbol include/*.h declares, keeps the reference's struct
+layout (suffix_array.h:16-21), and refuses to compute without a device."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    names = set()
+    for h in ("suffix_array.h", "sa_hip.h"):
+        src = open(os.path.join(ROOT, "include", h)).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        for m in re.finditer(r"^\s*[A-Za-z_][\w\s\*]*?\b([a-z_][a-z0-9_]*)\s*\([^;{]*\)\s*;", src, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_header_declarations_parsed():
+    names = declared_functions()
+    assert {"create_suffix_array", "build_suffix_array", "sa_build_ex", "sa_build_device"} <= names
+
+
+def test_exports_every_declared_symbol(sa_lib):
+    out = subprocess.run(["nm", "-D", "--defined-only", sa_lib.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = declared_functions() - exported
+    assert not missing, missing
+    assert set(sa_lib.DROPIN_SYMBOLS) <= exported
+    assert set(sa_lib.EXT_SYMBOLS) <= exported
+
+
+def test_library_loads_and_reports(sa_lib):
+    L = sa_lib.lib()
+    assert b"gfx950" in L.sa_version()
+    assert L.sa_device_count() >= 0
+    assert L.sa_workspace_bytes(1 << 30) >= 24 * (1 << 30)  # rank + 2 keys + 1 index buffer
+
+
+def test_code_object_targets_gfx950(sa_lib):
+    data = open(sa_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+
+
+def test_struct_layout(sa_lib):
+    S = sa_lib.SuffixArrayStruct
+    assert ctypes.sizeof(S) == 32
+    assert (S.str.offset, S.n.offset, S.sa.offset, S.lcp.offset) == (0, 8, 16, 24)
+
+
+def test_stats_struct_matches_header(sa_lib):
+    # sa_stats layout: 2 x i32, 3 doubles, 64 doubles, 64 u64, 64 i32, u64, 3 x 9 arrays
+    expected = 8 + 24 + 64 * 8 + 64 * 8 + 64 * 4 + 8 + 9 * 8 * 3
+    assert ctypes.sizeof(sa_lib.SaStats) == expected
+
+
+def test_create_has_strncpy_semantics(sa_lib):
+    # manber_myers.c:55-58: bytes after the first NUL become NUL; host-only code
+    L = sa_lib.lib()
+    p = L.create_suffix_array(b"ab\x00ba", 5)
+    assert p
+    try:
+        assert p.contents.n == 5
+        assert ctypes.string_at(p.contents.str, 6) == b"ab\x00\x00\x00\x00"
+    finally:
+        L.destroy_suffix_array(p)
+
+
+def test_no_cpu_fallback_without_device(sa_lib):
+    if sa_lib.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    from hpc_suffix_array_amd import SAError, build_suffix_array, check_suffix_array
+    with pytest.raises(SAError):
+        build_suffix_array(b"banana")
+    with pytest.raises(SAError):
+        check_suffix_array(b"banana", np.array([5, 3, 1, 0, 4, 2], np.uint32))
+    L = sa_lib.lib()
+    out = np.zeros(6, np.uint32)
+    rc = L.sa_build_ex(ctypes.c_char_p(b"banana"), 6, out.ctypes.data, 4, None, None)
+    assert rc < 0 and b"device" in L.sa_last_error()
+
+
+def test_invalid_arguments(sa_lib):
+    L = sa_lib.lib()
+    assert L.sa_build_ex(None, 4, None, 4, None, None) < 0
+    assert L.sa_build_ex(ctypes.c_char_p(b"abcd"), 4, None, 3, None, None) < 0
+    assert L.sa_context_create(0, 0, None) < 0

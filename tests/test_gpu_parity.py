@@ -1,0 +1,155 @@
+"""GPU parity: the HIP builder (through the C ABI) against the oracle.
+
+Bit-exact SA equality with
+  * the reference's own outputs (tests/golden, generated from the reference
+    compiled from its sources) -- small cases, every alphabet, ragged sizes;
+  * the C restatement of manber_myers.c (oracle/) on seeded inputs that the
+    oracle finishes in seconds;
+  * the SHA-256 known answer of config 2 (64 MiB DNA);
+and size-independent properties (O(n) checker, analytic degenerate SA) at
+larger sizes.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def test_golden_cases_ex(gpu, golden):
+    from hpc_suffix_array_amd import build_suffix_array, check_suffix_array
+    for name, c in golden["cases"].items():
+        got = build_suffix_array(c["text"])
+        assert got.dtype == np.uint32
+        assert (got == c["sa"]).all(), name
+        assert check_suffix_array(c["text"], got), name
+
+
+def test_golden_cases_dropin(gpu, golden):
+    """The six drop-in symbols, exactly as a reference caller uses them."""
+    from hpc_suffix_array_amd import SuffixArray
+    for name, c in golden["cases"].items():
+        t = bytes(c["text"])
+        if 0 in t:      # the drop-in truncates at NUL like strncpy (manber_myers.c:57)
+            continue
+        with SuffixArray(t) as s:
+            s.build()
+            assert (s.sa == c["sa"].astype(np.int32)).all(), name
+            s.build_lcp()
+            assert (s.lcp == c["lcp"].astype(np.int32)).all(), name
+            lrs = s.longest_repeated_substring()
+            assert (lrs or b"").hex() == c["lrs"], name
+            assert s.is_valid(), name
+
+
+def test_int64_output(gpu, oracle):
+    from hpc_suffix_array_amd import build_suffix_array
+    t = oracle.gen_text("alnum", 100_003, seed=5)
+    got = build_suffix_array(t, width=8)
+    assert got.dtype == np.int64
+    assert (got == oracle.sa_c(t).astype(np.int64)).all()
+
+
+@pytest.mark.parametrize("kind", ["dna", "alnum", "ascii127", "byte256", "binary"])
+@pytest.mark.parametrize("n", [1, 2, 3, 4095, 4096, 4097, 65535, 1 << 17, 1_000_003, 4_194_305])
+def test_random_vs_oracle(gpu, oracle, kind, n):
+    from hpc_suffix_array_amd import build_suffix_array
+    t = oracle.gen_text(kind, n, seed=n + len(kind))
+    got, st = build_suffix_array(t, return_stats=True)
+    ref, rounds, _, dj = oracle.sa_c(t, stats=True)
+    assert (got == ref).all()
+    if n > 1:
+        assert st["rounds"] == rounds
+        assert st["distinct"] == dj
+
+
+def test_known_answers_1mib(gpu, oracle, golden):
+    from hpc_suffix_array_amd import build_suffix_array
+    for key in ("alnum_1MiB", "ascii127_1MiB", "dna_1MiB", "byte256_1MiB"):
+        k = golden["known"][key]
+        t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
+        got = build_suffix_array(t)
+        assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"], key
+
+
+def test_config2_64mib_dna_known_answer(gpu, oracle, golden):
+    """configs[1]: 64 MiB random DNA on 1 MI355X, bit-exact vs sequential."""
+    from hpc_suffix_array_amd import build_suffix_array
+    k = golden["known"]["dna_64MiB"]
+    t = oracle.gen_text("dna", k["n"], seed=k["seed"])
+    assert oracle.sha256(t) == k["text_sha256"]
+    got, st = build_suffix_array(t, return_stats=True)
+    assert st["rounds"] == k["rounds"]
+    assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
+
+
+@pytest.mark.parametrize("n", [2, 17, 4096, 65537, 1 << 20, (1 << 22) + 3])
+def test_degenerate(gpu, n):
+    """configs[4] shape: one repeated symbol, log2 n rounds, analytic SA."""
+    from hpc_suffix_array_amd import build_suffix_array
+    got, st = build_suffix_array(np.full(n, ord("a"), np.uint8), return_stats=True)
+    assert (got == np.arange(n - 1, -1, -1, dtype=np.uint32)).all()
+    assert st["distinct"][-1] == n
+
+
+def test_periodic(gpu, oracle):
+    from hpc_suffix_array_amd import build_suffix_array
+    base = oracle.gen_text("alnum", 1000, seed=11)
+    t = np.tile(base, 300)
+    assert (build_suffix_array(t) == oracle.sa_c(t)).all()
+
+
+def test_checker_detects_corruption(gpu, oracle):
+    from hpc_suffix_array_amd import check_suffix_array
+    t = oracle.gen_text("dna", 300_000, seed=2)
+    sa = oracle.sa_c(t)
+    assert check_suffix_array(t, sa)
+    bad = sa.copy()
+    bad[[1000, 1001]] = bad[[1001, 1000]]
+    assert not check_suffix_array(t, bad)
+    dup = sa.copy()
+    dup[7] = dup[8]
+    assert not check_suffix_array(t, dup)
+    oob = sa.copy()
+    oob[0] = len(t)
+    assert not check_suffix_array(t, oob)
+
+
+def test_device_builder_torch(gpu, oracle):
+    """Device-resident path (what bench.py times), torch buffers in HBM."""
+    import torch
+    from hpc_suffix_array_amd import DeviceBuilder
+    n = 3_000_017
+    t = oracle.gen_text("dna", n, seed=4)
+    d_text = torch.from_numpy(t).cuda()
+    d_sa = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = DeviceBuilder(n)
+    st = b.build(d_text, n, d_sa, stream=torch.cuda.current_stream().cuda_stream, profile=True)
+    torch.cuda.synchronize()
+    got = d_sa.cpu().numpy().view(np.uint32)
+    assert (got == oracle.sa_c(t)).all()
+    assert b.check(d_text, n, d_sa)
+    assert st["kernels"]["scatter_keys"]["launches"] > 0
+    assert abs(sum(st["round_ms"]) - st["total_ms"]) < 0.5 * st["total_ms"] + 5
+    b.close()
+
+
+@pytest.mark.slow
+def test_config3_1gib_minus_1_known_answer(gpu, oracle, golden):
+    """configs[2] at the largest n the reference handles (2^30 - 1)."""
+    import torch
+    from hpc_suffix_array_amd import DeviceBuilder
+    k = golden["known"]["dna_1GiB_minus_1"]
+    n = k["n"]
+    t = oracle.gen_text("dna", n, seed=1)
+    d_text = torch.from_numpy(t).cuda()
+    del t
+    d_sa = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = DeviceBuilder(n)
+    st = b.build(d_text, n, d_sa)
+    assert st["rounds"] == k["rounds"]
+    assert b.check(d_text, n, d_sa)
+    sa = d_sa.cpu().numpy()
+    assert oracle.sha256(sa) == k["sa_sha256_i32"]
+    b.close()
