@@ -48,6 +48,18 @@ static int set_err(int code, const char* fmt, ...) {
                            __FILE__, __LINE__);                                              \
     } while (0)
 
+static bool trace_on() {
+    static const bool on = std::getenv("SA_TRACE") != nullptr;
+    return on;
+}
+#define SA_TRACE(...)                                   \
+    do {                                                \
+        if (trace_on()) {                               \
+            std::fprintf(stderr, "[sa] " __VA_ARGS__);  \
+            std::fputc('\n', stderr);                   \
+        }                                               \
+    } while (0)
+
 constexpr uint32_t kMaxChunks = 1024;
 constexpr int kEvPool = 256;
 
@@ -205,6 +217,7 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     SA_HIP(hipEventCreate(&start_all));
     SA_HIP(hipEventRecord(start_all, s));
 
+    SA_TRACE("build n=%llu", (unsigned long long)n);
     if (n == 1) {
         SA_HIP(hipMemsetAsync(d_sa, 0, 4, s));
     } else {
@@ -225,6 +238,8 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             const uint32_t w = bit_width(D);          // ranks are 0..D
             const uint32_t bits = 2 * w;
             const uint32_t P = (bits + 7) / 8;
+            SA_TRACE("round h=%llu D=%llu w=%u P=%u chunks=%u tpc=%u", (unsigned long long)h,
+                     (unsigned long long)D, w, P, ch.chunks, ch.tiles_per_chunk);
             // index buffers: pass p writes bufs[p & 1]; make pass P-1 write d_sa
             uint32_t* vb[2];
             vb[(P - 1) & 1] = d_sa;
@@ -257,6 +272,7 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4, hipMemcpyDeviceToHost, s));
             SA_HIP(hipStreamSynchronize(s));
             const uint64_t Dn = c->host_words[0];
+            SA_TRACE("  D'=%llu", (unsigned long long)Dn);
             const bool done = (Dn == n);
             if (!done) {
                 tm.begin(SA_K_RERANK);
@@ -480,7 +496,9 @@ int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, con
     }
     std::lock_guard<std::mutex> lk(g_mu);
     sa_context* c = nullptr;
+    SA_TRACE("sa_build_ex n=%llu", (unsigned long long)n);
     int rc = global_ctx(n, &c);
+    SA_TRACE("global ctx rc=%d", rc);
     if (rc) return rc;
     uint8_t* d_text = nullptr;
     uint32_t* d_sa = nullptr;
@@ -489,6 +507,7 @@ int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, con
         (void)hipGetLastError();
         return set_err(SA_E_NOMEM, "device allocation of text/SA failed");
     }
+    SA_TRACE("text/sa allocated");
     hipStream_t s = nullptr;
     hipEvent_t e0, e1;
     hipEventCreate(&e0);

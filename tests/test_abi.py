@@ -46,7 +46,8 @@ def test_library_loads_and_reports(sa_lib):
 
 def test_code_object_targets_gfx950(sa_lib):
     data = open(sa_lib.LIB_PATH, "rb").read()
-    assert b"gfx950" in data
+    assert b"amdgcn-amd-amdhsa--gfx950" in data
+    assert b"amdgcn-amd-amdhsa--gfx906" not in data
 
 
 def test_struct_layout(sa_lib):
