@@ -87,9 +87,9 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
 
 def pmc_traffic() -> dict | None:
     """Per-launch HBM traffic of the dominant kernel from the committed
-    rocprofv3 PMC summary (profiles/*pmc*.json, written by
-    profiles/collect_pmc.py), or None."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json")))
+    rocprofv3 PMC summary (profiles/<tag>_summary.json, written by
+    profiles/collect.sh + summarize.py), or None."""
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
     if not paths:
         return None
     try:

@@ -1,0 +1,21 @@
+#!/bin/bash
+# Run on the GPU box (via gpurun) from the repo root:
+#   bash profiles/collect.sh <tag> [bench args...]
+# 1. kernel trace + stats of the bench command (per-kernel average durations)
+# 2. FETCH_SIZE pass, 3. WRITE_SIZE pass (separate --pmc passes: on gfx950
+#    FETCH_SIZE takes 3 of the 4 TCC counter slots, WRITE_SIZE 2)
+# then profiles/summarize.py writes profiles/<tag>_summary.json and copies the
+# stats CSV into profiles/.
+set -euo pipefail
+tag=${1:?tag}; shift
+args=("$@")
+out=gpurun_out/prof_$tag
+mkdir -p "$out"
+export TMPDIR=/tmp
+timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o trace -- \
+    python3 bench.py --no-cpu-baseline --json-out "$out/bench.json" "${args[@]}" > "$out/trace.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o fetch -- \
+    python3 bench.py --no-cpu-baseline --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/fetch.log" 2>&1
+timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o write -- \
+    python3 bench.py --no-cpu-baseline --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/write.log" 2>&1
+python3 profiles/summarize.py "$tag" "$out" "${args[@]}"

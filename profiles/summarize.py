@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""Summarise a profiles/collect.sh run into profiles/<tag>_summary.json.
+
+Per kernel kind: calls, average duration (rocprofv3 kernel trace), FETCH_SIZE
+and WRITE_SIZE per launch (rocprofv3 --pmc, KiB -> bytes), and HBM traffic
+per launch corrected as MI355X_MICROARCH.md section HBM prescribes: on gfx950
+FETCH_SIZE under-reads wide coalesced streams (x2 for 16-B/lane reads) and
+other access widths must be calibrated on a known byte count.  The read
+calibration here is k_hist<SrcKeys>, which reads exactly 8 bytes per suffix
+(its u64 keys) and writes 1 KiB of counts: read_factor = 8n / FETCH bytes.
+WRITE_SIZE is reported as measured (exact for 16-B/lane streaming stores per
+the guide; the scatter's 8-B / 4-B run stores are uncalibrated).
+"""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcKeys>", "hist_keys"),
+         ("k_scan_rows", "scan"), ("k_scatter<sa::SrcRank>", "scatter_rank"),
+         ("k_scatter<sa::SrcKeys>", "scatter_keys"), ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
+         ("k_rerank", "rerank"), ("k_gen_text", "gen_text"), ("k_check_isa", "check_isa"),
+         ("k_check_pairs", "check_pairs"), ("k_fill_u32", "fill")]
+
+
+def kind_of(name):
+    for key, k in KINDS:
+        if key in name:
+            return k
+    return None
+
+
+def find(d, suffix):
+    hits = sorted(glob.glob(os.path.join(d, "**", f"*{suffix}"), recursive=True))
+    return hits[-1] if hits else None
+
+
+def main():
+    tag, out = sys.argv[1], sys.argv[2]
+    args = sys.argv[3:]
+    n = 1 << 30
+    kind = "dna"
+    for i, a in enumerate(args):
+        if a == "--n":
+            n = int(args[i + 1])
+        if a == "--kind":
+            kind = args[i + 1]
+    stats_csv = find(os.path.join(out, "trace"), "kernel_stats.csv")
+    trace_csv = find(os.path.join(out, "trace"), "kernel_trace.csv")
+    per = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
+    if trace_csv:
+        with open(trace_csv) as f:
+            for row in csv.DictReader(f):
+                k = kind_of(row.get("Kernel_Name", ""))
+                if k:
+                    per[k]["calls"] += 1
+                    per[k]["total_ns"] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+    pmc = {}
+    for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
+        c = find(os.path.join(out, sub), "counter_collection.csv")
+        acc = defaultdict(lambda: [0.0, 0])
+        if c:
+            with open(c) as f:
+                for row in csv.DictReader(f):
+                    if row.get("Counter_Name") != name:
+                        continue
+                    k = kind_of(row.get("Kernel_Name", ""))
+                    if k:
+                        acc[k][0] += float(row["Counter_Value"]) * 1024.0   # KiB -> bytes
+                        acc[k][1] += 1
+        pmc[name] = {k: v[0] / v[1] for k, v in acc.items() if v[1]}
+    fetch, write = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
+    read_factor = None
+    if fetch.get("hist_keys"):
+        read_factor = 8.0 * n / fetch["hist_keys"]
+    kernels = {}
+    for k, v in per.items():
+        e = {"calls": v["calls"], "avg_ms": v["total_ns"] / max(v["calls"], 1) / 1e6,
+             "total_ms": v["total_ns"] / 1e6}
+        if k in fetch:
+            e["fetch_bytes_raw"] = fetch[k]
+        if k in write:
+            e["write_bytes_raw"] = write[k]
+        if k in fetch and k in write:
+            rf = read_factor if read_factor else 2.0
+            e["traffic_bytes_corrected"] = fetch[k] * rf + write[k]
+        kernels[k] = e
+    bench = None
+    bj = os.path.join(out, "bench.json")
+    if os.path.exists(bj):
+        with open(bj) as f:
+            bench = json.loads(f.read())
+    summary = {
+        "tag": tag, "n": n, "kind": kind, "args": args,
+        "read_calibration": {"kernel": "hist_keys", "known_read_bytes": 8 * n, "factor": read_factor},
+        "kernels": kernels,
+        "traffic_bytes_per_launch": {"k_scatter_keys": kernels.get("scatter_keys", {}).get("traffic_bytes_corrected")},
+        "bench": bench,
+    }
+    here = os.path.dirname(os.path.abspath(__file__))
+    with open(os.path.join(here, f"{tag}_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+    if stats_csv:
+        shutil.copy(stats_csv, os.path.join(here, f"{tag}_kernel_stats.csv"))
+    print(json.dumps({k: {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()}
+                      for k, v in kernels.items()}, indent=1))
+
+
+if __name__ == "__main__":
+    main()
