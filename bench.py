@@ -54,6 +54,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample-n", type=int, default=1 << 25)
     ap.add_argument("--no-profile", action="store_true", help="no per-launch HIP events")
+    ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
+    ap.add_argument("--init-chars", type=int, default=0)
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -128,8 +130,9 @@ def main():
     torch.cuda.synchronize(dev)
 
     profile = not a.no_profile
+    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars)
     for _ in range(a.warmup):
-        b.build(d_text, n, d_sa, stream=sptr, profile=profile)
+        b.build(d_text, n, d_sa, **bkw)
 
     def barrier():
         if world > 1:
@@ -140,7 +143,7 @@ def main():
     t0 = time.perf_counter()
     stats = []
     for _ in range(a.steps):
-        stats.append(b.build(d_text, n, d_sa, stream=sptr, profile=profile))
+        stats.append(b.build(d_text, n, d_sa, **bkw))
     torch.cuda.synchronize(dev)
     barrier()
     elapsed = time.perf_counter() - t0
@@ -195,6 +198,11 @@ def main():
         "rounds": rounds,
         "distinct_per_round": stats[-1]["distinct"],
         "passes_per_round": stats[-1]["passes"],
+        "sorted_per_round": stats[-1]["sorted_n"],
+        "prefix_len_per_round": stats[-1]["prefix_len"],
+        "schedule": stats[-1]["schedule"],
+        "init_chars": stats[-1]["init_chars"],
+        "sigma": stats[-1]["sigma"],
         "model_bytes": stats[-1]["model_bytes"],
         "model_frac_of_hbm_peak": round(stats[-1]["model_bytes"] / (ms_per_step / 1e3) / 8e12, 4),
         "verified": verified,

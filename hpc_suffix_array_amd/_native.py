@@ -16,8 +16,10 @@ LIB_PATH = os.path.join(PKG_DIR, "lib", "libsa_hip.so")
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 SA_MAX_ROUNDS = 64
-KERNEL_KINDS = ["init", "hist_rank", "hist_keys", "scan", "scatter_rank", "scatter_keys",
-                "heads", "heads_scan", "rerank"]
+KERNEL_KINDS = ["init", "hist_first", "hist_keys", "scan", "scatter_first", "scatter_keys",
+                "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet"]
+SCHEDULE_PACKED = 0
+SCHEDULE_REFERENCE = 1
 SA_K_COUNT = len(KERNEL_KINDS)
 
 # every symbol include/*.h declares
@@ -25,7 +27,7 @@ DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_a
                   "build_lcp_array", "find_longest_repeated_substring", "is_valid_suffix_array"]
 EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", "sa_build_device",
                "sa_build_ex", "sa_check_device", "sa_check", "sa_generate_text_device",
-               "sa_last_error", "sa_device_count", "sa_version"]
+               "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
 
 
 class SAError(RuntimeError):
@@ -33,7 +35,8 @@ class SAError(RuntimeError):
 
 
 class SaOpts(ctypes.Structure):
-    _fields_ = [("profile", ctypes.c_int32), ("reserved", ctypes.c_int32 * 7)]
+    _fields_ = [("profile", ctypes.c_int32), ("schedule", ctypes.c_int32), ("init_chars", ctypes.c_int32),
+                ("reserved", ctypes.c_int32 * 5)]
 
 
 class SaStats(ctypes.Structure):
@@ -46,6 +49,12 @@ class SaStats(ctypes.Structure):
         ("round_ms", ctypes.c_double * SA_MAX_ROUNDS),
         ("distinct", ctypes.c_uint64 * SA_MAX_ROUNDS),
         ("passes", ctypes.c_int32 * SA_MAX_ROUNDS),
+        ("sorted_n", ctypes.c_uint64 * SA_MAX_ROUNDS),
+        ("prefix_len", ctypes.c_uint64 * SA_MAX_ROUNDS),
+        ("schedule", ctypes.c_int32),
+        ("init_chars", ctypes.c_int32),
+        ("sigma", ctypes.c_int32),
+        ("pad0", ctypes.c_int32),
         ("model_bytes", ctypes.c_uint64),
         ("kern_ms", ctypes.c_double * SA_K_COUNT),
         ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
@@ -62,6 +71,11 @@ class SaStats(ctypes.Structure):
             "round_ms": list(self.round_ms[:r]),
             "distinct": [int(x) for x in self.distinct[:r]],
             "passes": list(self.passes[:r]),
+            "sorted_n": [int(x) for x in self.sorted_n[:r]],
+            "prefix_len": [int(x) for x in self.prefix_len[:r]],
+            "schedule": "reference" if self.schedule == SCHEDULE_REFERENCE else "packed",
+            "init_chars": self.init_chars,
+            "sigma": self.sigma,
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

@@ -30,18 +30,27 @@ def _as_bytes_array(text) -> np.ndarray:
     return np.ascontiguousarray(text, dtype=np.uint8)
 
 
-def _opts(profile: bool) -> N.SaOpts:
+SCHEDULES = {"packed": N.SCHEDULE_PACKED, "reference": N.SCHEDULE_REFERENCE}
+
+
+def _opts(profile: bool = False, schedule: str = "packed", init_chars: int = 0) -> N.SaOpts:
     o = N.SaOpts()
     o.profile = 1 if profile else 0
+    o.schedule = SCHEDULES[schedule]
+    o.init_chars = int(init_chars)
     return o
 
 
-def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False):
+def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False,
+                       schedule: str = "packed", init_chars: int = 0):
     """Suffix array of ``text`` (bytes / uint8 array), built on the GPU.
 
     Unsigned-byte order, end of string smallest (== the reference's order on
     its valid domain, manber_myers.c:81-133).  Returns uint32 (width 4) or
-    int64 (width 8); with ``return_stats`` also the per-round statistics."""
+    int64 (width 8); with ``return_stats`` also the per-round statistics.
+    ``schedule``: "packed" (default; packed K-symbol first round, later rounds
+    re-sort unsorted groups only) or "reference" (h = 1, 2, 4, ... over all
+    n suffixes, round for round as manber_myers.c:94-125)."""
     t = _as_bytes_array(text)
     n = int(t.size)
     N.require_device()
@@ -49,7 +58,7 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     st = N.SaStats()
     L = N.lib()
     N.check(L.sa_build_ex(t.ctypes.data if n else None, n, out.ctypes.data, width,
-                          ctypes.byref(_opts(profile)), ctypes.byref(st)), "sa_build_ex")
+                          ctypes.byref(_opts(profile, schedule, init_chars)), ctypes.byref(st)), "sa_build_ex")
     out = out[:n]
     return (out, st.to_dict()) if return_stats else out
 
@@ -155,12 +164,14 @@ class DeviceBuilder:
     def _ptr(x) -> int:
         return x if isinstance(x, int) else int(x.data_ptr())
 
-    def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False) -> dict:
+    def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False, schedule: str = "packed",
+              init_chars: int = 0) -> dict:
         """Build the SA of the n bytes at d_text into the n uint32 at d_sa."""
         st = N.SaStats()
         s = None if stream is None else ctypes.c_void_p(int(stream))
         N.check(self.L.sa_build_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s,
-                                       ctypes.byref(_opts(profile)), ctypes.byref(st)), "sa_build_device")
+                                       ctypes.byref(_opts(profile, schedule, init_chars)), ctypes.byref(st)),
+                "sa_build_device")
         return st.to_dict()
 
     def generate_text(self, d_out, n: int, alphabet: bytes, seed: int = 1, stream=None) -> None:

@@ -86,25 +86,33 @@ static Chunking plan_chunks(uint64_t n) {
 
 struct sa_context {
     int device = 0;
-    uint64_t cap = 0;
+    uint64_t cap = 0;      // rank / keys / vals_alt capacity (symbols)
+    uint64_t ucap = 0;     // unsorted-set buffers capacity
     uint32_t* rank = nullptr;
     uint64_t* keys[2] = {nullptr, nullptr};
     uint32_t* vals_alt = nullptr;
+    uint32_t* vals_u = nullptr;                 // sorted idx of an unsorted-set round
+    uint32_t* u_pos[2] = {nullptr, nullptr};    // compacted unsorted set, ping-pong
+    uint32_t* u_idx[2] = {nullptr, nullptr};
+    uint32_t* u_g[2] = {nullptr, nullptr};
     uint32_t* hist = nullptr;      // 256 * kMaxChunks
     uint32_t* totals = nullptr;    // 256
-    uint32_t* counts = nullptr;    // kMaxChunks
-    uint32_t* words = nullptr;     // [0] = D, [1] = check error flags
-    uint32_t* host_words = nullptr;  // pinned mirror
+    uint32_t* counts = nullptr;    // 4 * kMaxChunks (heads, u, uheads, last)
+    uint32_t* words = nullptr;     // [0..2] = D, m, G; [3] = check error flags
+    uint32_t* alpha = nullptr;     // 256 byte counts
+    uint16_t* code = nullptr;      // 256 byte -> dense code 1..sigma
+    uint32_t* host_words = nullptr;  // pinned: 64 words, 256 counts, 128 words of codes
     hipEvent_t ev[sa::kEvPool];
     int ev_ready = 0;
 };
 
 namespace sa {
 
-// Device memory a context holds for n symbols (rank + 2 key + 1 index buffer).
+// Device memory a context holds for n symbols: rank + 2 key + 1 index buffer
+// (the reference schedule), plus 7 u32 arrays for the unsorted set (packed).
 static uint64_t ws_bytes(uint64_t n) {
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
-    return m * 4 + 2 * m * 8 + m * 4 + (uint64_t)kRadix * kMaxChunks * 4 + 4096;
+    return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
 }
 
 static void free_ctx_buffers(sa_context* c) {
@@ -116,6 +124,18 @@ static void free_ctx_buffers(sa_context* c) {
     c->keys[0] = c->keys[1] = nullptr;
     c->vals_alt = nullptr;
     c->cap = 0;
+}
+
+static void free_u_buffers(sa_context* c) {
+    hipFree(c->vals_u);
+    c->vals_u = nullptr;
+    for (int i = 0; i < 2; ++i) {
+        hipFree(c->u_pos[i]);
+        hipFree(c->u_idx[i]);
+        hipFree(c->u_g[i]);
+        c->u_pos[i] = c->u_idx[i] = c->u_g[i] = nullptr;
+    }
+    c->ucap = 0;
 }
 
 static int ensure_capacity(sa_context* c, uint64_t n) {
@@ -134,14 +154,32 @@ static int ensure_capacity(sa_context* c, uint64_t n) {
     return SA_OK;
 }
 
+static int ensure_u_capacity(sa_context* c, uint64_t n) {
+    if (n <= c->ucap && c->vals_u) return SA_OK;
+    SA_HIP(hipSetDevice(c->device));
+    free_u_buffers(c);
+    const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64) * 4;
+    bool ok = hipMalloc(&c->vals_u, m) == hipSuccess;
+    for (int i = 0; i < 2 && ok; ++i)
+        ok = hipMalloc(&c->u_pos[i], m) == hipSuccess && hipMalloc(&c->u_idx[i], m) == hipSuccess &&
+             hipMalloc(&c->u_g[i], m) == hipSuccess;
+    if (!ok) {
+        free_u_buffers(c);
+        (void)hipGetLastError();
+        return set_err(SA_E_NOMEM, "device allocation of the unsorted-set buffers failed");
+    }
+    c->ucap = n;
+    return SA_OK;
+}
+
 // Per-launch HIP-event timing, enabled by sa_opts.profile.
 struct Timer {
     sa_context* c;
     hipStream_t s;
     bool on;
+    sa_stats* st;
     int used = 0;
     int kind[kEvPool / 2];
-    sa_stats* st;
     void begin(int k) {
         if (!on) return;
         if (used >= kEvPool / 2) flush();
@@ -167,6 +205,26 @@ struct Timer {
         used = 0;
     }
 };
+
+// owned HIP events (destroyed on every return path)
+struct Events {
+    hipEvent_t e[3] = {nullptr, nullptr, nullptr};
+    int make() {
+        for (auto& x : e)
+            if (hipEventCreate(&x) != hipSuccess) return set_err(SA_E_HIP, "hipEventCreate failed");
+        return SA_OK;
+    }
+    ~Events() {
+        for (auto& x : e)
+            if (x) hipEventDestroy(x);
+    }
+};
+
+static float elapsed(hipEvent_t a, hipEvent_t b) {
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, a, b);
+    return ms;
+}
 
 static void add_bytes(sa_stats* st, int kind, uint64_t b) {
     if (st) st->kern_bytes[kind] += b;
@@ -195,124 +253,309 @@ static int radix_pass(sa_context* c, const Src& src, const Chunking& ch, uint32_
     return SA_OK;
 }
 
+// Stable LSD sort of ch.n (key, idx) pairs over key bits [0, bits): the first
+// pass generates pairs from `first`, later passes read the ping-pong buffers.
+// The sorted idx land in vals_final; *kbuf = index of the sorted key buffer.
+template <class Src>
+static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, const Chunking& ch, uint32_t bits,
+                      uint32_t* vals_final, uint32_t* vals_other, hipStream_t s, Timer& tm, sa_stats* st,
+                      int* kbuf, uint32_t* passes) {
+    const uint32_t P = (bits + 7) / 8;
+    uint32_t* vb[2];
+    vb[(P - 1) & 1] = vals_final;
+    vb[P & 1] = vals_other;
+    for (uint32_t p = 0; p < P; ++p) {
+        const uint32_t shift = 8 * p;
+        const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
+        int rc;
+        if (p == 0) {
+            rc = radix_pass(c, first, ch, shift, nbits, c->keys[0], vb[0], s, tm, st, SA_K_HIST_FIRST,
+                            SA_K_SCATTER_FIRST, first_bytes);
+        } else {
+            SrcKeys src{c->keys[(p - 1) & 1], vb[(p - 1) & 1]};
+            rc = radix_pass(c, src, ch, shift, nbits, c->keys[p & 1], vb[p & 1], s, tm, st, SA_K_HIST_KEYS,
+                            SA_K_SCATTER_KEYS, 12 * ch.n);
+        }
+        if (rc) return rc;
+    }
+    *kbuf = (int)((P - 1) & 1);
+    *passes = P;
+    return SA_OK;
+}
+
+static void record_round(sa_stats* st, float ms, uint64_t D, uint32_t P, uint64_t sorted_n, uint64_t h) {
+    if (!st) return;
+    const int r = st->rounds;
+    if (r < SA_MAX_ROUNDS) {
+        st->round_ms[r] = ms;
+        st->distinct[r] = D;
+        st->passes[r] = (int32_t)P;
+        st->sorted_n[r] = sorted_n;
+        st->prefix_len[r] = h;
+    }
+    // B_j = n_j (3 rb + 2 S (P_j + 1)), rb = 4, S = 12
+    st->model_bytes += sorted_n * (3ull * 4 + 2ull * 12 * (P + 1));
+    st->rounds++;
+}
+
+// ---------------------------------------------------------------------------
+// reference schedule: manber_myers.c:88-125 round for round
+// ---------------------------------------------------------------------------
+static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
+                           sa_stats* st, Timer& tm) {
+    Events ev;
+    int rc = ev.make();
+    if (rc) return rc;
+    const Chunking ch = plan_chunks(n);
+    tm.begin(SA_K_INIT);
+    {
+        const uint64_t grid = std::min<uint64_t>((n + kBlock * 4 - 1) / (kBlock * 4), 4096);
+        hipLaunchKernelGGL(k_init_rank, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n, c->rank);
+    }
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_INIT, 5 * n);
+
+    uint64_t D = 256;   // manber_myers.c:94
+    for (uint64_t h = 1;; h *= 2) {
+        SA_HIP(hipEventRecord(ev.e[0], s));
+        const uint32_t w = bit_width(D);          // ranks are 0..D
+        SA_TRACE("reference round h=%llu D=%llu w=%u", (unsigned long long)h, (unsigned long long)D, w);
+        SrcRank src{c->rank, n, h, w};
+        int kb;
+        uint32_t P;
+        rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, s, tm, st, &kb, &P);
+        if (rc) return rc;
+        const uint64_t* sorted = c->keys[kb];
+        tm.begin(SA_K_HEADS);
+        hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts);
+        tm.end();
+        tm.begin(SA_K_HEADS_SCAN);
+        hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, c->counts, ch.chunks, c->words);
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_HEADS, 8 * n);
+        add_bytes(st, SA_K_HEADS_SCAN, 8ull * ch.chunks);
+        SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipStreamSynchronize(s));
+        const uint64_t Dn = c->host_words[0];
+        const bool done = (Dn == n);                  // manber_myers.c:113
+        if (!done) {
+            tm.begin(SA_K_RERANK);
+            hipLaunchKernelGGL(k_rerank, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, (const uint32_t*)d_sa, ch,
+                               (const uint32_t*)c->counts, c->rank);
+            tm.end();
+            SA_HIP(hipGetLastError());
+            add_bytes(st, SA_K_RERANK, 16 * n);
+        }
+        SA_HIP(hipEventRecord(ev.e[1], s));
+        SA_HIP(hipEventSynchronize(ev.e[1]));
+        tm.flush();
+        record_round(st, elapsed(ev.e[0], ev.e[1]), Dn, P, n, 2 * h);
+        if (Dn > n || Dn == 0)
+            return set_err(SA_E_INTERNAL, "distinct count %llu out of range", (unsigned long long)Dn);
+        if (done) break;
+        if (h > n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)", (unsigned long long)h);
+        D = Dn;
+    }
+    return SA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// packed schedule
+// ---------------------------------------------------------------------------
+// K for base B: largest K with B^K - 1 < 2^64
+static uint32_t max_chars(uint64_t base) {
+    uint32_t K = 0;
+    uint64_t prod = 1;
+    while (prod <= UINT64_MAX / base) {
+        prod *= base;
+        ++K;
+    }
+    return K;
+}
+
+static uint32_t key_bits(uint64_t base, uint32_t K) {   // bit width of B^K - 1
+    unsigned __int128 p = 1;
+    for (uint32_t t = 0; t < K; ++t) p *= base;
+    p -= 1;
+    uint32_t w = 0;
+    while (p) { ++w; p >>= 1; }
+    return w;
+}
+
+// auto K: enough symbols that a random text of this alphabet leaves few
+// unsorted suffixes (sigma^K >= 512 n), rounded up to fill the radix passes.
+static uint32_t choose_chars(uint32_t sigma, uint64_t n, int32_t req) {
+    const uint64_t base = (uint64_t)sigma + 1;
+    const uint32_t kmax = max_chars(base);
+    if (req > 0) return std::min<uint32_t>((uint32_t)req, kmax);
+    if (sigma <= 1) return kmax;
+    uint32_t kmin = 1;
+    {
+        unsigned __int128 p = sigma, target = (unsigned __int128)n * 512u;
+        while (p < target && kmin < kmax) {
+            p *= sigma;
+            ++kmin;
+        }
+    }
+    const uint32_t P = (key_bits(base, kmin) + 7) / 8;
+    uint32_t K = kmin;
+    while (K + 1 <= kmax && key_bits(base, K + 1) <= 8 * P) ++K;
+    return K;
+}
+
+template <class Pos>
+static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
+                    uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
+                    uint64_t* G) {
+    uint32_t* c_h = c->counts;
+    uint32_t* c_u = c->counts + kMaxChunks;
+    uint32_t* c_uh = c->counts + 2 * kMaxChunks;
+    uint32_t* c_l = c->counts + 3 * kMaxChunks;
+    tm.begin(SA_K_SEG_COUNT);
+    hipLaunchKernelGGL(k_seg_count, dim3(ch.chunks), dim3(kBlock), 0, s, keys, ch, c_h, c_u, c_uh, c_l);
+    tm.end();
+    tm.begin(SA_K_SEG_SCAN);
+    hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(kBlock), 0, s, c_h, c_u, c_uh, c_l, ch.chunks, c->words);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 12, hipMemcpyDeviceToHost, s));
+    tm.begin(SA_K_SEG_WRITE);
+    hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
+                       (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, c->rank, sa,
+                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo]);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipStreamSynchronize(s));
+    *D = c->host_words[0];
+    *m = c->host_words[1];
+    *G = c->host_words[2];
+    add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);
+    add_bytes(st, SA_K_SEG_SCAN, 32ull * ch.chunks);
+    add_bytes(st, SA_K_SEG_WRITE, ch.n * (8 + 4 + 4 + (sa ? 8 : 0)) + *m * 12);
+    return SA_OK;
+}
+
+static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
+                        const sa_opts* opts, sa_stats* st, Timer& tm) {
+    Events ev;
+    int rc = ev.make();
+    if (rc) return rc;
+    rc = ensure_u_capacity(c, n);
+    if (rc) return rc;
+    SA_HIP(hipEventRecord(ev.e[0], s));
+    // alphabet -> dense codes (host reads 256 counts)
+    uint32_t* h_alpha = c->host_words + 64;
+    uint16_t* h_code = reinterpret_cast<uint16_t*>(c->host_words + 320);
+    SA_HIP(hipMemsetAsync(c->alpha, 0, 256 * 4, s));
+    tm.begin(SA_K_ALPHABET);
+    {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 1024);
+        hipLaunchKernelGGL(k_byte_hist, dim3(grid), dim3(kBlock), 0, s, d_text, n, c->alpha);
+    }
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_ALPHABET, n);
+    SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 256 * 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    uint32_t sigma = 0;
+    for (int b = 0; b < 256; ++b) h_code[b] = h_alpha[b] ? (uint16_t)(++sigma) : 0;
+    SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
+    const uint32_t K = choose_chars(sigma, n, opts ? opts->init_chars : 0);
+    const uint64_t base = (uint64_t)sigma + 1;
+    const uint32_t bits1 = key_bits(base, K);
+    if (st) {
+        st->init_chars = (int32_t)K;
+        st->sigma = (int32_t)sigma;
+    }
+    SA_TRACE("packed: sigma=%u K=%u bits=%u", sigma, K, bits1);
+
+    // round 1: sort the packed K-prefix of every suffix
+    const Chunking ch = plan_chunks(n);
+    SrcText src{d_text, c->code, n, base, K};
+    int kb;
+    uint32_t P;
+    rc = radix_sort(c, src, n, ch, bits1, d_sa, c->vals_alt, s, tm, st, &kb, &P);
+    if (rc) return rc;
+    uint64_t D, m, G;
+    int uo = 0;
+    rc = segments(c, c->keys[kb], d_sa, ch, PosIdentity{}, nullptr, uo, s, tm, st, &D, &m, &G);
+    if (rc) return rc;
+    SA_HIP(hipEventRecord(ev.e[1], s));
+    SA_HIP(hipEventSynchronize(ev.e[1]));
+    tm.flush();
+    record_round(st, elapsed(ev.e[0], ev.e[1]), D, P, n, K);
+    SA_TRACE("  round 1: D=%llu unsorted=%llu groups=%llu", (unsigned long long)D, (unsigned long long)m,
+             (unsigned long long)G);
+
+    // doubling rounds over the unsorted set only
+    const uint32_t wr = bit_width(n);   // rank values 0..n
+    for (uint64_t h = K; m > 0; h *= 2) {
+        if (h >= 2 * n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)", (unsigned long long)h);
+        SA_HIP(hipEventRecord(ev.e[0], s));
+        const uint32_t wg = G > 1 ? bit_width(G - 1) : 0;
+        const uint32_t bits = wg + wr;
+        if (bits > 64) return set_err(SA_E_INTERNAL, "key of %u bits", bits);
+        const Chunking cu = plan_chunks(m);
+        const int ui = uo;
+        uo ^= 1;
+        SrcU su{c->u_idx[ui], c->u_g[ui], c->rank, n, h, wr};
+        rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, s, tm, st, &kb, &P);
+        if (rc) return rc;
+        uint64_t Du, m2, G2;
+        rc = segments(c, c->keys[kb], c->vals_u, cu, PosArray{c->u_pos[ui]}, d_sa, uo, s, tm, st, &Du, &m2, &G2);
+        if (rc) return rc;
+        SA_HIP(hipEventRecord(ev.e[1], s));
+        SA_HIP(hipEventSynchronize(ev.e[1]));
+        tm.flush();
+        D = (n - m) + Du;
+        record_round(st, elapsed(ev.e[0], ev.e[1]), D, P, m, 2 * h);
+        SA_TRACE("  round h=%llu: sorted %llu, D=%llu unsorted=%llu groups=%llu", (unsigned long long)h,
+                 (unsigned long long)m, (unsigned long long)D, (unsigned long long)m2, (unsigned long long)G2);
+        m = m2;
+        G = G2;
+    }
+    if (D != n) return set_err(SA_E_INTERNAL, "finished with %llu groups for n=%llu", (unsigned long long)D,
+                               (unsigned long long)n);
+    return SA_OK;
+}
+
 static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                         const sa_opts* opts, sa_stats* st) {
     if (st) {
         std::memset(st, 0, sizeof *st);
         st->n_kinds = SA_K_COUNT;
     }
+    const int schedule = opts ? opts->schedule : SA_SCHEDULE_PACKED;
+    if (st) st->schedule = schedule;
     if (n == 0) return SA_OK;
     if (!d_text || !d_sa) return set_err(SA_E_INVALID, "NULL device pointer");
     if (n > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "n = %llu exceeds 2^32-1 on one device",
                                           (unsigned long long)n);
+    if (schedule != SA_SCHEDULE_PACKED && schedule != SA_SCHEDULE_REFERENCE)
+        return set_err(SA_E_INVALID, "unknown schedule %d", schedule);
     SA_HIP(hipSetDevice(c->device));
     int rc = ensure_capacity(c, n);
     if (rc) return rc;
-    Timer tm{c, s, opts && opts->profile, 0, {}, st};
-
-    // round / whole-build events (the pool's events are reserved for Timer)
-    hipEvent_t r0, r1, start_all;
-    SA_HIP(hipEventCreate(&r0));
-    SA_HIP(hipEventCreate(&r1));
-    SA_HIP(hipEventCreate(&start_all));
-    SA_HIP(hipEventRecord(start_all, s));
-
-    SA_TRACE("build n=%llu", (unsigned long long)n);
+    Timer tm{c, s, opts && opts->profile, st};
+    Events ev;
+    rc = ev.make();
+    if (rc) return rc;
+    SA_TRACE("build n=%llu schedule=%d", (unsigned long long)n, schedule);
+    SA_HIP(hipEventRecord(ev.e[0], s));
     if (n == 1) {
         SA_HIP(hipMemsetAsync(d_sa, 0, 4, s));
+    } else if (schedule == SA_SCHEDULE_REFERENCE) {
+        rc = build_reference(c, d_text, n, d_sa, s, st, tm);
     } else {
-        const Chunking ch = plan_chunks(n);
-        tm.begin(SA_K_INIT);
-        {
-            const uint64_t grid = std::min<uint64_t>((n + kBlock * 4 - 1) / (kBlock * 4), 4096);
-            hipLaunchKernelGGL(k_init_rank, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n, c->rank);
-        }
-        tm.end();
-        SA_HIP(hipGetLastError());
-        add_bytes(st, SA_K_INIT, 5 * n);
-
-        uint64_t D = 256;   // manber_myers.c:94
-        for (uint64_t h = 1;; h *= 2) {
-            const int round = st ? st->rounds : 0;
-            SA_HIP(hipEventRecord(r0, s));
-            const uint32_t w = bit_width(D);          // ranks are 0..D
-            const uint32_t bits = 2 * w;
-            const uint32_t P = (bits + 7) / 8;
-            SA_TRACE("round h=%llu D=%llu w=%u P=%u chunks=%u tpc=%u", (unsigned long long)h,
-                     (unsigned long long)D, w, P, ch.chunks, ch.tiles_per_chunk);
-            // index buffers: pass p writes bufs[p & 1]; make pass P-1 write d_sa
-            uint32_t* vb[2];
-            vb[(P - 1) & 1] = d_sa;
-            vb[P & 1] = c->vals_alt;
-            for (uint32_t p = 0; p < P; ++p) {
-                const uint32_t shift = 8 * p;
-                const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
-                uint64_t* ok = c->keys[p & 1];
-                if (p == 0) {
-                    SrcRank src{c->rank, n, h, w};
-                    rc = radix_pass(c, src, ch, shift, nbits, ok, vb[0], s, tm, st, SA_K_HIST_RANK,
-                                    SA_K_SCATTER_RANK, 4 * n);
-                } else {
-                    SrcKeys src{c->keys[(p - 1) & 1], vb[(p - 1) & 1]};
-                    rc = radix_pass(c, src, ch, shift, nbits, ok, vb[p & 1], s, tm, st, SA_K_HIST_KEYS,
-                                    SA_K_SCATTER_KEYS, 12 * n);
-                }
-                if (rc) return rc;
-            }
-            const uint64_t* sorted = c->keys[(P - 1) & 1];
-            tm.begin(SA_K_HEADS);
-            hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts);
-            tm.end();
-            tm.begin(SA_K_HEADS_SCAN);
-            hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, c->counts, ch.chunks, c->words);
-            tm.end();
-            SA_HIP(hipGetLastError());
-            add_bytes(st, SA_K_HEADS, 8 * n);
-            add_bytes(st, SA_K_HEADS_SCAN, 8ull * ch.chunks);
-            SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4, hipMemcpyDeviceToHost, s));
-            SA_HIP(hipStreamSynchronize(s));
-            const uint64_t Dn = c->host_words[0];
-            SA_TRACE("  D'=%llu", (unsigned long long)Dn);
-            const bool done = (Dn == n);
-            if (!done) {
-                tm.begin(SA_K_RERANK);
-                hipLaunchKernelGGL(k_rerank, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, (const uint32_t*)d_sa,
-                                   ch, (const uint32_t*)c->counts, c->rank);
-                tm.end();
-                SA_HIP(hipGetLastError());
-                add_bytes(st, SA_K_RERANK, 16 * n);
-            }
-            SA_HIP(hipEventRecord(r1, s));
-            SA_HIP(hipEventSynchronize(r1));
-            tm.flush();
-            if (st && round < SA_MAX_ROUNDS) {
-                float ms = 0.f;
-                hipEventElapsedTime(&ms, r0, r1);
-                st->round_ms[round] = ms;
-                st->distinct[round] = Dn;
-                st->passes[round] = (int32_t)P;
-                // B_j = n (3 rb + 2 S (P_j + 1)), rb = 4, S = 12
-                st->model_bytes += n * (3ull * 4 + 2ull * 12 * (P + 1));
-            }
-            if (st) st->rounds++;
-            if (Dn > n || Dn == 0) return set_err(SA_E_INTERNAL, "distinct count %llu out of range",
-                                                 (unsigned long long)Dn);
-            if (done) break;
-            if (h > n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)",
-                                      (unsigned long long)h);
-            D = Dn;
-        }
+        rc = build_packed(c, d_text, n, d_sa, s, opts, st, tm);
     }
-    SA_HIP(hipEventRecord(r1, s));
-    SA_HIP(hipEventSynchronize(r1));
-    if (st) {
-        float ms = 0.f;
-        hipEventElapsedTime(&ms, start_all, r1);
-        st->total_ms = ms;
-    }
-    hipEventDestroy(start_all);
-    hipEventDestroy(r0);
-    hipEventDestroy(r1);
+    if (rc) return rc;
+    SA_HIP(hipEventRecord(ev.e[1], s));
+    SA_HIP(hipEventSynchronize(ev.e[1]));
+    tm.flush();
+    if (st) st->total_ms = elapsed(ev.e[0], ev.e[1]);
     return SA_OK;
 }
 
@@ -364,14 +607,14 @@ static int check_device(sa_context* c, const uint8_t* d_text, uint64_t n, const 
     uint32_t* isa = c->rank;
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192);
     hipLaunchKernelGGL(k_fill_u32, dim3(grid), dim3(kBlock), 0, s, isa, n, 0xFFFFFFFFu);
-    SA_HIP(hipMemsetAsync(c->words + 1, 0, 4, s));
-    hipLaunchKernelGGL(k_check_isa, dim3(grid), dim3(kBlock), 0, s, d_sa, n, isa, c->words + 1);
+    SA_HIP(hipMemsetAsync(c->words + 3, 0, 4, s));
+    hipLaunchKernelGGL(k_check_isa, dim3(grid), dim3(kBlock), 0, s, d_sa, n, isa, c->words + 3);
     hipLaunchKernelGGL(k_check_pairs, dim3(grid), dim3(kBlock), 0, s, d_text, d_sa, n, (const uint32_t*)isa,
-                       c->words + 1);
+                       c->words + 3);
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words + 1, c->words + 1, 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words + 3, c->words + 3, 4, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
-    return c->host_words[1] == 0 ? 1 : 0;
+    return c->host_words[3] == 0 ? 1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -437,9 +680,10 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
     sa_context* c = new sa_context();
     c->device = device;
     if (hipMalloc(&c->hist, (size_t)kRadix * kMaxChunks * 4) != hipSuccess ||
-        hipMalloc(&c->totals, kRadix * 4) != hipSuccess || hipMalloc(&c->counts, kMaxChunks * 4) != hipSuccess ||
-        hipMalloc(&c->words, 64) != hipSuccess ||
-        hipHostMalloc(&c->host_words, 64, hipHostMallocDefault) != hipSuccess) {
+        hipMalloc(&c->totals, kRadix * 4) != hipSuccess || hipMalloc(&c->counts, 4 * kMaxChunks * 4) != hipSuccess ||
+        hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
+        hipMalloc(&c->code, 256 * 2) != hipSuccess ||
+        hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);
         return set_err(SA_E_NOMEM, "context allocation failed");
@@ -466,6 +710,9 @@ void sa_context_destroy(sa_context* c) {
     if (!c) return;
     hipSetDevice(c->device);
     free_ctx_buffers(c);
+    free_u_buffers(c);
+    hipFree(c->alpha);
+    hipFree(c->code);
     hipFree(c->hist);
     hipFree(c->totals);
     hipFree(c->counts);

@@ -113,3 +113,7 @@ int is_valid_suffix_array(SuffixArray* sa) {
 }
 
 }  // extern "C"
+
+extern "C" uint64_t sa_struct_size(int which) {
+    return which == 0 ? sizeof(sa_stats) : which == 1 ? sizeof(sa_opts) : 0;
+}

@@ -59,6 +59,48 @@ struct SrcRank {
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
 };
 
+// Packed schedule, first round: key = the first K symbols of suffix i packed
+// base B = sigma + 1 (dense codes 1..sigma, 0 = past the end), so key order
+// is the lexicographic order of K-prefixes with the end smallest.  Replaces
+// rounds h = 1 .. K/2 of the reference loop (manber_myers.c:88-125) by one
+// sort.  B^K <= 2^64 is guaranteed by the host.
+struct SrcText {
+    const uint8_t* __restrict__ text;
+    const uint16_t* __restrict__ code;  // 256-entry byte -> dense code 1..sigma
+    uint64_t n;
+    uint64_t base;
+    uint32_t K;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const {
+        uint64_t x = 0;
+        if (e + K <= n) {
+            for (uint32_t t = 0; t < K; ++t) x = x * base + code[text[e + t]];
+        } else {
+            for (uint32_t t = 0; t < K; ++t) x = x * base + ((e + t < n) ? code[text[e + t]] : 0u);
+        }
+        return x;
+    }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
+};
+
+// Packed schedule, later rounds: only the suffixes whose group is not yet a
+// singleton (compacted in SA order: idx, dense group id g).  key =
+// (g << wr) | rank[idx + h]; rank is the group-head position + 1 (0 = past
+// the end), so sorting by key refines every group by its next h symbols.
+struct SrcU {
+    const uint32_t* __restrict__ u_idx;
+    const uint32_t* __restrict__ u_g;
+    const uint32_t* __restrict__ rank;
+    uint64_t n;
+    uint64_t h;
+    uint32_t wr;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const {
+        const uint64_t i = u_idx[e];
+        const uint64_t r1 = (i + h < n) ? rank[i + h] : 0u;
+        return ((uint64_t)u_g[e] << wr) | r1;
+    }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
+};
+
 // Later passes: the previous pass's output.
 struct SrcKeys {
     const uint64_t* __restrict__ keys;
@@ -415,6 +457,265 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
         run += ttot;
     }
     (void)s_tmp;
+}
+
+// ---------------------------------------------------------------------------
+// alphabet: 256-bin byte histogram (per-wave LDS bins, one global atomic per
+// bin per block).  The host turns it into dense codes 1..sigma.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_byte_hist(const uint8_t* __restrict__ text, uint64_t n,
+                                                      uint32_t* __restrict__ counts) {
+    __shared__ uint32_t s_h[kWaves][kRadix];
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_h[0][0])[i] = 0;
+    __syncthreads();
+    uint32_t* my = s_h[wave_id()];
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 16;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16; i < n; i += stride) {
+        if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int b = 0; b < 4; ++b) atomicAdd(&my[(w[q] >> (8 * b)) & 0xFFu], 1u);
+        } else {
+            for (uint64_t j = i; j < n && j < i + 16; ++j) atomicAdd(&my[text[j]], 1u);
+        }
+    }
+    __syncthreads();
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += s_h[w][threadIdx.x];
+    if (s) atomicAdd(&counts[threadIdx.x], s);
+}
+
+// ---------------------------------------------------------------------------
+// Segments of a sorted key sequence s = 0..m-1 (packed schedule).
+//   head(s)   key[s] != key[s-1]               (manber_myers.c:104-105)
+//   single(s) head(s) and head(s+1)            (group of size 1: final)
+//   inU(s)    !single(s)                       (still unsorted)
+//   uhead(s)  head(s) and inU(s)               (first member of an unsorted group)
+// pos(s) maps a sorted index to its SA position: identity in the first round,
+// the compacted position array in later rounds.
+// ---------------------------------------------------------------------------
+struct PosIdentity {
+    __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return (uint32_t)s; }
+};
+struct PosArray {
+    const uint32_t* __restrict__ p;
+    __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return p[s]; }
+};
+
+__device__ __forceinline__ void seg_masks(const uint64_t* __restrict__ keys, uint64_t s, uint64_t m,
+                                          uint64_t& mf, uint64_t& mu, uint64_t& muh) {
+    bool f = false, u = false;
+    if (s < m) {
+        const uint64_t k = keys[s];
+        f = (s == 0) || keys[s - 1] != k;
+        const bool nf = (s + 1 >= m) || keys[s + 1] != k;
+        u = !(f && nf);
+    }
+    mf = __ballot(f);
+    mu = __ballot(u);
+    muh = __ballot(f && u);
+}
+
+// per chunk: number of heads, unsorted members, unsorted groups, and
+// (last head index + 1) or 0.
+__global__ __launch_bounds__(kBlock) void k_seg_count(const uint64_t* __restrict__ keys, Chunking ch,
+                                                      uint32_t* __restrict__ c_heads, uint32_t* __restrict__ c_u,
+                                                      uint32_t* __restrict__ c_uh, uint32_t* __restrict__ c_last) {
+    __shared__ uint32_t s_v[4][kWaves];
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    uint32_t nh = 0, nu = 0, nuh = 0, last = 0;
+    for (uint64_t tb = e0; tb < e1; tb += kTile) {
+        const uint64_t w0 = tb + (uint64_t)wave_id() * kWaveTile;
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t rb = w0 + (uint64_t)j * kWave;
+            if (rb >= e1) break;
+            uint64_t mf, mu, muh;
+            // neighbours are compared across chunk borders (global m = ch.n);
+            // lanes past the chunk end are counted by the next chunk
+            seg_masks(keys, rb + lane_id(), ch.n, mf, mu, muh);
+            const uint64_t lim = e1 - rb >= 64 ? ~0ull : ((1ull << (e1 - rb)) - 1ull);
+            mf &= lim;
+            mu &= lim;
+            muh &= lim;
+            nh += __popcll(mf);
+            nu += __popcll(mu);
+            nuh += __popcll(muh);
+            if (mf) last = (uint32_t)(rb + 63 - __clzll(mf)) + 1u;
+        }
+    }
+    if (lane_id() == 0) {
+        s_v[0][wave_id()] = nh;
+        s_v[1][wave_id()] = nu;
+        s_v[2][wave_id()] = nuh;
+        s_v[3][wave_id()] = last;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t a = 0, b = 0, d = 0, l = 0;
+        for (int w = 0; w < kWaves; ++w) {
+            a += s_v[0][w];
+            b += s_v[1][w];
+            d += s_v[2][w];
+            l = s_v[3][w] > l ? s_v[3][w] : l;
+        }
+        c_heads[c] = a;
+        c_u[c] = b;
+        c_uh[c] = d;
+        c_last[c] = l;
+    }
+}
+
+// exclusive sums of c_heads/c_u/c_uh and exclusive max of c_last over the
+// chunks (one workgroup; chunks <= a few thousand); totals -> words[0..2].
+__global__ __launch_bounds__(kBlock) void k_seg_scan(uint32_t* __restrict__ c_heads, uint32_t* __restrict__ c_u,
+                                                     uint32_t* __restrict__ c_uh, uint32_t* __restrict__ c_last,
+                                                     uint32_t chunks, uint32_t* __restrict__ words) {
+    __shared__ uint32_t s_tmp[kWaves];
+    __shared__ uint32_t s_max[kBlock];
+    uint32_t* arr[3] = {c_heads, c_u, c_uh};
+    for (int a = 0; a < 3; ++a) {
+        uint32_t carry = 0;
+        for (uint32_t base = 0; base < chunks; base += kBlock * 4) {
+            uint32_t v[4], sum = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t i = base + threadIdx.x * 4 + j;
+                v[j] = (i < chunks) ? arr[a][i] : 0u;
+                sum += v[j];
+            }
+            uint32_t tot;
+            uint32_t off = block_exclusive_sum(sum, s_tmp, &tot) + carry;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t i = base + threadIdx.x * 4 + j;
+                if (i < chunks) arr[a][i] = off;
+                off += v[j];
+            }
+            carry += tot;
+        }
+        if (threadIdx.x == 0) words[a] = carry;
+        __syncthreads();
+    }
+    // exclusive running max of c_last (Hillis-Steele in LDS, kBlock per step)
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < chunks; base += kBlock) {
+        const uint32_t i = base + threadIdx.x;
+        const uint32_t v = (i < chunks) ? c_last[i] : 0u;
+        s_max[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < kBlock; o <<= 1) {
+            const uint32_t y = (threadIdx.x >= (uint32_t)o) ? s_max[threadIdx.x - o] : 0u;
+            __syncthreads();
+            if (y > s_max[threadIdx.x]) s_max[threadIdx.x] = y;
+            __syncthreads();
+        }
+        const uint32_t incl = s_max[threadIdx.x] > carry ? s_max[threadIdx.x] : carry;
+        const uint32_t prev = threadIdx.x ? s_max[threadIdx.x - 1] : 0u;
+        const uint32_t excl = prev > carry ? prev : carry;
+        if (i < chunks) c_last[i] = excl;
+        __syncthreads();
+        const uint32_t blk = s_max[kBlock - 1];
+        carry = blk > carry ? blk : carry;
+        (void)incl;
+        __syncthreads();
+    }
+}
+
+// Per sorted index s (idx = sorted suffix index):
+//   rank[idx]   = pos(head of s's group) + 1
+//   sa[pos(s)]  = idx                               (when sa != nullptr)
+//   unsorted members are compacted, in order, to (u_pos, u_idx, u_g) with
+//   u_g the dense id of their group among unsorted groups.
+template <class Pos>
+__global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ idx, Chunking ch, Pos pos,
+                                                      const uint32_t* __restrict__ o_u,
+                                                      const uint32_t* __restrict__ o_uh,
+                                                      const uint32_t* __restrict__ o_last,
+                                                      uint32_t* __restrict__ rank, uint32_t* __restrict__ sa,
+                                                      uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
+                                                      uint32_t* __restrict__ u_g) {
+    __shared__ uint64_t s_m[kWaves][kItems][3];
+    __shared__ uint32_t s_w[3][kWaves];
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint64_t lt = lanemask_lt(), le = lt | (1ull << lane);
+    uint32_t run_u = o_u[c], run_uh = o_uh[c], run_last = o_last[c];
+    for (uint64_t tb = e0; tb < e1; tb += kTile) {
+        const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
+        uint32_t cu = 0, cuh = 0, lf = 0;
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t rb = w0 + (uint64_t)j * kWave;
+            uint64_t mf = 0, mu = 0, muh = 0;
+            if (rb < e1) {
+                seg_masks(keys, rb + lane, ch.n, mf, mu, muh);
+                const uint64_t lim = e1 - rb >= 64 ? ~0ull : ((1ull << (e1 - rb)) - 1ull);
+                mf &= lim;
+                mu &= lim;
+                muh &= lim;
+            }
+            if (lane == 0) {
+                s_m[wave][j][0] = mf;
+                s_m[wave][j][1] = mu;
+                s_m[wave][j][2] = muh;
+            }
+            cu += __popcll(mu);
+            cuh += __popcll(muh);
+            if (mf) lf = (uint32_t)(rb + 63 - __clzll(mf)) + 1u;
+        }
+        if (lane == 0) {
+            s_w[0][wave] = cu;
+            s_w[1][wave] = cuh;
+            s_w[2][wave] = lf;
+        }
+        __syncthreads();
+        uint32_t off_u = run_u, off_uh = run_uh, carried = run_last;
+        uint32_t tu = 0, tuh = 0, tl = run_last;
+        for (int w = 0; w < kWaves; ++w) {
+            const uint32_t a = s_w[0][w], b = s_w[1][w], l = s_w[2][w];
+            if (w < (int)wave) {
+                off_u += a;
+                off_uh += b;
+                carried = l > carried ? l : carried;
+            }
+            tu += a;
+            tuh += b;
+            tl = l > tl ? l : tl;
+        }
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t rb = w0 + (uint64_t)j * kWave;
+            if (rb >= e1) break;
+            const uint64_t mf = s_m[wave][j][0], mu = s_m[wave][j][1], muh = s_m[wave][j][2];
+            const uint64_t s = rb + lane;
+            if (s < e1) {
+                const uint64_t mh = mf & le;
+                const uint64_t hs = mh ? rb + 63 - __clzll(mh) : (uint64_t)carried - 1u;
+                const uint32_t x = idx[s];
+                const uint32_t p = pos(s);
+                rank[x] = (mh && (63 - __clzll(mh)) == (int)lane ? p : pos(hs)) + 1u;
+                if (sa) sa[p] = x;
+                if ((mu >> lane) & 1ull) {
+                    const uint32_t q = off_u + (uint32_t)__popcll(mu & lt);
+                    u_pos[q] = p;
+                    u_idx[q] = x;
+                    u_g[q] = off_uh + (uint32_t)__popcll(muh & le) - 1u;
+                }
+            }
+            off_u += __popcll(mu);
+            off_uh += __popcll(muh);
+            if (mf) carried = (uint32_t)(rb + 63 - __clzll(mf)) + 1u;
+        }
+        run_u += tu;
+        run_uh += tuh;
+        run_last = tl;
+        __syncthreads();
+    }
 }
 
 }  // namespace sa

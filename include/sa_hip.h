@@ -34,21 +34,35 @@ extern "C" {
 
 /* kernel kinds timed when sa_opts.profile != 0 */
 enum sa_kernel_kind {
-    SA_K_INIT = 0,          /* text -> rank_1 */
-    SA_K_HIST_RANK = 1,     /* digit histogram, keys generated from ranks */
-    SA_K_HIST_KEYS = 2,     /* digit histogram over stored keys */
-    SA_K_SCAN = 3,          /* digit x chunk offset scan */
-    SA_K_SCATTER_RANK = 4,  /* stable scatter, keys generated from ranks */
-    SA_K_SCATTER_KEYS = 5,  /* stable scatter over stored (key, idx) */
-    SA_K_HEADS = 6,         /* group-head count per chunk */
-    SA_K_HEADS_SCAN = 7,    /* chunk scan of head counts, D_j */
-    SA_K_RERANK = 8,        /* dense rank -> rank[idx] scatter */
-    SA_K_COUNT = 9
+    SA_K_INIT = 0,           /* text -> rank_1 (reference schedule) */
+    SA_K_HIST_FIRST = 1,     /* digit histogram, keys generated (text/ranks) */
+    SA_K_HIST_KEYS = 2,      /* digit histogram over stored keys */
+    SA_K_SCAN = 3,           /* digit x chunk offset scan */
+    SA_K_SCATTER_FIRST = 4,  /* stable scatter, keys generated (text/ranks) */
+    SA_K_SCATTER_KEYS = 5,   /* stable scatter over stored (key, idx) */
+    SA_K_HEADS = 6,          /* group-head count per chunk (reference schedule) */
+    SA_K_HEADS_SCAN = 7,     /* chunk scan of head counts, D_j */
+    SA_K_RERANK = 8,         /* dense rank -> rank[idx] scatter */
+    SA_K_SEG_COUNT = 9,      /* heads / unsorted / group counts per chunk */
+    SA_K_SEG_SCAN = 10,      /* chunk scan of those counts */
+    SA_K_SEG_WRITE = 11,     /* rank + SA update, unsorted-set compaction */
+    SA_K_ALPHABET = 12,      /* byte histogram of the text */
+    SA_K_COUNT = 13
 };
+
+/* doubling schedules */
+#define SA_SCHEDULE_PACKED 0     /* default: first round sorts a packed K-symbol
+                                    prefix; later rounds re-sort only suffixes
+                                    whose group is not yet a singleton */
+#define SA_SCHEDULE_REFERENCE 1  /* the reference's schedule (manber_myers.c:
+                                    94-125): h = 1, 2, 4, ...; D_0 = 256; every
+                                    round sorts all n (rank[i], rank[i+h]) pairs */
 
 typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
-    int32_t reserved[7];
+    int32_t schedule;       /* SA_SCHEDULE_* */
+    int32_t init_chars;     /* packed schedule: symbols in the first key, 0 = auto */
+    int32_t reserved[5];
 } sa_opts;
 
 typedef struct {
@@ -57,8 +71,14 @@ typedef struct {
     double total_ms;                     /* build time on the stream (HBM in -> HBM out) */
     double h2d_ms, d2h_ms;               /* sa_build_ex only: PCIe copies */
     double round_ms[SA_MAX_ROUNDS];      /* per doubling round */
-    uint64_t distinct[SA_MAX_ROUNDS];    /* D_j after round j */
+    uint64_t distinct[SA_MAX_ROUNDS];    /* D_j: distinct h-prefix groups after round j */
     int32_t passes[SA_MAX_ROUNDS];       /* radix passes in round j */
+    uint64_t sorted_n[SA_MAX_ROUNDS];    /* suffixes (re-)sorted in round j */
+    uint64_t prefix_len[SA_MAX_ROUNDS];  /* h after round j (prefix length sorted) */
+    int32_t schedule;                    /* SA_SCHEDULE_* used */
+    int32_t init_chars;                  /* K of the packed schedule */
+    int32_t sigma;                       /* distinct symbols in the text */
+    int32_t pad0;
     uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
     double kern_ms[SA_K_COUNT];          /* profile only */
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */
@@ -99,6 +119,8 @@ const char* sa_last_error(void);
 int sa_device_count(void);
 /* library build identification, e.g. "sa_hip gfx950 <date>" */
 const char* sa_version(void);
+/* sizeof(sa_stats) (which = 0) / sizeof(sa_opts) (which = 1), for bindings */
+uint64_t sa_struct_size(int which);
 
 #ifdef __cplusplus
 }

@@ -57,9 +57,12 @@ def test_struct_layout(sa_lib):
 
 
 def test_stats_struct_matches_header(sa_lib):
-    # sa_stats layout: 2 x i32, 3 doubles, 64 doubles, 64 u64, 64 i32, u64, 3 x 9 arrays
-    expected = 8 + 24 + 64 * 8 + 64 * 8 + 64 * 4 + 8 + 9 * 8 * 3
-    assert ctypes.sizeof(sa_lib.SaStats) == expected
+    L = sa_lib.lib()
+    L.sa_struct_size.argtypes = [ctypes.c_int]
+    L.sa_struct_size.restype = ctypes.c_uint64
+    assert ctypes.sizeof(sa_lib.SaStats) == L.sa_struct_size(0)
+    assert ctypes.sizeof(sa_lib.SaOpts) == L.sa_struct_size(1)
+    assert len(sa_lib.KERNEL_KINDS) == sa_lib.SA_K_COUNT == 13
 
 
 def test_create_has_strncpy_semantics(sa_lib):

@@ -51,17 +51,36 @@ def test_int64_output(gpu, oracle):
     assert (got == oracle.sa_c(t).astype(np.int64)).all()
 
 
+@pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("kind", ["dna", "alnum", "ascii127", "byte256", "binary"])
 @pytest.mark.parametrize("n", [1, 2, 3, 4095, 4096, 4097, 65535, 1 << 17, 1_000_003, 4_194_305])
-def test_random_vs_oracle(gpu, oracle, kind, n):
+def test_random_vs_oracle(gpu, oracle, kind, n, schedule):
     from hpc_suffix_array_amd import build_suffix_array
     t = oracle.gen_text(kind, n, seed=n + len(kind))
-    got, st = build_suffix_array(t, return_stats=True)
+    got, st = build_suffix_array(t, return_stats=True, schedule=schedule)
     ref, rounds, _, dj = oracle.sa_c(t, stats=True)
     assert (got == ref).all()
-    if n > 1:
+    if n > 1 and schedule == "reference":
+        # the reference schedule reproduces manber_myers.c round for round
         assert st["rounds"] == rounds
         assert st["distinct"] == dj
+    if n > 1:
+        assert st["distinct"][-1] == n
+
+
+@pytest.mark.parametrize("init_chars", [1, 2, 3, 5])
+@pytest.mark.parametrize("kind", ["dna", "binary", "alnum"])
+def test_packed_short_first_key(gpu, oracle, kind, init_chars):
+    """A short first key leaves most suffixes unsorted: exercises the
+    unsorted-set doubling rounds (compaction, (g, rank[i+h]) keys, SA/rank
+    updates through the position map)."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for n in (5, 777, 70_001, 1_000_000):
+        t = oracle.gen_text(kind, n, seed=init_chars * 7 + n)
+        got, st = build_suffix_array(t, return_stats=True, init_chars=init_chars)
+        assert st["init_chars"] == init_chars
+        assert (got == oracle.sa_c(t)).all(), (kind, n, init_chars)
+        assert st["distinct"][-1] == n
 
 
 def test_known_answers_1mib(gpu, oracle, golden):
@@ -73,31 +92,38 @@ def test_known_answers_1mib(gpu, oracle, golden):
         assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"], key
 
 
-def test_config2_64mib_dna_known_answer(gpu, oracle, golden):
+@pytest.mark.parametrize("schedule", ["packed", "reference"])
+def test_config2_64mib_dna_known_answer(gpu, oracle, golden, schedule):
     """configs[1]: 64 MiB random DNA on 1 MI355X, bit-exact vs sequential."""
     from hpc_suffix_array_amd import build_suffix_array
     k = golden["known"]["dna_64MiB"]
     t = oracle.gen_text("dna", k["n"], seed=k["seed"])
     assert oracle.sha256(t) == k["text_sha256"]
-    got, st = build_suffix_array(t, return_stats=True)
-    assert st["rounds"] == k["rounds"]
+    got, st = build_suffix_array(t, return_stats=True, schedule=schedule)
+    if schedule == "reference":
+        assert st["rounds"] == k["rounds"]
     assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
 
 
+@pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("n", [2, 17, 4096, 65537, 1 << 20, (1 << 22) + 3])
-def test_degenerate(gpu, n):
+def test_degenerate(gpu, n, schedule):
     """configs[4] shape: one repeated symbol, log2 n rounds, analytic SA."""
     from hpc_suffix_array_amd import build_suffix_array
-    got, st = build_suffix_array(np.full(n, ord("a"), np.uint8), return_stats=True)
+    got, st = build_suffix_array(np.full(n, ord("a"), np.uint8), return_stats=True, schedule=schedule)
     assert (got == np.arange(n - 1, -1, -1, dtype=np.uint32)).all()
     assert st["distinct"][-1] == n
 
 
-def test_periodic(gpu, oracle):
+@pytest.mark.parametrize("schedule", ["packed", "reference"])
+def test_periodic(gpu, oracle, schedule):
     from hpc_suffix_array_amd import build_suffix_array
     base = oracle.gen_text("alnum", 1000, seed=11)
     t = np.tile(base, 300)
-    assert (build_suffix_array(t) == oracle.sa_c(t)).all()
+    assert (build_suffix_array(t, schedule=schedule) == oracle.sa_c(t)).all()
+    # short period, long repeats: most suffixes stay unsorted for many rounds
+    t = np.tile(np.frombuffer(b"abaababa", np.uint8), 40_000)
+    assert (build_suffix_array(t, schedule=schedule) == oracle.sa_c(t)).all()
 
 
 def test_checker_detects_corruption(gpu, oracle):
