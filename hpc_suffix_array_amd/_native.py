@@ -17,7 +17,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 SA_MAX_ROUNDS = 64
 KERNEL_KINDS = ["init", "hist_first", "hist_keys", "scan", "scatter_first", "scatter_keys",
-                "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet"]
+                "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet", "pack"]
 SCHEDULE_PACKED = 0
 SCHEDULE_REFERENCE = 1
 SA_K_COUNT = len(KERNEL_KINDS)
@@ -54,7 +54,7 @@ class SaStats(ctypes.Structure):
         ("schedule", ctypes.c_int32),
         ("init_chars", ctypes.c_int32),
         ("sigma", ctypes.c_int32),
-        ("pad0", ctypes.c_int32),
+        ("sparse_ranks", ctypes.c_int32),
         ("model_bytes", ctypes.c_uint64),
         ("kern_ms", ctypes.c_double * SA_K_COUNT),
         ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
@@ -76,6 +76,7 @@ class SaStats(ctypes.Structure):
             "schedule": "reference" if self.schedule == SCHEDULE_REFERENCE else "packed",
             "init_chars": self.init_chars,
             "sigma": self.sigma,
+            "sparse_ranks": bool(self.sparse_ranks),
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

@@ -61,6 +61,8 @@ static bool trace_on() {
     } while (0)
 
 constexpr uint32_t kMaxChunks = 1024;
+// sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
+constexpr uint64_t kSparseDiv = 8;
 constexpr int kEvPool = 256;
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
@@ -95,6 +97,8 @@ struct sa_context {
     uint32_t* u_pos[2] = {nullptr, nullptr};    // compacted unsorted set, ping-pong
     uint32_t* u_idx[2] = {nullptr, nullptr};
     uint32_t* u_g[2] = {nullptr, nullptr};
+    uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
+    uint32_t* member = nullptr;                 // bitmap of round-1 unsorted positions
     uint32_t* hist = nullptr;      // 256 * kMaxChunks
     uint32_t* totals = nullptr;    // 256
     uint32_t* counts = nullptr;    // 4 * kMaxChunks (heads, u, uheads, last)
@@ -112,7 +116,7 @@ namespace sa {
 // (the reference schedule), plus 7 u32 arrays for the unsorted set (packed).
 static uint64_t ws_bytes(uint64_t n) {
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
-    return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
+    return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + m * 8 + m / 8 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
 }
 
 static void free_ctx_buffers(sa_context* c) {
@@ -128,7 +132,11 @@ static void free_ctx_buffers(sa_context* c) {
 
 static void free_u_buffers(sa_context* c) {
     hipFree(c->vals_u);
+    hipFree(c->keys_u);
+    hipFree(c->member);
     c->vals_u = nullptr;
+    c->keys_u = nullptr;
+    c->member = nullptr;
     for (int i = 0; i < 2; ++i) {
         hipFree(c->u_pos[i]);
         hipFree(c->u_idx[i]);
@@ -159,7 +167,8 @@ static int ensure_u_capacity(sa_context* c, uint64_t n) {
     SA_HIP(hipSetDevice(c->device));
     free_u_buffers(c);
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64) * 4;
-    bool ok = hipMalloc(&c->vals_u, m) == hipSuccess;
+    bool ok = hipMalloc(&c->vals_u, m) == hipSuccess && hipMalloc(&c->keys_u, 2 * m) == hipSuccess &&
+              hipMalloc(&c->member, align_up(n, 1024) / 8) == hipSuccess;
     for (int i = 0; i < 2 && ok; ++i)
         ok = hipMalloc(&c->u_pos[i], m) == hipSuccess && hipMalloc(&c->u_idx[i], m) == hipSuccess &&
              hipMalloc(&c->u_g[i], m) == hipSuccess;
@@ -234,11 +243,14 @@ static void add_bytes(sa_stats* st, int kind, uint64_t b) {
 template <class Src>
 static int radix_pass(sa_context* c, const Src& src, const Chunking& ch, uint32_t shift, uint32_t nbits,
                       uint64_t* out_keys, uint32_t* out_vals, hipStream_t s, Timer& tm, sa_stats* st,
-                      int kind_hist, int kind_scatter, uint64_t in_bytes) {
+                      int kind_hist, int kind_scatter, uint64_t in_bytes, bool hist_ready = false) {
     const uint32_t mask = (1u << nbits) - 1u;
-    tm.begin(kind_hist);
-    hipLaunchKernelGGL(k_hist<Src>, dim3(ch.chunks), dim3(kBlock), 0, s, src, ch, shift, mask, c->hist);
-    tm.end();
+    if (!hist_ready) {
+        tm.begin(kind_hist);
+        hipLaunchKernelGGL(k_hist<Src>, dim3(ch.chunks), dim3(kBlock), 0, s, src, ch, shift, mask, c->hist);
+        tm.end();
+        add_bytes(st, kind_hist, in_bytes);
+    }
     tm.begin(SA_K_SCAN);
     hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(kBlock), 0, s, c->hist, ch.chunks, c->totals);
     tm.end();
@@ -247,7 +259,6 @@ static int radix_pass(sa_context* c, const Src& src, const Chunking& ch, uint32_
                        (const uint32_t*)c->hist, (const uint32_t*)c->totals, out_keys, out_vals);
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, kind_hist, in_bytes);
     add_bytes(st, SA_K_SCAN, 2ull * 4 * kRadix * ch.chunks);
     add_bytes(st, kind_scatter, in_bytes + 12ull * ch.n);
     return SA_OK;
@@ -258,27 +269,28 @@ static int radix_pass(sa_context* c, const Src& src, const Chunking& ch, uint32_
 // The sorted idx land in vals_final; *kbuf = index of the sorted key buffer.
 template <class Src>
 static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, const Chunking& ch, uint32_t bits,
-                      uint32_t* vals_final, uint32_t* vals_other, hipStream_t s, Timer& tm, sa_stats* st,
-                      int* kbuf, uint32_t* passes) {
+                      uint32_t* vals_final, uint32_t* vals_other, uint64_t* kb0, uint64_t* kb1, hipStream_t s,
+                      Timer& tm, sa_stats* st, uint64_t** sorted_keys, uint32_t* passes, bool hist0_ready = false) {
     const uint32_t P = (bits + 7) / 8;
     uint32_t* vb[2];
     vb[(P - 1) & 1] = vals_final;
     vb[P & 1] = vals_other;
+    uint64_t* kb[2] = {kb0, kb1};
     for (uint32_t p = 0; p < P; ++p) {
         const uint32_t shift = 8 * p;
         const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
         int rc;
         if (p == 0) {
-            rc = radix_pass(c, first, ch, shift, nbits, c->keys[0], vb[0], s, tm, st, SA_K_HIST_FIRST,
-                            SA_K_SCATTER_FIRST, first_bytes);
+            rc = radix_pass(c, first, ch, shift, nbits, kb[0], vb[0], s, tm, st, SA_K_HIST_FIRST,
+                            SA_K_SCATTER_FIRST, first_bytes, hist0_ready);
         } else {
-            SrcKeys src{c->keys[(p - 1) & 1], vb[(p - 1) & 1]};
-            rc = radix_pass(c, src, ch, shift, nbits, c->keys[p & 1], vb[p & 1], s, tm, st, SA_K_HIST_KEYS,
+            SrcKeys src{kb[(p - 1) & 1], vb[(p - 1) & 1]};
+            rc = radix_pass(c, src, ch, shift, nbits, kb[p & 1], vb[p & 1], s, tm, st, SA_K_HIST_KEYS,
                             SA_K_SCATTER_KEYS, 12 * ch.n);
         }
         if (rc) return rc;
     }
-    *kbuf = (int)((P - 1) & 1);
+    *sorted_keys = kb[(P - 1) & 1];
     *passes = P;
     return SA_OK;
 }
@@ -322,11 +334,10 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const uint32_t w = bit_width(D);          // ranks are 0..D
         SA_TRACE("reference round h=%llu D=%llu w=%u", (unsigned long long)h, (unsigned long long)D, w);
         SrcRank src{c->rank, n, h, w};
-        int kb;
+        uint64_t* sorted;
         uint32_t P;
-        rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, s, tm, st, &kb, &P);
+        rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &sorted, &P);
         if (rc) return rc;
-        const uint64_t* sorted = c->keys[kb];
         tm.begin(SA_K_HEADS);
         hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts);
         tm.end();
@@ -407,6 +418,7 @@ static uint32_t choose_chars(uint32_t sigma, uint64_t n, int32_t req) {
 
 template <class Pos>
 static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
+                    bool sparse_ok, bool* sparse_out,
                     uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
                     uint64_t* G) {
     uint32_t* c_h = c->counts;
@@ -421,19 +433,27 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     tm.end();
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 12, hipMemcpyDeviceToHost, s));
-    tm.begin(SA_K_SEG_WRITE);
-    hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
-                       (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, c->rank, sa,
-                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo]);
-    tm.end();
-    SA_HIP(hipGetLastError());
     SA_HIP(hipStreamSynchronize(s));
     *D = c->host_words[0];
     *m = c->host_words[1];
     *G = c->host_words[2];
+    // first round with few unsorted suffixes: keep ranks only for those
+    const bool sparse = sparse_ok && *m <= ch.n / kSparseDiv;
+    uint32_t* member = nullptr;
+    if (sparse) {
+        SA_HIP(hipMemsetAsync(c->member, 0, (ch.n + 31) / 32 * 4, s));
+        member = c->member;
+    }
+    if (sparse_out) *sparse_out = sparse;
+    tm.begin(SA_K_SEG_WRITE);
+    hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
+                       (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, c->rank, sa,
+                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1);
+    tm.end();
+    SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);
     add_bytes(st, SA_K_SEG_SCAN, 32ull * ch.chunks);
-    add_bytes(st, SA_K_SEG_WRITE, ch.n * (8 + 4 + 4 + (sa ? 8 : 0)) + *m * 12);
+    add_bytes(st, SA_K_SEG_WRITE, ch.n * (8 + (sparse ? 0 : 8)) + (sa ? 8 * ch.n : 0) + *m * 16);
     return SA_OK;
 }
 
@@ -473,15 +493,30 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
 
     // round 1: sort the packed K-prefix of every suffix
     const Chunking ch = plan_chunks(n);
-    SrcText src{d_text, c->code, n, base, K};
-    int kb;
+    uint64_t top = 1;   // B^(K-1)
+    for (uint32_t t = 1; t < K; ++t) top *= base;
+    tm.begin(SA_K_PACK);
+    hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, (const uint16_t*)c->code, ch,
+                       base, top, K, c->keys[1], c->hist);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_PACK, 9 * n);
+    SrcKeysIota src{c->keys[1]};
+    uint64_t* keys1;
     uint32_t P;
-    rc = radix_sort(c, src, n, ch, bits1, d_sa, c->vals_alt, s, tm, st, &kb, &P);
+    rc = radix_sort(c, src, 8 * n, ch, bits1, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &keys1, &P,
+                    true);
     if (rc) return rc;
     uint64_t D, m, G;
     int uo = 0;
-    rc = segments(c, c->keys[kb], d_sa, ch, PosIdentity{}, nullptr, uo, s, tm, st, &D, &m, &G);
+    bool sparse = false;
+    rc = segments(c, keys1, d_sa, ch, PosIdentity{}, true, &sparse, nullptr, uo, s, tm, st, &D, &m, &G);
     if (rc) return rc;
+    // later rounds sort in the two buffers that do not hold the round-1 keys
+    uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
+    uint64_t* ukb1 = c->keys_u;
+    const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K};
+    if (st) st->sparse_ranks = sparse ? 1 : 0;
     SA_HIP(hipEventRecord(ev.e[1], s));
     SA_HIP(hipEventSynchronize(ev.e[1]));
     tm.flush();
@@ -500,11 +535,18 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         const Chunking cu = plan_chunks(m);
         const int ui = uo;
         uo ^= 1;
-        SrcU su{c->u_idx[ui], c->u_g[ui], c->rank, n, h, wr};
-        rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, s, tm, st, &kb, &P);
+        uint64_t* sorted;
+        if (sparse) {
+            SrcU<true> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
+            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P);
+        } else {
+            SrcU<false> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
+            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P);
+        }
         if (rc) return rc;
         uint64_t Du, m2, G2;
-        rc = segments(c, c->keys[kb], c->vals_u, cu, PosArray{c->u_pos[ui]}, d_sa, uo, s, tm, st, &Du, &m2, &G2);
+        rc = segments(c, sorted, c->vals_u, cu, PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm, st, &Du,
+                      &m2, &G2);
         if (rc) return rc;
         SA_HIP(hipEventRecord(ev.e[1], s));
         SA_HIP(hipEventSynchronize(ev.e[1]));

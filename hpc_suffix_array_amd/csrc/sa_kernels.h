@@ -86,16 +86,50 @@ struct SrcText {
 // singleton (compacted in SA order: idx, dense group id g).  key =
 // (g << wr) | rank[idx + h]; rank is the group-head position + 1 (0 = past
 // the end), so sorting by key refines every group by its next h symbols.
+//
+// kSparse: after a first round that left few suffixes unsorted, rank[] is
+// only maintained for those (flagged in `member`); the rank of any other
+// position j is its round-1 group head, found by a binary search of its
+// packed K-symbol key in the round-1 sorted keys (a singleton's head is its
+// own SA position).  This avoids a random scatter of all n ranks.
+struct RankLookup {
+    const uint32_t* __restrict__ rank;
+    const uint32_t* __restrict__ member;   // bitmap of round-1 unsorted positions
+    const uint64_t* __restrict__ keys1;    // round-1 sorted packed keys (n)
+    const uint8_t* __restrict__ text;
+    const uint16_t* __restrict__ code;
+    uint64_t n;
+    uint64_t base;
+    uint32_t K;
+    __device__ __forceinline__ uint32_t sparse(uint64_t j) const {
+        if ((member[j >> 5] >> (j & 31)) & 1u) return rank[j];
+        uint64_t x = 0;
+        for (uint32_t t = 0; t < K; ++t) x = x * base + ((j + t < n) ? code[text[j + t]] : 0u);
+        uint64_t lo = 0, len = n;      // lower_bound(keys1, x)
+        while (len > 0) {
+            const uint64_t half = len >> 1;
+            if (keys1[lo + half] < x) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        return (uint32_t)lo + 1u;
+    }
+};
+
+template <bool kSparse>
 struct SrcU {
     const uint32_t* __restrict__ u_idx;
     const uint32_t* __restrict__ u_g;
-    const uint32_t* __restrict__ rank;
-    uint64_t n;
+    RankLookup rl;
     uint64_t h;
     uint32_t wr;
     __device__ __forceinline__ uint64_t key(uint64_t e) const {
         const uint64_t i = u_idx[e];
-        const uint64_t r1 = (i + h < n) ? rank[i + h] : 0u;
+        uint64_t r1 = 0;
+        if (i + h < rl.n) r1 = kSparse ? rl.sparse(i + h) : rl.rank[i + h];
         return ((uint64_t)u_g[e] << wr) | r1;
     }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
@@ -107,6 +141,13 @@ struct SrcKeys {
     const uint32_t* __restrict__ vals;
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return vals[e]; }
+};
+
+// Keys already materialised in text order (k_pack_text), index = position.
+struct SrcKeysIota {
+    const uint64_t* __restrict__ keys;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
 };
 
 struct Chunking {
@@ -490,6 +531,73 @@ __global__ __launch_bounds__(kBlock) void k_byte_hist(const uint8_t* __restrict_
 }
 
 // ---------------------------------------------------------------------------
+// packed schedule, round 1 key build: key(i) = sum_t code(i+t) B^(K-1-t),
+// t < K.  One tile of codes (+ K-1 halo) is staged in LDS; each lane builds
+// 16 consecutive keys, the first by Horner, the rest by the rolling update
+// key' = (key - c_out B^(K-1)) B + c_in.  The digit-0 histogram of the first
+// radix pass is taken here as well (same chunking as k_hist), so that pass
+// starts with its scatter.
+// ---------------------------------------------------------------------------
+constexpr int kPackRun = kTile / kBlock;   // 16 consecutive keys per lane
+constexpr int kMaxK = 64;
+
+__global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict__ text,
+                                                      const uint16_t* __restrict__ code, Chunking ch,
+                                                      uint64_t base, uint64_t top, uint32_t K,
+                                                      uint64_t* __restrict__ keys, uint32_t* __restrict__ hist) {
+    __shared__ uint16_t s_code[256];
+    __shared__ uint16_t s_c[kTile + kMaxK];
+    __shared__ uint32_t s_hist[kWaves][kRadix];
+    s_code[threadIdx.x] = code[threadIdx.x];
+    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    const uint64_t n = ch.n;
+    uint32_t* my = s_hist[wave_id()];
+    __syncthreads();
+    for (uint64_t tb = e0; tb < e1; tb += kTile) {
+        for (uint32_t q = threadIdx.x; q < (uint32_t)kTile + K; q += kBlock) {
+            const uint64_t i = tb + q;
+            s_c[q] = (i < n) ? s_code[text[i]] : (uint16_t)0;
+        }
+        __syncthreads();
+        const uint32_t l0 = threadIdx.x * kPackRun;
+        uint64_t x = 0;
+        for (uint32_t t = 0; t < K; ++t) x = x * base + s_c[l0 + t];
+        uint64_t out[kPackRun];
+        out[0] = x;
+#pragma unroll
+        for (int j = 1; j < kPackRun; ++j) {
+            x = (x - (uint64_t)s_c[l0 + j - 1] * top) * base + s_c[l0 + j - 1 + K];
+            out[j] = x;
+        }
+        const uint64_t g0 = tb + l0;
+        if (g0 + kPackRun <= e1) {
+            uint4* dst = reinterpret_cast<uint4*>(keys + g0);
+#pragma unroll
+            for (int j = 0; j < kPackRun; j += 2) {
+                dst[j / 2] = make_uint4((uint32_t)out[j], (uint32_t)(out[j] >> 32), (uint32_t)out[j + 1],
+                                        (uint32_t)(out[j + 1] >> 32));
+                atomicAdd(&my[out[j] & 0xFFu], 1u);
+                atomicAdd(&my[out[j + 1] & 0xFFu], 1u);
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kPackRun; ++j)
+                if (g0 + j < e1) {
+                    keys[g0 + j] = out[j];
+                    atomicAdd(&my[out[j] & 0xFFu], 1u);
+                }
+        }
+        __syncthreads();
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) s += s_hist[w][threadIdx.x];
+    hist[(uint64_t)threadIdx.x * ch.chunks + c] = s;
+}
+
+// ---------------------------------------------------------------------------
 // Segments of a sorted key sequence s = 0..m-1 (packed schedule).
 //   head(s)   key[s] != key[s-1]               (manber_myers.c:104-105)
 //   single(s) head(s) and head(s+1)            (group of size 1: final)
@@ -639,7 +747,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                                                       const uint32_t* __restrict__ o_last,
                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ sa,
                                                       uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
-                                                      uint32_t* __restrict__ u_g) {
+                                                      uint32_t* __restrict__ u_g, uint32_t* __restrict__ member,
+                                                      int dense_rank) {
     __shared__ uint64_t s_m[kWaves][kItems][3];
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
@@ -698,9 +807,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                 const uint64_t hs = mh ? rb + 63 - __clzll(mh) : (uint64_t)carried - 1u;
                 const uint32_t x = idx[s];
                 const uint32_t p = pos(s);
-                rank[x] = (mh && (63 - __clzll(mh)) == (int)lane ? p : pos(hs)) + 1u;
+                const bool in_u = (mu >> lane) & 1ull;
+                if (dense_rank || in_u) rank[x] = (hs == s ? p : pos(hs)) + 1u;
                 if (sa) sa[p] = x;
-                if ((mu >> lane) & 1ull) {
+                if (member && in_u) atomicOr(&member[x >> 5], 1u << (x & 31));
+                if (in_u) {
                     const uint32_t q = off_u + (uint32_t)__popcll(mu & lt);
                     u_pos[q] = p;
                     u_idx[q] = x;

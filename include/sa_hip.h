@@ -47,7 +47,8 @@ enum sa_kernel_kind {
     SA_K_SEG_SCAN = 10,      /* chunk scan of those counts */
     SA_K_SEG_WRITE = 11,     /* rank + SA update, unsorted-set compaction */
     SA_K_ALPHABET = 12,      /* byte histogram of the text */
-    SA_K_COUNT = 13
+    SA_K_PACK = 13,          /* packed K-symbol keys + first digit histogram */
+    SA_K_COUNT = 14
 };
 
 /* doubling schedules */
@@ -78,7 +79,7 @@ typedef struct {
     int32_t schedule;                    /* SA_SCHEDULE_* used */
     int32_t init_chars;                  /* K of the packed schedule */
     int32_t sigma;                       /* distinct symbols in the text */
-    int32_t pad0;
+    int32_t sparse_ranks;                /* 1: round-1 ranks kept for unsorted suffixes only */
     uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
     double kern_ms[SA_K_COUNT];          /* profile only */
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */

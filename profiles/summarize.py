@@ -20,9 +20,10 @@ import sys
 from collections import defaultdict
 
 KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcText>", "hist_text"),
-         ("k_hist<sa::SrcU>", "hist_u"), ("k_hist<sa::SrcKeys>", "hist_keys"),
+         ("k_hist<sa::SrcU", "hist_u"), ("k_hist<sa::SrcKeys>", "hist_keys"),
          ("k_scan_rows", "scan"), ("k_scatter<sa::SrcRank>", "scatter_rank"),
-         ("k_scatter<sa::SrcText>", "scatter_text"), ("k_scatter<sa::SrcU>", "scatter_u"),
+         ("k_scatter<sa::SrcText>", "scatter_text"), ("k_scatter<sa::SrcU", "scatter_u"),
+         ("k_scatter<sa::SrcKeysIota>", "scatter_iota"), ("k_pack_text", "pack"),
          ("k_scatter<sa::SrcKeys>", "scatter_keys"), ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
          ("k_rerank", "rerank"), ("k_seg_count", "seg_count"), ("k_seg_scan", "seg_scan"),
          ("k_seg_write", "seg_write"), ("k_byte_hist", "alphabet"), ("k_gen_text", "gen_text"),
