@@ -56,6 +56,7 @@ def parse():
     ap.add_argument("--no-profile", action="store_true", help="no per-launch HIP events")
     ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("--init-chars", type=int, default=0)
+    ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -130,7 +131,7 @@ def main():
     torch.cuda.synchronize(dev)
 
     profile = not a.no_profile
-    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars)
+    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars, radix=a.radix)
     for _ in range(a.warmup):
         b.build(d_text, n, d_sa, **bkw)
 

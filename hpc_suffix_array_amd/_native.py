@@ -36,7 +36,7 @@ class SAError(RuntimeError):
 
 class SaOpts(ctypes.Structure):
     _fields_ = [("profile", ctypes.c_int32), ("schedule", ctypes.c_int32), ("init_chars", ctypes.c_int32),
-                ("reserved", ctypes.c_int32 * 5)]
+                ("radix", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
 
 
 class SaStats(ctypes.Structure):

@@ -31,18 +31,21 @@ def _as_bytes_array(text) -> np.ndarray:
 
 
 SCHEDULES = {"packed": N.SCHEDULE_PACKED, "reference": N.SCHEDULE_REFERENCE}
+RADIX = {"onesweep": 0, "reduce_scan": 1}
 
 
-def _opts(profile: bool = False, schedule: str = "packed", init_chars: int = 0) -> N.SaOpts:
+def _opts(profile: bool = False, schedule: str = "packed", init_chars: int = 0,
+          radix: str = "onesweep") -> N.SaOpts:
     o = N.SaOpts()
     o.profile = 1 if profile else 0
     o.schedule = SCHEDULES[schedule]
     o.init_chars = int(init_chars)
+    o.radix = RADIX[radix]
     return o
 
 
 def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False,
-                       schedule: str = "packed", init_chars: int = 0):
+                       schedule: str = "packed", init_chars: int = 0, radix: str = "onesweep"):
     """Suffix array of ``text`` (bytes / uint8 array), built on the GPU.
 
     Unsigned-byte order, end of string smallest (== the reference's order on
@@ -58,7 +61,8 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     st = N.SaStats()
     L = N.lib()
     N.check(L.sa_build_ex(t.ctypes.data if n else None, n, out.ctypes.data, width,
-                          ctypes.byref(_opts(profile, schedule, init_chars)), ctypes.byref(st)), "sa_build_ex")
+                          ctypes.byref(_opts(profile, schedule, init_chars, radix)), ctypes.byref(st)),
+            "sa_build_ex")
     out = out[:n]
     return (out, st.to_dict()) if return_stats else out
 
@@ -165,12 +169,13 @@ class DeviceBuilder:
         return x if isinstance(x, int) else int(x.data_ptr())
 
     def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False, schedule: str = "packed",
-              init_chars: int = 0) -> dict:
+              init_chars: int = 0, radix: str = "onesweep") -> dict:
         """Build the SA of the n bytes at d_text into the n uint32 at d_sa."""
         st = N.SaStats()
         s = None if stream is None else ctypes.c_void_p(int(stream))
         N.check(self.L.sa_build_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s,
-                                       ctypes.byref(_opts(profile, schedule, init_chars)), ctypes.byref(st)),
+                                       ctypes.byref(_opts(profile, schedule, init_chars, radix)),
+                                       ctypes.byref(st)),
                 "sa_build_device")
         return st.to_dict()
 

@@ -25,6 +25,7 @@
 
 #include "../../include/sa_hip.h"
 #include "sa_kernels.h"
+#include "sa_onesweep.h"
 
 namespace sa {
 
@@ -98,6 +99,10 @@ struct sa_context {
     uint32_t* u_idx[2] = {nullptr, nullptr};
     uint32_t* u_g[2] = {nullptr, nullptr};
     uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
+    uint32_t* os = nullptr;                     // onesweep ghist / digit bases / tickets
+    uint64_t* states = nullptr;                 // onesweep tile states [tiles][256]
+    uint32_t epoch = 0;                         // onesweep state tag of the last pass
+    int radix = 0;                              // 0 onesweep, 1 reduce-then-scan
     uint32_t* member = nullptr;                 // bitmap of round-1 unsorted positions
     uint32_t* hist = nullptr;      // 256 * kMaxChunks
     uint32_t* totals = nullptr;    // 256
@@ -119,14 +124,18 @@ static uint64_t ws_bytes(uint64_t n) {
     return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + m * 8 + m / 8 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
 }
 
+static uint64_t tile_states_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * kRadix * 8; }
+
 static void free_ctx_buffers(sa_context* c) {
     hipFree(c->rank);
     hipFree(c->keys[0]);
     hipFree(c->keys[1]);
     hipFree(c->vals_alt);
+    hipFree(c->states);
     c->rank = nullptr;
     c->keys[0] = c->keys[1] = nullptr;
     c->vals_alt = nullptr;
+    c->states = nullptr;
     c->cap = 0;
 }
 
@@ -152,7 +161,9 @@ static int ensure_capacity(sa_context* c, uint64_t n) {
     free_ctx_buffers(c);
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
     if (hipMalloc(&c->rank, m * 4) != hipSuccess || hipMalloc(&c->keys[0], m * 8) != hipSuccess ||
-        hipMalloc(&c->keys[1], m * 8) != hipSuccess || hipMalloc(&c->vals_alt, m * 4) != hipSuccess) {
+        hipMalloc(&c->keys[1], m * 8) != hipSuccess || hipMalloc(&c->vals_alt, m * 4) != hipSuccess ||
+        hipMalloc(&c->states, tile_states_bytes(n)) != hipSuccess ||
+        hipMemset(c->states, 0, tile_states_bytes(n)) != hipSuccess) {
         free_ctx_buffers(c);
         (void)hipGetLastError();
         return set_err(SA_E_NOMEM, "device allocation of %.2f GiB workspace failed",
@@ -264,14 +275,86 @@ static int radix_pass(sa_context* c, const Src& src, const Chunking& ch, uint32_
     return SA_OK;
 }
 
+// single-pass (onesweep) scratch: ghist[8][256] | base[8][256] | tickets[8]
+static uint32_t* os_ghist(sa_context* c) { return c->os; }
+static uint32_t* os_base(sa_context* c) { return c->os + kMaxPasses * kRadix; }
+static uint32_t* os_tickets(sa_context* c) { return c->os + 2 * kMaxPasses * kRadix; }
+
+// zero the global histograms and tile tickets of the next sort
+static int onesweep_prepare(sa_context* c, hipStream_t s) {
+    SA_HIP(hipMemsetAsync(c->os, 0, (2 * kMaxPasses * kRadix + kMaxPasses) * 4, s));
+    return SA_OK;
+}
+
+static uint32_t next_epoch(sa_context* c, hipStream_t s, uint64_t tiles) {
+    if (++c->epoch > kEpochMask) {
+        hipMemsetAsync(c->states, 0, tiles * kRadix * 8, s);
+        c->epoch = 1;
+    }
+    return c->epoch;
+}
+
+template <class Src>
+static void onesweep_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits,
+                          const uint32_t* base, uint32_t* ticket, uint64_t* out_keys, uint32_t* out_vals,
+                          hipStream_t s) {
+    const uint64_t tiles = (n + kTile - 1) / kTile;
+    const uint32_t epoch = next_epoch(c, s, tiles);
+    hipLaunchKernelGGL((k_onesweep<Src, kBlock, kItems>), dim3((uint32_t)tiles), dim3(kBlock), 0, s, src, n, shift,
+                       nbits, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
+}
+
 // Stable LSD sort of ch.n (key, idx) pairs over key bits [0, bits): the first
 // pass generates pairs from `first`, later passes read the ping-pong buffers.
-// The sorted idx land in vals_final; *kbuf = index of the sorted key buffer.
+// The sorted idx land in vals_final; *sorted_keys = the sorted key buffer.
+// hist0_ready: the first source's histograms are already computed (per chunk
+// for the reduce-then-scan sort; global, after onesweep_prepare, otherwise).
 template <class Src>
 static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, const Chunking& ch, uint32_t bits,
                       uint32_t* vals_final, uint32_t* vals_other, uint64_t* kb0, uint64_t* kb1, hipStream_t s,
                       Timer& tm, sa_stats* st, uint64_t** sorted_keys, uint32_t* passes, bool hist0_ready = false) {
     const uint32_t P = (bits + 7) / 8;
+    if (P > kMaxPasses) return set_err(SA_E_INTERNAL, "%u radix passes", P);
+    if (c->radix == 0) {
+        const uint64_t n = ch.n;
+        uint32_t* vb[2];
+        vb[(P - 1) & 1] = vals_final;
+        vb[P & 1] = vals_other;
+        uint64_t* kb[2] = {kb0, kb1};
+        if (!hist0_ready) {
+            int rc = onesweep_prepare(c, s);
+            if (rc) return rc;
+            tm.begin(SA_K_HIST_FIRST);
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
+            hipLaunchKernelGGL(k_global_hist<Src>, dim3(grid), dim3(kBlock), 0, s, first, n, P, os_ghist(c));
+            tm.end();
+            add_bytes(st, SA_K_HIST_FIRST, first_bytes);
+        }
+        tm.begin(SA_K_SCAN);
+        hipLaunchKernelGGL(k_digit_base, dim3(P), dim3(kBlock), 0, s, (const uint32_t*)os_ghist(c), os_base(c));
+        tm.end();
+        for (uint32_t p = 0; p < P; ++p) {
+            const uint32_t shift = 8 * p;
+            const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
+            if (p == 0) {
+                tm.begin(SA_K_SCATTER_FIRST);
+                onesweep_pass(c, first, n, shift, nbits, os_base(c), os_tickets(c), kb[0], vb[0], s);
+                tm.end();
+                add_bytes(st, SA_K_SCATTER_FIRST, first_bytes + 12 * n);
+            } else {
+                SrcKeys src{kb[(p - 1) & 1], vb[(p - 1) & 1]};
+                tm.begin(SA_K_SCATTER_KEYS);
+                onesweep_pass(c, src, n, shift, nbits, os_base(c) + p * kRadix, os_tickets(c) + p, kb[p & 1],
+                              vb[p & 1], s);
+                tm.end();
+                add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);
+            }
+        }
+        SA_HIP(hipGetLastError());
+        *sorted_keys = kb[(P - 1) & 1];
+        *passes = P;
+        return SA_OK;
+    }
     uint32_t* vb[2];
     vb[(P - 1) & 1] = vals_final;
     vb[P & 1] = vals_other;
@@ -347,8 +430,9 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         SA_HIP(hipGetLastError());
         add_bytes(st, SA_K_HEADS, 8 * n);
         add_bytes(st, SA_K_HEADS_SCAN, 8ull * ch.chunks);
-        SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipMemcpyAsync(c->host_words, c->words, 20, hipMemcpyDeviceToHost, s));
         SA_HIP(hipStreamSynchronize(s));
+        if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
         const uint64_t Dn = c->host_words[0];
         const bool done = (Dn == n);                  // manber_myers.c:113
         if (!done) {
@@ -432,8 +516,9 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     hipLaunchKernelGGL(k_seg_scan, dim3(1), dim3(kBlock), 0, s, c_h, c_u, c_uh, c_l, ch.chunks, c->words);
     tm.end();
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 12, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 20, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
+    if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
     *D = c->host_words[0];
     *m = c->host_words[1];
     *G = c->host_words[2];
@@ -495,9 +580,13 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const Chunking ch = plan_chunks(n);
     uint64_t top = 1;   // B^(K-1)
     for (uint32_t t = 1; t < K; ++t) top *= base;
+    if (c->radix == 0) {
+        rc = onesweep_prepare(c, s);
+        if (rc) return rc;
+    }
     tm.begin(SA_K_PACK);
     hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, (const uint16_t*)c->code, ch,
-                       base, top, K, c->keys[1], c->hist);
+                       base, top, K, c->keys[1], c->hist, c->radix == 0 ? (bits1 + 7) / 8 : 0u, os_ghist(c));
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_PACK, 9 * n);
@@ -581,6 +670,9 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     int rc = ensure_capacity(c, n);
     if (rc) return rc;
     Timer tm{c, s, opts && opts->profile, st};
+    c->radix = opts ? opts->radix : 0;
+    if (c->radix != 0 && c->radix != 1) return set_err(SA_E_INVALID, "unknown radix algorithm %d", c->radix);
+    SA_HIP(hipMemsetAsync(c->words, 0, 64, s));
     Events ev;
     rc = ev.make();
     if (rc) return rc;
@@ -725,6 +817,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->totals, kRadix * 4) != hipSuccess || hipMalloc(&c->counts, 4 * kMaxChunks * 4) != hipSuccess ||
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
+        hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);
@@ -755,6 +848,7 @@ void sa_context_destroy(sa_context* c) {
     free_u_buffers(c);
     hipFree(c->alpha);
     hipFree(c->code);
+    hipFree(c->os);
     hipFree(c->hist);
     hipFree(c->totals);
     hipFree(c->counts);

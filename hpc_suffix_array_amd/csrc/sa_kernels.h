@@ -534,26 +534,36 @@ __global__ __launch_bounds__(kBlock) void k_byte_hist(const uint8_t* __restrict_
 // packed schedule, round 1 key build: key(i) = sum_t code(i+t) B^(K-1-t),
 // t < K.  One tile of codes (+ K-1 halo) is staged in LDS; each lane builds
 // 16 consecutive keys, the first by Horner, the rest by the rolling update
-// key' = (key - c_out B^(K-1)) B + c_in.  The digit-0 histogram of the first
-// radix pass is taken here as well (same chunking as k_hist), so that pass
-// starts with its scatter.
+// key' = (key - c_out B^(K-1)) B + c_in.  Histograms are taken here too:
+// with passes == 0 the digit-0 histogram per chunk (reduce-then-scan sort,
+// same chunking as k_hist); with passes > 0 the global histograms of all
+// passes' digits (single-pass sort, ghist[passes][256]).
 // ---------------------------------------------------------------------------
 constexpr int kPackRun = kTile / kBlock;   // 16 consecutive keys per lane
 constexpr int kMaxK = 64;
+constexpr int kPackMaxPasses = 8;
 
 __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict__ text,
                                                       const uint16_t* __restrict__ code, Chunking ch,
                                                       uint64_t base, uint64_t top, uint32_t K,
-                                                      uint64_t* __restrict__ keys, uint32_t* __restrict__ hist) {
+                                                      uint64_t* __restrict__ keys, uint32_t* __restrict__ hist,
+                                                      uint32_t passes, uint32_t* __restrict__ ghist) {
     __shared__ uint16_t s_code[256];
     __shared__ uint16_t s_c[kTile + kMaxK];
-    __shared__ uint32_t s_hist[kWaves][kRadix];
+    __shared__ uint32_t s_hist[kPackMaxPasses][kRadix];
     s_code[threadIdx.x] = code[threadIdx.x];
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < kPackMaxPasses * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
     const uint64_t n = ch.n;
-    uint32_t* my = s_hist[wave_id()];
+    uint32_t* my = s_hist[passes ? 0u : wave_id()];
+    auto count = [&](uint64_t key) {
+        if (passes == 0) {
+            atomicAdd(&my[key & 0xFFu], 1u);
+        } else {
+            for (uint32_t p = 0; p < passes; ++p) atomicAdd(&s_hist[p][(key >> (8 * p)) & 0xFFu], 1u);
+        }
+    };
     __syncthreads();
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         for (uint32_t q = threadIdx.x; q < (uint32_t)kTile + K; q += kBlock) {
@@ -578,23 +588,30 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
             for (int j = 0; j < kPackRun; j += 2) {
                 dst[j / 2] = make_uint4((uint32_t)out[j], (uint32_t)(out[j] >> 32), (uint32_t)out[j + 1],
                                         (uint32_t)(out[j + 1] >> 32));
-                atomicAdd(&my[out[j] & 0xFFu], 1u);
-                atomicAdd(&my[out[j + 1] & 0xFFu], 1u);
+                count(out[j]);
+                count(out[j + 1]);
             }
         } else {
 #pragma unroll
             for (int j = 0; j < kPackRun; ++j)
                 if (g0 + j < e1) {
                     keys[g0 + j] = out[j];
-                    atomicAdd(&my[out[j] & 0xFFu], 1u);
+                    count(out[j]);
                 }
         }
         __syncthreads();
     }
-    uint32_t s = 0;
+    if (passes == 0) {
+        uint32_t s = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) s += s_hist[w][threadIdx.x];
-    hist[(uint64_t)threadIdx.x * ch.chunks + c] = s;
+        for (int w = 0; w < kWaves; ++w) s += s_hist[w][threadIdx.x];
+        hist[(uint64_t)threadIdx.x * ch.chunks + c] = s;
+    } else {
+        for (uint32_t p = 0; p < passes; ++p) {
+            const uint32_t v = s_hist[p][threadIdx.x];
+            if (v) atomicAdd(&ghist[p * kRadix + threadIdx.x], v);
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------

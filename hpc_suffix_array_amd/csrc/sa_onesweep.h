@@ -1,0 +1,199 @@
+// sa_onesweep.h -- single-pass LSD radix passes with decoupled look-back
+// (the per-pass sort of one doubling round, replacing the two stable
+// counting passes of radix_sort_suffixes_seq, manber_myers.c:37-48).
+//
+// Per sort:
+//   k_global_hist  one read of the pass-0 source -> digit totals of EVERY
+//                  pass (the multiset of keys is the same in all passes)
+//                  (k_pack_text computes them itself for the packed round 1)
+//   k_digit_base   exclusive scan of each pass's 256 totals
+// Per pass (one launch, one tile per workgroup, tile ids from an atomic
+// ticket so a tile only ever waits on tiles that are already running):
+//   1. load the tile, rank it stably per wave (match-any from ballots)
+//   2. publish the tile's per-digit count (AGGREGATE) in its state words
+//   3. look back over predecessors, summing AGGREGATEs until an INCLUSIVE
+//      prefix; publish this tile's INCLUSIVE prefix
+//   4. stage the tile digit-sorted in LDS, write each digit run to
+//      digit_base[d] + exclusive prefix + offset in run
+// State words are 64-bit agent-scope atomics holding {status, epoch, count}:
+// the data is its own flag (MI355X_MICROARCH.md "R2" granule), so no fences;
+// the epoch makes a stale word from an earlier pass read as "not ready".
+#pragma once
+#include "sa_kernels.h"
+
+namespace sa {
+
+constexpr uint64_t kStAgg = 1ull << 62;
+constexpr uint64_t kStPrefix = 2ull << 62;
+constexpr uint32_t kEpochBits = 14;
+constexpr uint32_t kEpochMask = (1u << kEpochBits) - 1u;
+constexpr uint64_t kCountMask = (1ull << 48) - 1ull;
+constexpr uint32_t kMaxPasses = 8;
+constexpr uint32_t kSpinLimit = 1u << 26;
+
+__device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// digit histograms of all `passes` 8-bit digits of the source keys
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_global_hist(Src src, uint64_t n, uint32_t passes,
+                                                        uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t s_h[kMaxPasses][kRadix];
+    for (int i = threadIdx.x; i < (int)(kMaxPasses * kRadix); i += kBlock) (&s_h[0][0])[i] = 0;
+    __syncthreads();
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = src.key(e);
+        for (uint32_t p = 0; p < passes; ++p) atomicAdd(&s_h[p][(k >> (8 * p)) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t v = s_h[p][threadIdx.x];
+        if (v) atomicAdd(&ghist[p * kRadix + threadIdx.x], v);
+    }
+}
+
+// base[p][d] = sum of ghist[p][d'] for d' < d; one workgroup per pass
+__global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restrict__ ghist,
+                                                       uint32_t* __restrict__ base) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint32_t p = blockIdx.x;
+    base[p * kRadix + threadIdx.x] = block_exclusive_sum(ghist[p * kRadix + threadIdx.x], s_tmp, nullptr);
+}
+
+template <class Src, int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
+                                                    const uint32_t* __restrict__ digit_base,
+                                                    uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
+                                                    uint32_t epoch, uint64_t* __restrict__ out_keys,
+                                                    uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr int WTILE = kWave * ITEMS;
+    static_assert(BLOCK >= kRadix, "one thread per digit");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_vals[TILE];
+    __shared__ uint32_t s_wcnt[WAVES][kRadix];
+    __shared__ uint32_t s_start[kRadix];
+    __shared__ uint32_t s_gofs[kRadix];
+    __shared__ uint32_t s_tmp[kWaves];
+    __shared__ uint32_t s_tile;
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t mask = (1u << nbits) - 1u;
+    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    for (int i = threadIdx.x; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const uint64_t t = s_tile;
+    const uint64_t tb = t * TILE;
+    const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    uint32_t d[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t le = wave * WTILE + j * kWave + lane;
+        const bool ok = le < valid;
+        k[j] = ok ? src.key(tb + le) : 0ull;
+        v[j] = ok ? src.val(tb + le) : 0u;
+        d[j] = ok ? (uint32_t)(k[j] >> shift) & mask : kRadix;
+    }
+    uint32_t r[ITEMS];
+    uint32_t* wc = s_wcnt[wave];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const bool ok = d[j] < (uint32_t)kRadix;
+        uint64_t peers = __ballot(ok);
+        for (uint32_t b = 0; b < nbits; ++b) {
+            const bool bit = (d[j] >> b) & 1u;
+            const uint64_t bal = __ballot(bit);
+            peers &= bit ? bal : ~bal;
+        }
+        uint32_t cnt = 0;
+        if (ok) cnt = wc[d[j]];
+        const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+        r[j] = cnt + below;
+        if (ok && below == 0) wc[d[j]] = cnt + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+
+    const uint32_t dg = threadIdx.x;   // digit owned by this thread (dg < 256)
+    uint32_t tile_cnt = 0;
+    if (dg < (uint32_t)kRadix) {
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) {
+            const uint32_t x = s_wcnt[w][dg];
+            s_wcnt[w][dg] = tile_cnt;
+            tile_cnt += x;
+        }
+        const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
+        st_store(&states[t * kRadix + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+    }
+    // tile layout: exclusive scan of the per-digit counts (threads >= 256 add 0)
+    {
+        const uint32_t x = (dg < (uint32_t)kRadix) ? tile_cnt : 0u;
+        const uint32_t inc = wave_inclusive_sum(x);
+        if (lane == kWave - 1 && wave < (uint32_t)kWaves) s_tmp[wave] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+        if (dg < (uint32_t)kRadix) s_start[dg] = off + inc - x;
+    }
+    // look back (one thread per digit)
+    if (dg < (uint32_t)kRadix) {
+        uint64_t excl = 0;
+        if (t > 0) {
+            int64_t tp = (int64_t)t - 1;
+            uint32_t spins = 0;
+            while (tp >= 0) {
+                const uint64_t s = st_load(&states[(uint64_t)tp * kRadix + dg]);
+                const uint32_t ep = (uint32_t)(s >> 48) & kEpochMask;
+                const uint64_t status = s & (3ull << 62);
+                if (ep != (epoch & kEpochMask) || status == 0) {
+                    if (++spins > kSpinLimit) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += s & kCountMask;
+                if (status == kStPrefix) break;
+                --tp;
+            }
+            const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
+            st_store(&states[t * kRadix + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
+        }
+        s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        if (d[j] < (uint32_t)kRadix) {
+            const uint32_t pos = s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
+            s_keys[pos] = k[j];
+            s_vals[pos] = v[j];
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + threadIdx.x;
+        if (q < valid) {
+            const uint64_t key = s_keys[q];
+            const uint32_t dd = (uint32_t)(key >> shift) & mask;
+            const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+            if (g < n) {
+                out_keys[g] = key;
+                out_vals[g] = s_vals[q];
+            }
+        }
+    }
+}
+
+}  // namespace sa

@@ -63,7 +63,9 @@ typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
     int32_t schedule;       /* SA_SCHEDULE_* */
     int32_t init_chars;     /* packed schedule: symbols in the first key, 0 = auto */
-    int32_t reserved[5];
+    int32_t radix;          /* 0: single-pass radix (decoupled look-back, default);
+                               1: reduce-then-scan radix (3 kernels per pass) */
+    int32_t reserved[4];
 } sa_opts;
 
 typedef struct {

@@ -68,6 +68,18 @@ def test_random_vs_oracle(gpu, oracle, kind, n, schedule):
         assert st["distinct"][-1] == n
 
 
+@pytest.mark.parametrize("schedule", ["packed", "reference"])
+@pytest.mark.parametrize("radix", ["onesweep", "reduce_scan"])
+def test_radix_algorithms(gpu, oracle, schedule, radix):
+    """Both radix sorts (single-pass look-back / reduce-then-scan) under both
+    schedules, across tile and chunk boundaries."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for kind, n in (("dna", 4096 * 3 + 17), ("byte256", 1 << 18), ("alnum", 2_500_001), ("binary", 333_333)):
+        t = oracle.gen_text(kind, n, seed=n)
+        got = build_suffix_array(t, schedule=schedule, radix=radix)
+        assert (got == oracle.sa_c(t)).all(), (kind, n)
+
+
 @pytest.mark.parametrize("init_chars", [1, 2, 3, 5])
 @pytest.mark.parametrize("kind", ["dna", "binary", "alnum"])
 def test_packed_short_first_key(gpu, oracle, kind, init_chars):
