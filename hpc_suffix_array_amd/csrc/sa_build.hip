@@ -300,7 +300,10 @@ static void onesweep_pass(sa_context* c, const Src& src, uint64_t n, uint32_t sh
                           hipStream_t s) {
     const uint64_t tiles = (n + kTile - 1) / kTile;
     const uint32_t epoch = next_epoch(c, s, tiles);
-    hipLaunchKernelGGL((k_onesweep<Src, kBlock, kItems>), dim3((uint32_t)tiles), dim3(kBlock), 0, s, src, n, shift,
+    // 1024 x 4: 16 waves per tile, 2 workgroups (32 waves) per CU -- the
+    // fastest shape in microbench.hip (r01: 10.4 ms per 2^30-pair pass)
+    static_assert(kOsBlock * kOsItems == kTile, "tile states are sized for kTile");
+    hipLaunchKernelGGL((k_onesweep<Src, kOsBlock, kOsItems>), dim3((uint32_t)tiles), dim3(kOsBlock), 0, s, src, n, shift,
                        nbits, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
 }
 
@@ -550,22 +553,22 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     rc = ensure_u_capacity(c, n);
     if (rc) return rc;
     SA_HIP(hipEventRecord(ev.e[0], s));
-    // alphabet -> dense codes (host reads 256 counts)
+    // alphabet -> dense codes (host reads the 256-bit presence mask)
     uint32_t* h_alpha = c->host_words + 64;
     uint16_t* h_code = reinterpret_cast<uint16_t*>(c->host_words + 320);
-    SA_HIP(hipMemsetAsync(c->alpha, 0, 256 * 4, s));
+    SA_HIP(hipMemsetAsync(c->alpha, 0, 8 * 4, s));
     tm.begin(SA_K_ALPHABET);
     {
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 1024);
-        hipLaunchKernelGGL(k_byte_hist, dim3(grid), dim3(kBlock), 0, s, d_text, n, c->alpha);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 2048);
+        hipLaunchKernelGGL(k_alphabet, dim3(grid), dim3(kBlock), 0, s, d_text, n, c->alpha);
     }
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_ALPHABET, n);
-    SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 256 * 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 8 * 4, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     uint32_t sigma = 0;
-    for (int b = 0; b < 256; ++b) h_code[b] = h_alpha[b] ? (uint16_t)(++sigma) : 0;
+    for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
     const uint32_t K = choose_chars(sigma, n, opts ? opts->init_chars : 0);
     const uint64_t base = (uint64_t)sigma + 1;

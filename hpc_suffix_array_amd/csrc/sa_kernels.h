@@ -501,33 +501,38 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
 }
 
 // ---------------------------------------------------------------------------
-// alphabet: 256-bin byte histogram (per-wave LDS bins, one global atomic per
-// bin per block).  The host turns it into dense codes 1..sigma.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_byte_hist(const uint8_t* __restrict__ text, uint64_t n,
-                                                      uint32_t* __restrict__ counts) {
-    __shared__ uint32_t s_h[kWaves][kRadix];
-    for (int i = threadIdx.x; i < kWaves * kRadix; i += kBlock) (&s_h[0][0])[i] = 0;
-    __syncthreads();
-    uint32_t* my = s_h[wave_id()];
+// alphabet presence: bit b of present[b >> 5] is set when byte b occurs.
+// Presence is all the dense codes need; it is kept in 8 registers per lane
+// (no LDS atomics, so a 4-symbol text costs no bank conflicts), OR-reduced
+// over the wave, one atomicOr per word per wave.
+__global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__ text, uint64_t n,
+                                                     uint32_t* __restrict__ present) {
+    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    auto add = [&](uint32_t b) {
+        const uint32_t bit = 1u << (b & 31u), w = b >> 5;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) m[i] |= (w == (uint32_t)i) ? bit : 0u;
+    };
     const uint64_t stride = (uint64_t)gridDim.x * kBlock * 16;
     for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16; i < n; i += stride) {
         if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
             const uint4 v = *reinterpret_cast<const uint4*>(text + i);
-            const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+            const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) atomicAdd(&my[(w[q] >> (8 * b)) & 0xFFu], 1u);
+                for (int b = 0; b < 4; ++b) add((w4[q] >> (8 * b)) & 0xFFu);
         } else {
-            for (uint64_t j = i; j < n && j < i + 16; ++j) atomicAdd(&my[text[j]], 1u);
+            for (uint64_t j = i; j < n && j < i + 16; ++j) add(text[j]);
         }
     }
-    __syncthreads();
-    uint32_t s = 0;
 #pragma unroll
-    for (int w = 0; w < kWaves; ++w) s += s_h[w][threadIdx.x];
-    if (s) atomicAdd(&counts[threadIdx.x], s);
+    for (int i = 0; i < 8; ++i) {
+        uint32_t x = m[i];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o, kWave);
+        if (lane_id() == 0 && x) atomicOr(&present[i], x);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -551,6 +556,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
     __shared__ uint16_t s_code[256];
     __shared__ uint16_t s_c[kTile + kMaxK];
     __shared__ uint32_t s_hist[kPackMaxPasses][kRadix];
+    // keys staged for a coalesced store; one u64 of padding per 16 keys keeps
+    // the lane-strided writes (16 keys apart) off a single LDS bank
+    __shared__ uint64_t s_k[kTile + kTile / kPackRun];
     s_code[threadIdx.x] = code[threadIdx.x];
     for (int i = threadIdx.x; i < kPackMaxPasses * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
     const uint32_t c = blockIdx.x;
@@ -566,38 +574,43 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
     };
     __syncthreads();
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
-        for (uint32_t q = threadIdx.x; q < (uint32_t)kTile + K; q += kBlock) {
-            const uint64_t i = tb + q;
-            s_c[q] = (i < n) ? s_code[text[i]] : (uint16_t)0;
+        {   // 16 text bytes per lane (one dwordx4), then the K-1 halo
+            const uint64_t i = tb + (uint64_t)threadIdx.x * 16;
+            uint16_t* dst = s_c + threadIdx.x * 16;
+            if (i + 16 <= n) {
+                const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) dst[4 * q + b] = s_code[(w4[q] >> (8 * b)) & 0xFFu];
+            } else {
+                for (int q = 0; q < 16; ++q) dst[q] = (i + q < n) ? s_code[text[i + q]] : (uint16_t)0;
+            }
+            if (threadIdx.x < K) {
+                const uint64_t h = tb + kTile + threadIdx.x;
+                s_c[kTile + threadIdx.x] = (h < n) ? s_code[text[h]] : (uint16_t)0;
+            }
         }
         __syncthreads();
         const uint32_t l0 = threadIdx.x * kPackRun;
         uint64_t x = 0;
         for (uint32_t t = 0; t < K; ++t) x = x * base + s_c[l0 + t];
-        uint64_t out[kPackRun];
-        out[0] = x;
+        uint64_t* kd = s_k + threadIdx.x * (kPackRun + 1);
+        kd[0] = x;
+        if (tb + l0 < e1) count(x);
 #pragma unroll
         for (int j = 1; j < kPackRun; ++j) {
             x = (x - (uint64_t)s_c[l0 + j - 1] * top) * base + s_c[l0 + j - 1 + K];
-            out[j] = x;
+            kd[j] = x;
+            if (tb + l0 + j < e1) count(x);
         }
-        const uint64_t g0 = tb + l0;
-        if (g0 + kPackRun <= e1) {
-            uint4* dst = reinterpret_cast<uint4*>(keys + g0);
+        __syncthreads();
 #pragma unroll
-            for (int j = 0; j < kPackRun; j += 2) {
-                dst[j / 2] = make_uint4((uint32_t)out[j], (uint32_t)(out[j] >> 32), (uint32_t)out[j + 1],
-                                        (uint32_t)(out[j + 1] >> 32));
-                count(out[j]);
-                count(out[j + 1]);
-            }
-        } else {
-#pragma unroll
-            for (int j = 0; j < kPackRun; ++j)
-                if (g0 + j < e1) {
-                    keys[g0 + j] = out[j];
-                    count(out[j]);
-                }
+        for (int j = 0; j < kPackRun; ++j) {
+            const uint32_t q = j * kBlock + threadIdx.x;
+            const uint64_t g = tb + q;
+            if (g < e1) keys[g] = s_k[q + q / kPackRun];
         }
         __syncthreads();
     }
@@ -631,13 +644,20 @@ struct PosArray {
     __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return p[s]; }
 };
 
+// one row of 64 consecutive sorted keys starting at rb (s = rb + lane); the
+// neighbours come from the adjacent lanes, only lanes 0 / 63 load one more key
 __device__ __forceinline__ void seg_masks(const uint64_t* __restrict__ keys, uint64_t s, uint64_t m,
                                           uint64_t& mf, uint64_t& mu, uint64_t& muh) {
+    const uint32_t lane = lane_id();
+    const uint64_t k = s < m ? keys[s] : ~0ull;
+    uint64_t prev = __shfl_up(k, 1, kWave);
+    uint64_t next = __shfl_down(k, 1, kWave);
+    if (lane == 0) prev = (s > 0 && s - 1 < m) ? keys[s - 1] : ~k;
+    if (lane == kWave - 1) next = (s + 1 < m) ? keys[s + 1] : ~k;
     bool f = false, u = false;
     if (s < m) {
-        const uint64_t k = keys[s];
-        f = (s == 0) || keys[s - 1] != k;
-        const bool nf = (s + 1 >= m) || keys[s + 1] != k;
+        f = (s == 0) || prev != k;
+        const bool nf = (s + 1 >= m) || next != k;
         u = !(f && nf);
     }
     mf = __ballot(f);
@@ -776,6 +796,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
         uint32_t cu = 0, cuh = 0, lf = 0;
+#pragma unroll 4
         for (int j = 0; j < kItems; ++j) {
             const uint64_t rb = w0 + (uint64_t)j * kWave;
             uint64_t mf = 0, mu = 0, muh = 0;
@@ -814,12 +835,14 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
             tuh += b;
             tl = l > tl ? l : tl;
         }
+#pragma unroll 2
         for (int j = 0; j < kItems; ++j) {
             const uint64_t rb = w0 + (uint64_t)j * kWave;
             if (rb >= e1) break;
             const uint64_t mf = s_m[wave][j][0], mu = s_m[wave][j][1], muh = s_m[wave][j][2];
             const uint64_t s = rb + lane;
-            if (s < e1) {
+            // sparse first round: rows without unsorted members write nothing
+            if ((dense_rank || sa || mu) && s < e1) {
                 const uint64_t mh = mf & le;
                 const uint64_t hs = mh ? rb + 63 - __clzll(mh) : (uint64_t)carried - 1u;
                 const uint32_t x = idx[s];

@@ -30,6 +30,8 @@ constexpr uint32_t kEpochMask = (1u << kEpochBits) - 1u;
 constexpr uint64_t kCountMask = (1ull << 48) - 1ull;
 constexpr uint32_t kMaxPasses = 8;
 constexpr uint32_t kSpinLimit = 1u << 26;
+constexpr int kOsBlock = 1024;   // product shape of k_onesweep
+constexpr int kOsItems = 4;
 
 __device__ __forceinline__ uint64_t st_load(const uint64_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -64,7 +66,10 @@ __global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restric
     base[p * kRadix + threadIdx.x] = block_exclusive_sum(ghist[p * kRadix + threadIdx.x], s_tmp, nullptr);
 }
 
-template <class Src, int BLOCK, int ITEMS>
+// kVariant (microbenchmarks only; 0 in the product): bit 0 skips the look-back
+// (tile offsets faked), bit 1 skips the ranking (identity layout), bit 2
+// skips the LDS staging (writes straight from registers).
+template <class Src, int BLOCK, int ITEMS, int kVariant = 0>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
                                                     const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
@@ -74,17 +79,29 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     constexpr int TILE = BLOCK * ITEMS;
     constexpr int WTILE = kWave * ITEMS;
     static_assert(BLOCK >= kRadix, "one thread per digit");
+    static_assert(TILE <= 65535, "16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint32_t s_vals[TILE];
-    __shared__ uint32_t s_wcnt[WAVES][kRadix];
-    __shared__ uint32_t s_start[kRadix];
+    __shared__ uint16_t s_wcnt[WAVES][kRadix];   // per-wave digit counts, then wave offsets
+    __shared__ uint16_t s_start[kRadix];         // digit run starts in the tile
     __shared__ uint32_t s_gofs[kRadix];
     __shared__ uint32_t s_tmp[kWaves];
     __shared__ uint32_t s_tile;
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t mask = (1u << nbits) - 1u;
-    if (threadIdx.x == 0) s_tile = atomicAdd(ticket, 1u);
+    if (threadIdx.x == 0) {
+        uint32_t tk = atomicAdd(ticket, 1u);
+        if constexpr ((kVariant & 8) != 0) {
+            // microbenchmark only: consecutive tiles on one XCD (blocks are
+            // dealt round-robin over the 8 XCDs); unsafe with the look-back
+            const uint32_t tiles = (uint32_t)((n + TILE - 1) / TILE);
+            const uint32_t g = tk / 64, j = tk % 64;
+            const uint32_t cand = g * 64 + (j % 8) * 8 + j / 8;
+            tk = cand < tiles ? cand : tk;
+        }
+        s_tile = tk;
+    }
     for (int i = threadIdx.x; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t t = s_tile;
@@ -103,21 +120,26 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         d[j] = ok ? (uint32_t)(k[j] >> shift) & mask : kRadix;
     }
     uint32_t r[ITEMS];
-    uint32_t* wc = s_wcnt[wave];
+    uint16_t* wc = s_wcnt[wave];
+    if constexpr ((kVariant & 2) == 0) {
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        const bool ok = d[j] < (uint32_t)kRadix;
-        uint64_t peers = __ballot(ok);
-        for (uint32_t b = 0; b < nbits; ++b) {
-            const bool bit = (d[j] >> b) & 1u;
-            const uint64_t bal = __ballot(bit);
-            peers &= bit ? bal : ~bal;
+        for (int j = 0; j < ITEMS; ++j) {
+            const bool ok = d[j] < (uint32_t)kRadix;
+            uint64_t peers = __ballot(ok);
+            for (uint32_t b = 0; b < nbits; ++b) {
+                const bool bit = (d[j] >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint32_t cnt = 0;
+            if (ok) cnt = wc[d[j]];
+            const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+            r[j] = cnt + below;
+            if (ok && below == 0) wc[d[j]] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
         }
-        uint32_t cnt = 0;
-        if (ok) cnt = wc[d[j]];
-        const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
-        r[j] = cnt + below;
-        if (ok && below == 0) wc[d[j]] = cnt + (uint32_t)__popcll(peers);
+    } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) r[j] = j * kWave + lane;
     }
     __syncthreads();
 
@@ -127,7 +149,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) {
             const uint32_t x = s_wcnt[w][dg];
-            s_wcnt[w][dg] = tile_cnt;
+            s_wcnt[w][dg] = (uint16_t)tile_cnt;
             tile_cnt += x;
         }
         const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
@@ -142,29 +164,49 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         uint32_t off = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
-        if (dg < (uint32_t)kRadix) s_start[dg] = off + inc - x;
+        if (dg < (uint32_t)kRadix) s_start[dg] = (uint16_t)(off + inc - x);
     }
     // look back (one thread per digit)
     if (dg < (uint32_t)kRadix) {
         uint64_t excl = 0;
-        if (t > 0) {
+        if constexpr ((kVariant & 1) != 0) {
+            excl = t * (uint64_t)(TILE / kRadix);
+        } else if (t > 0) {
+            // read kLook predecessors per step (independent loads: one
+            // fabric round trip per kLook tiles instead of per tile)
+            constexpr int kLook = 4;
             int64_t tp = (int64_t)t - 1;
             uint32_t spins = 0;
+            const uint32_t ep_now = epoch & kEpochMask;
             while (tp >= 0) {
-                const uint64_t s = st_load(&states[(uint64_t)tp * kRadix + dg]);
-                const uint32_t ep = (uint32_t)(s >> 48) & kEpochMask;
-                const uint64_t status = s & (3ull << 62);
-                if (ep != (epoch & kEpochMask) || status == 0) {
+                uint64_t sv[kLook];
+#pragma unroll
+                for (int i = 0; i < kLook; ++i)
+                    sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * kRadix + dg]) : 0ull;
+                int used = 0;
+                bool done = false;
+#pragma unroll
+                for (int i = 0; i < kLook; ++i) {
+                    if (done || used != i) break;
+                    if (tp - i < 0) {
+                        done = true;
+                        break;
+                    }
+                    const uint64_t status = sv[i] & (3ull << 62);
+                    if (((uint32_t)(sv[i] >> 48) & kEpochMask) != ep_now || status == 0) break;
+                    excl += sv[i] & kCountMask;
+                    ++used;
+                    if (status == kStPrefix) done = true;
+                }
+                if (done) break;
+                tp -= used;
+                if (used == 0) {
                     if (++spins > kSpinLimit) {
                         atomicOr(err, 1u);
                         break;
                     }
                     __builtin_amdgcn_s_sleep(1);
-                    continue;
                 }
-                excl += s & kCountMask;
-                if (status == kStPrefix) break;
-                --tp;
             }
             const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
             st_store(&states[t * kRadix + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
@@ -172,10 +214,25 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
     }
     __syncthreads();
+    if constexpr ((kVariant & 4) != 0) {
+        // no LDS staging: scatter straight from registers
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (d[j] < (uint32_t)kRadix) {
+                const uint64_t g = (uint64_t)s_gofs[d[j]] + s_wcnt[wave][d[j]] + r[j];
+                if (g < n) {
+                    out_keys[g] = k[j];
+                    out_vals[g] = v[j];
+                }
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         if (d[j] < (uint32_t)kRadix) {
-            const uint32_t pos = s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
+            const uint32_t pos = (kVariant & 2) ? (uint32_t)(wave * WTILE) + r[j]
+                                                : s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
             s_keys[pos] = k[j];
             s_vals[pos] = v[j];
         }
