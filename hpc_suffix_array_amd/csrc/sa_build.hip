@@ -61,7 +61,9 @@ static bool trace_on() {
         }                                               \
     } while (0)
 
-constexpr uint32_t kMaxChunks = 1024;
+// chunks of the chunked (tile-sequential) kernels: 4096 workgroups keep 16
+// per CU in flight on the 256 CUs
+constexpr uint32_t kMaxChunks = 4096;
 // sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
 constexpr uint64_t kSparseDiv = 8;
 constexpr int kEvPool = 256;

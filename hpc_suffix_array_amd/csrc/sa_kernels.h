@@ -644,6 +644,41 @@ struct PosArray {
     __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return p[s]; }
 };
 
+// Keys of one wave's 16 rows of 64 (s = w0 + 64 j + lane), all loads issued
+// before any is used; lane 0 / 63 also fetch the key before / after its row.
+struct SegRows {
+    uint64_t k[kItems], lo[kItems];
+    __device__ __forceinline__ void load(const uint64_t* __restrict__ keys, uint64_t w0, uint64_t m) {
+        const uint32_t lane = lane_id();
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t s = w0 + (uint64_t)j * kWave + lane;
+            k[j] = s < m ? keys[s] : ~0ull;
+            const uint64_t nb = lane == 0 ? s - 1 : s + 1;   // lanes 1..62 load nothing extra
+            const bool edge = (lane == 0 && s > 0 && s - 1 < m) || (lane == kWave - 1 && s + 1 < m);
+            lo[j] = edge ? keys[nb] : 0ull;
+        }
+    }
+};
+
+__device__ __forceinline__ void seg_masks_reg(uint64_t k, uint64_t edge, uint64_t s, uint64_t m, uint64_t& mf,
+                                              uint64_t& mu, uint64_t& muh) {
+    const uint32_t lane = lane_id();
+    uint64_t prev = __shfl_up(k, 1, kWave);
+    uint64_t next = __shfl_down(k, 1, kWave);
+    if (lane == 0) prev = edge;
+    if (lane == kWave - 1) next = edge;
+    bool f = false, u = false;
+    if (s < m) {
+        f = (s == 0) || prev != k;
+        const bool nf = (s + 1 >= m) || next != k;
+        u = !(f && nf);
+    }
+    mf = __ballot(f);
+    mu = __ballot(u);
+    muh = __ballot(f && u);
+}
+
 // one row of 64 consecutive sorted keys starting at rb (s = rb + lane); the
 // neighbours come from the adjacent lanes, only lanes 0 / 63 load one more key
 __device__ __forceinline__ void seg_masks(const uint64_t* __restrict__ keys, uint64_t s, uint64_t m,
@@ -676,13 +711,16 @@ __global__ __launch_bounds__(kBlock) void k_seg_count(const uint64_t* __restrict
     uint32_t nh = 0, nu = 0, nuh = 0, last = 0;
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave_id() * kWaveTile;
+        SegRows rows;
+        rows.load(keys, w0, ch.n);
+#pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t rb = w0 + (uint64_t)j * kWave;
-            if (rb >= e1) break;
             uint64_t mf, mu, muh;
             // neighbours are compared across chunk borders (global m = ch.n);
             // lanes past the chunk end are counted by the next chunk
-            seg_masks(keys, rb + lane_id(), ch.n, mf, mu, muh);
+            seg_masks_reg(rows.k[j], rows.lo[j], rb + lane_id(), ch.n, mf, mu, muh);
+            if (rb >= e1) continue;
             const uint64_t lim = e1 - rb >= 64 ? ~0ull : ((1ull << (e1 - rb)) - 1ull);
             mf &= lim;
             mu &= lim;
@@ -796,12 +834,16 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
         uint32_t cu = 0, cuh = 0, lf = 0;
-#pragma unroll 4
+        SegRows rows;
+        rows.load(keys, w0, ch.n);
+#pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t rb = w0 + (uint64_t)j * kWave;
             uint64_t mf = 0, mu = 0, muh = 0;
-            if (rb < e1) {
-                seg_masks(keys, rb + lane, ch.n, mf, mu, muh);
+            seg_masks_reg(rows.k[j], rows.lo[j], rb + lane, ch.n, mf, mu, muh);
+            if (rb >= e1) {
+                mf = mu = muh = 0;
+            } else {
                 const uint64_t lim = e1 - rb >= 64 ? ~0ull : ((1ull << (e1 - rb)) - 1ull);
                 mf &= lim;
                 mu &= lim;
