@@ -1,0 +1,90 @@
+"""The benchmark entry points and the CLI contract (reference
+scripts/benchmark_sequential.py, src/sequential/main_sequential.c)."""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "scripts"))
+
+CLI_TEXT = """Reading from file: test_data/banana.txt
+Actual string length: 6
+
+=== RESULTS ===
+Valid suffix array: YES
+Longest repeated substring: 'ana' (length: 3)
+Total execution time: 0.001234 seconds
+
+===STRUCTURED_RESULTS===
+IMPLEMENTATION:sequential
+TOTAL_TIME:0.001234
+SA_TIME:0.001000
+LCP_TIME:0.000234
+===END_RESULTS===
+"""
+
+
+def test_parse_output_contract():
+    import benchmark_sequential as B
+    r = B.parse_output(CLI_TEXT)
+    assert r["lrs_length"] == 3 and r["lrs_string"] == "ana"
+    assert r["suffix_array_length"] == 6
+    assert r["total_time"] == pytest.approx(0.001234)
+    assert r["sa_time"] == pytest.approx(0.001) and r["lcp_time"] == pytest.approx(0.000234)
+
+
+def test_csv_schema_is_the_references():
+    import benchmark_sequential as B
+    # reference scripts/benchmark_sequential.py:192-209, in order
+    assert B.CSV_COLUMNS == ["file", "size_bytes", "size_mb", "backend", "time_seconds", "throughput_mb_s",
+                             "throughput_chars_per_second", "lrs_length", "lrs_string", "suffix_array_length",
+                             "execution_details", "total_time", "sa_time", "lcp_time", "success", "timestamp"]
+
+
+def test_dataset_generator_matches_oracle(tmp_path, oracle):
+    import generate_large_datasets as G
+    t = G.splitmix_text(G.ALNUM, 100_000, 1)
+    assert t == oracle.gen_text("alnum", 100_000, seed=1).tobytes()
+    G.main(["--sizes", "1", "--out", str(tmp_path)])
+    data = (tmp_path / "large" / "random_1MB.txt").read_bytes()
+    assert oracle.sha256(np.frombuffer(data, np.uint8)).startswith("cd3b75303b322388")   # config 1 text
+
+
+def test_cli_builds_and_refuses_without_gpu(sa_lib):
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools")], check=True)
+    exe = os.path.join(ROOT, "bin", "main_sequential")
+    r = subprocess.run([exe], capture_output=True, text=True)
+    assert r.returncode == 1 and "Usage" in r.stdout
+    if sa_lib.device_count() == 0:
+        r = subprocess.run([exe, "banana"], capture_output=True, text=True)
+        assert r.returncode == 1 and "no HIP device" in r.stderr
+
+
+@pytest.mark.gpu
+def test_cli_and_shim_on_gpu(gpu, oracle, tmp_path):
+    import benchmark_sequential as B
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools")], check=True)
+    files = []
+    for name, text in (("banana.txt", b"banana"), ("mississippi.txt", b"mississippi"),
+                       ("rand.txt", oracle.gen_text("alnum", 300_000, seed=3).tobytes())):
+        p = tmp_path / name
+        p.write_bytes(text)
+        files.append(str(p))
+    for f in files:
+        t = np.frombuffer(open(f, "rb").read(), np.uint8)
+        sa = oracle.sa_c(t)
+        want = oracle.lrs_c(t, sa, oracle.lcp_c(t, sa)).decode("latin-1")
+        for cli in (False, True):
+            r = B.run_benchmark(f, use_cli=cli)
+            assert r["success"], r["error"]
+            assert r["lrs_string"] == want and r["lrs_length"] == len(want)
+            assert r["suffix_array_length"] == len(t)
+            assert "Valid suffix array: YES" in r["output"]
+    out = tmp_path / "res.csv"
+    assert B.main(["--files"] + files + ["--out", str(out)]) == 0
+    import pandas as pd
+    df = pd.read_csv(out)
+    assert list(df.columns) == B.CSV_COLUMNS and len(df) == 3
