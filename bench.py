@@ -5,19 +5,22 @@ BASELINE.json metric: "suffixes sorted/sec + ms/doubling-round, 1 GiB input
 at 1/2/4/8 MI355X".  Workload (configs[2]): 1 GiB (n = 2^30) random DNA,
 seeded splitmix64, generated directly in HBM.  One step =
 one complete suffix-array construction (every doubling round: radix passes,
-re-rank, D_j read-back) from text resident in HBM to SA resident in HBM.
+re-rank, read-backs) from text resident in HBM to SA resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n N] [--kind dna]
 
-N > 1 is launched by torch.distributed.run (one process per GPU); in this
-round each rank builds the SA of its own 1 GiB string (independent replicas,
-weak scaling, no data-path collective -- DESIGN.md "Multi-GPU").
+N = 1: the single-GPU builder (libsa_hip sa_build_device).
+N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
+range-partitioned build of ONE n-symbol string over all ranks
+(hpc_suffix_array_amd/distributed.py) -- total work fixed, "scaling":
+"strong"; `--mode replicas` instead builds one string per rank (weak).
 
 Output: one JSON line on rank 0 with the driver's contract keys plus
-"roofline" (dominant kernel: the radix scatter over stored keys, algorithmic
-bytes 24 B/suffix per launch, HIP-event timed in the timed region) and
-"cpu_baseline" (the oracle's reference-identical single-thread restatement
-of src/sequential on a bounded sample, rank 0 at N=1 only).
+"roofline" (dominant kernel: the single-pass radix scatter over stored keys,
+algorithmic bytes 24 B/suffix per launch, HIP-event timed in the timed
+region; N = 1) and "cpu_baseline" (the oracle's reference-identical
+single-thread restatement of src/sequential on a bounded sample, rank 0,
+N = 1 only).
 """
 from __future__ import annotations
 
@@ -33,6 +36,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+METRIC = "suffixes sorted/sec + ms/doubling-round, 1 GiB input"
 
 ALPHABETS = {
     "dna": b"ACGT",
@@ -57,6 +61,8 @@ def parse():
     ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("--init-chars", type=int, default=0)
     ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
+    ap.add_argument("--mode", default="distributed", choices=["distributed", "replicas"],
+                    help="N > 1: one string over all ranks, or one string per rank")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -88,19 +94,125 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
                       f"median of {reps} ({med:.2f} s, {rounds} rounds), cpu '{model}'"}
 
 
-def pmc_traffic() -> dict | None:
-    """Per-launch HBM traffic of the dominant kernel from the committed
-    rocprofv3 PMC summary (profiles/<tag>_summary.json, written by
-    profiles/collect.sh + summarize.py), or None."""
+def pmc_summary() -> dict | None:
+    """The latest committed rocprofv3 summary (profiles/<tag>_summary.json,
+    written by profiles/collect.sh + summarize.py), or None."""
     paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
     if not paths:
         return None
     try:
         with open(paths[-1]) as f:
-            d = json.load(f)
-        return d
+            return json.load(f)
     except (OSError, ValueError):
         return None
+
+
+def make_text(b, n, kind, seed, dev, sptr):
+    import torch
+    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
+    if kind == "degenerate":
+        d_text.fill_(ord("a"))
+    else:
+        b.generate_text(d_text, n, ALPHABETS[kind], seed=seed, stream=sptr)
+    return d_text
+
+
+def timed(steps, warmup, fn, barrier):
+    for _ in range(warmup):
+        fn()
+    barrier()
+    t0 = time.perf_counter()
+    res = [fn() for _ in range(steps)]
+    barrier()
+    return time.perf_counter() - t0, res
+
+
+def run_single(a, torch, dev, world, rank, barrier):
+    """Single-GPU builder; with world > 1 (--mode replicas) one string per rank."""
+    from hpc_suffix_array_amd import DeviceBuilder
+    n = a.n
+    b = DeviceBuilder(n, device=dev.index)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    d_text = make_text(b, n, a.kind, a.seed + rank, dev, sptr)
+    d_sa = torch.empty(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize(dev)
+    profile = not a.no_profile
+    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars, radix=a.radix)
+    elapsed, stats = timed(a.steps, a.warmup, lambda: b.build(d_text, n, d_sa, **bkw), barrier)
+    verified = b.check(d_text, n, d_sa, stream=sptr)
+
+    rounds = stats[-1]["rounds"]
+    round_ms = [statistics.mean(s["round_ms"][j] for s in stats) for j in range(rounds)]
+    kern = {}
+    for k in stats[-1]["kernels"]:
+        kern[k] = {key: sum(s["kernels"][k][key] for s in stats) for key in ("ms", "launches", "bytes")}
+    dom = "scatter_keys"
+    roofline = None
+    if profile and kern[dom]["launches"]:
+        avg_s = kern[dom]["ms"] / kern[dom]["launches"] / 1e3
+        per_launch = kern[dom]["bytes"] / kern[dom]["launches"]
+        ach = per_launch / avg_s / 1e9
+        traffic = None
+        pmc = pmc_summary()
+        if pmc and pmc.get("n") == n and pmc.get("kind") == a.kind:
+            traffic = pmc.get("traffic_bytes_per_launch", {}).get("scatter_keys")
+        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                    "kernel": "k_onesweep<SrcKeys,1024,4> (single-pass radix scatter, stored keys)",
+                    "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
+    extra = {
+        "ms_per_round": [round(x, 3) for x in round_ms],
+        "rounds": rounds,
+        "distinct_per_round": stats[-1]["distinct"],
+        "passes_per_round": stats[-1]["passes"],
+        "sorted_per_round": stats[-1]["sorted_n"],
+        "prefix_len_per_round": stats[-1]["prefix_len"],
+        "schedule": stats[-1]["schedule"],
+        "init_chars": stats[-1]["init_chars"],
+        "sigma": stats[-1]["sigma"],
+        "sparse_ranks": stats[-1]["sparse_ranks"],
+        "model_bytes": stats[-1]["model_bytes"],
+        "verified": verified,
+        "roofline": roofline,
+        "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
+    }
+    b.close()
+    return elapsed, extra
+
+
+def run_distributed(a, torch, dev, world, rank, barrier):
+    """One string over all ranks (range-partitioned build, RCCL exchange)."""
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.builder import DeviceBuilder
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, gather_sa
+    n = a.n
+    ops = HipOps(max(1, 2 * n // world), dev.index)
+    sptr = torch.cuda.current_stream(dev).cuda_stream
+    d_text = make_text(ops.b, n, a.kind, a.seed, dev, sptr)   # same text on every rank
+    torch.cuda.synchronize(dev)
+    holder = {}
+
+    def step():
+        d = DistributedSA(ops)
+        holder["sa"] = d.build(d_text, n)
+        torch.cuda.synchronize(dev)
+        return d.stats
+
+    elapsed, stats = timed(a.steps, a.warmup, step, barrier)
+    verified = None
+    if n < (1 << 31):
+        sa = gather_sa(holder["sa"], n)
+        if rank == 0:
+            chk = DeviceBuilder(n, device=dev.index)
+            verified = chk.check(d_text, n, sa.to(torch.int32))
+            chk.close()
+        del sa
+    dist.barrier()
+    st = stats[-1]
+    extra = {"rounds": st["rounds"], "distinct_per_round": st["distinct"], "unsorted_per_round": st["unsorted"],
+             "init_chars": st["K"], "sigma": st["sigma"], "verified": verified, "roofline": None,
+             "note": "range-partitioned build: local HIP radix sorts, RCCL all_to_all bucket and rank exchange"}
+    return elapsed, extra
 
 
 def main():
@@ -111,115 +223,56 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-
-    from hpc_suffix_array_amd import DeviceBuilder
-    n = a.n
-    b = DeviceBuilder(n, device=local)
-    stream = torch.cuda.current_stream(dev)
-    sptr = stream.cuda_stream
-    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
-    d_sa = torch.empty(n, dtype=torch.int32, device=dev)
-    if a.kind == "degenerate":
-        d_text.fill_(ord("a"))
-    else:
-        b.generate_text(d_text, n, ALPHABETS[a.kind], seed=a.seed + rank, stream=sptr)
-    torch.cuda.synchronize(dev)
-
-    profile = not a.no_profile
-    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars, radix=a.radix)
-    for _ in range(a.warmup):
-        b.build(d_text, n, d_sa, **bkw)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
+        torch.cuda.synchronize(dev)
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    barrier()
-    t0 = time.perf_counter()
-    stats = []
-    for _ in range(a.steps):
-        stats.append(b.build(d_text, n, d_sa, **bkw))
-    torch.cuda.synchronize(dev)
-    barrier()
-    elapsed = time.perf_counter() - t0
+    distributed = world > 1 and a.mode == "distributed"
+    runner = run_distributed if distributed else run_single
+    elapsed, extra = runner(a, torch, dev, world, rank, barrier)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
-    ms_per_step = 1e3 * elapsed / max(a.steps, 1)
-
-    verified = b.check(d_text, n, d_sa, stream=sptr)
-
-    # per-round ms (mean over timed steps) and kernel aggregates
-    rounds = stats[-1]["rounds"]
-    round_ms = [statistics.mean(s["round_ms"][j] for s in stats) for j in range(rounds)]
-    kern = {}
-    for k in stats[-1]["kernels"]:
-        ms = sum(s["kernels"][k]["ms"] for s in stats)
-        nl = sum(s["kernels"][k]["launches"] for s in stats)
-        by = sum(s["kernels"][k]["bytes"] for s in stats)
-        kern[k] = {"ms": ms, "launches": nl, "bytes": by}
-    dom = "scatter_keys"
-    roofline = None
-    if profile and kern[dom]["launches"]:
-        avg_s = kern[dom]["ms"] / kern[dom]["launches"] / 1e3
-        per_launch = kern[dom]["bytes"] / kern[dom]["launches"]
-        ach = per_launch / avg_s / 1e9
-        traffic = None
-        pmc = pmc_traffic()
-        if pmc and pmc.get("n") == n and pmc.get("kind") == a.kind:
-            traffic = pmc.get("traffic_bytes_per_launch", {}).get("k_scatter_keys")
-        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_scatter<SrcKeys> (radix downsweep, stored keys)",
-                    "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
-
+    ms_per_step = 1e3 * float(t.item()) / max(a.steps, 1)
+    total = a.n if distributed else world * a.n
     out = {
-        "metric": "suffixes sorted/sec + ms/doubling-round, 1 GiB input",
-        "value": world * n / (ms_per_step / 1e3),
+        "metric": METRIC,
+        "value": total / (ms_per_step / 1e3),
         "unit": "suffixes/s",
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if distributed else "weak",
         "vs_baseline": None,
         "dtype": "u32",
-        "data": f"synthetic: seeded splitmix64 {a.kind} text generated in HBM (SURVEY.md 8(d)), seed {a.seed}+rank",
-        "config": {"workload": f"{a.kind} n={n} ({n / (1 << 30):.3g} GiB) per GPU, full Manber-Myers build",
-                   "n": n, "kind": a.kind, "parallelism": f"replicas{world}" if world > 1 else "single"},
-        "ms_per_round": [round(x, 3) for x in round_ms],
-        "rounds": rounds,
-        "distinct_per_round": stats[-1]["distinct"],
-        "passes_per_round": stats[-1]["passes"],
-        "sorted_per_round": stats[-1]["sorted_n"],
-        "prefix_len_per_round": stats[-1]["prefix_len"],
-        "schedule": stats[-1]["schedule"],
-        "init_chars": stats[-1]["init_chars"],
-        "sigma": stats[-1]["sigma"],
-        "model_bytes": stats[-1]["model_bytes"],
-        "model_frac_of_hbm_peak": round(stats[-1]["model_bytes"] / (ms_per_step / 1e3) / 8e12, 4),
-        "verified": verified,
-        "roofline": roofline,
-        "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
-        "cpu_baseline": None,
+        "data": f"synthetic: seeded splitmix64 {a.kind} text generated in HBM (SURVEY.md 8(d)), seed {a.seed}"
+                + ("" if distributed or world == 1 else "+rank"),
+        "config": {"workload": f"{a.kind} n={a.n} ({a.n / (1 << 30):.3g} GiB)"
+                               + (" over all GPUs" if distributed else " per GPU") + ", full suffix-array build",
+                   "n": a.n, "kind": a.kind,
+                   "parallelism": (f"range-partitioned x{world}" if distributed
+                                   else (f"replicas x{world}" if world > 1 else "single"))},
     }
+    out.update(extra)
+    out["cpu_baseline"] = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(a.kind, min(a.cpu_sample_n, n), a.seed)
+        out["cpu_baseline"] = cpu_baseline(a.kind, min(a.cpu_sample_n, a.n), a.seed)
     if rank == 0:
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    b.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -590,7 +590,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         if (rc) return rc;
     }
     tm.begin(SA_K_PACK);
-    hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, (const uint16_t*)c->code, ch,
+    hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
                        base, top, K, c->keys[1], c->hist, c->radix == 0 ? (bits1 + 7) / 8 : 0u, os_ghist(c));
     tm.end();
     SA_HIP(hipGetLastError());
@@ -937,6 +937,74 @@ int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, con
     hipFree(d_text);
     hipFree(d_sa);
     return rc;
+}
+
+int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8], void* stream) {
+    if (!present_out) return set_err(SA_E_INVALID, "present_out is NULL");
+    std::memset(present_out, 0, 32);
+    if (n == 0) return SA_OK;
+    if (!d_text) return set_err(SA_E_INVALID, "NULL device pointer");
+    hipStream_t s = (hipStream_t)stream;
+    uint32_t* d_mask = nullptr;
+    SA_HIP(hipMallocAsync((void**)&d_mask, 32, s));
+    SA_HIP(hipMemsetAsync(d_mask, 0, 32, s));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 2048);
+    hipLaunchKernelGGL(k_alphabet, dim3(grid), dim3(kBlock), 0, s, d_text, n, d_mask);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(present_out, d_mask, 32, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipFreeAsync(d_mask, s));
+    SA_HIP(hipStreamSynchronize(s));
+    return SA_OK;
+}
+
+int sa_pack_keys_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t hi,
+                        const uint16_t code[256], uint64_t base, uint32_t K, uint64_t* d_keys_out, void* stream) {
+    if (!ctx || !d_text || !d_keys_out || !code) return set_err(SA_E_INVALID, "NULL argument");
+    if (lo > hi || hi > n) return set_err(SA_E_INVALID, "bad range [%llu, %llu) of %llu", (unsigned long long)lo,
+                                          (unsigned long long)hi, (unsigned long long)n);
+    if (K == 0 || K >= (uint32_t)kMaxK || base < 2 || key_bits(base, K) > 64)
+        return set_err(SA_E_INVALID, "bad packing K=%u base=%llu", K, (unsigned long long)base);
+    if (hi == lo) return SA_OK;
+    hipStream_t s = (hipStream_t)stream;
+    SA_HIP(hipSetDevice(ctx->device));
+    SA_HIP(hipMemcpyAsync(ctx->code, code, 512, hipMemcpyHostToDevice, s));
+    uint64_t top = 1;
+    for (uint32_t t = 1; t < K; ++t) top *= base;
+    const Chunking ch = plan_chunks(hi - lo);
+    hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text + lo, n - lo,
+                       (const uint16_t*)ctx->code, ch, base, top, K, d_keys_out, (uint32_t*)nullptr, 0u,
+                       (uint32_t*)nullptr);
+    SA_HIP(hipGetLastError());
+    return SA_OK;
+}
+
+int sa_sort_pairs_device(sa_context* ctx, const uint64_t* d_keys_in, const uint32_t* d_vals_in, uint64_t m,
+                         uint32_t bits, uint64_t* d_keys_out, uint32_t* d_vals_out, void* stream) {
+    if (!ctx || !d_keys_in || !d_vals_in || !d_keys_out || !d_vals_out) return set_err(SA_E_INVALID, "NULL argument");
+    if (bits == 0 || bits > 64) return set_err(SA_E_INVALID, "bits must be 1..64");
+    if (m == 0) return SA_OK;
+    if (m > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "m too large");
+    if ((const void*)d_keys_in == (const void*)d_keys_out || (const void*)d_vals_in == (const void*)d_vals_out)
+        return set_err(SA_E_INVALID, "outputs may not alias inputs");
+    hipStream_t s = (hipStream_t)stream;
+    SA_HIP(hipSetDevice(ctx->device));
+    int rc = ensure_capacity(ctx, m);
+    if (rc) return rc;
+    ctx->radix = 0;
+    SA_HIP(hipMemsetAsync(ctx->words, 0, 64, s));
+    Timer tm{ctx, s, false, nullptr};
+    const Chunking ch = plan_chunks(m);
+    SrcKeys src{d_keys_in, d_vals_in};
+    uint64_t* sorted;
+    uint32_t P;
+    rc = radix_sort(ctx, src, 12 * m, ch, bits, d_vals_out, ctx->vals_alt, d_keys_out, ctx->keys[1], s, tm, nullptr,
+                    &sorted, &P);
+    if (rc) return rc;
+    if (sorted != d_keys_out) SA_HIP(hipMemcpyAsync(d_keys_out, sorted, m * 8, hipMemcpyDeviceToDevice, s));
+    SA_HIP(hipMemcpyAsync(ctx->host_words, ctx->words, 20, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    if (ctx->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
+    return SA_OK;
 }
 
 int sa_generate_text_device(uint8_t* d_out, uint64_t n, uint64_t seed, const uint8_t* alphabet, uint32_t sigma,

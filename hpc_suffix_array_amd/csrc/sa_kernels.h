@@ -548,7 +548,9 @@ constexpr int kPackRun = kTile / kBlock;   // 16 consecutive keys per lane
 constexpr int kMaxK = 64;
 constexpr int kPackMaxPasses = 8;
 
-__global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict__ text,
+// text points at the first position keyed (lo); `avail` bytes are readable
+// from there (n - lo); ch.n keys are produced.
+__global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict__ text, uint64_t avail,
                                                       const uint16_t* __restrict__ code, Chunking ch,
                                                       uint64_t base, uint64_t top, uint32_t K,
                                                       uint64_t* __restrict__ keys, uint32_t* __restrict__ hist,
@@ -563,7 +565,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
     for (int i = threadIdx.x; i < kPackMaxPasses * kRadix; i += kBlock) (&s_hist[0][0])[i] = 0;
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
-    const uint64_t n = ch.n;
+    const uint64_t n = avail;
     uint32_t* my = s_hist[passes ? 0u : wave_id()];
     auto count = [&](uint64_t key) {
         if (passes == 0) {
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
         {   // 16 text bytes per lane (one dwordx4), then the K-1 halo
             const uint64_t i = tb + (uint64_t)threadIdx.x * 16;
             uint16_t* dst = s_c + threadIdx.x * 16;
-            if (i + 16 <= n) {
+            if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
                 const uint4 v = *reinterpret_cast<const uint4*>(text + i);
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -618,7 +620,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_text(const uint8_t* __restrict_
         uint32_t s = 0;
 #pragma unroll
         for (int w = 0; w < kWaves; ++w) s += s_hist[w][threadIdx.x];
-        hist[(uint64_t)threadIdx.x * ch.chunks + c] = s;
+        if (hist) hist[(uint64_t)threadIdx.x * ch.chunks + c] = s;
     } else {
         for (uint32_t p = 0; p < passes; ++p) {
             const uint32_t v = s_hist[p][threadIdx.x];

@@ -1,0 +1,360 @@
+"""Range-partitioned multi-GPU suffix-array build.
+
+One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
+MI355X, "gloo" for the CPU tests).  Rank r owns text positions
+[r n / G, (r+1) n / G) and, at the end, the same slice of the SA.  Every
+rank holds the text (the packed keys of its positions read up to K-1 bytes
+past its slice).  Per round the local work runs on the HIP kernels of
+libsa_hip (``HipOps``); the exchange steps are collectives:
+
+  round 1   packed K-symbol keys of the rank's positions (sa_pack_keys_device)
+            -> global sort: local radix sort, G*64 samples all_gathered,
+               (key, rank, position) splitters, all_to_all_v of the buckets,
+               local radix sort of the received runs (stable, so the order
+               is (key, source rank, source position))
+            -> group heads with the neighbours' boundary keys (all_gather)
+            -> rank[i] = global head position + 1, sent to the owner of i
+               (all_to_all_v); singletons are final
+  round h   (only suffixes whose group is not a singleton)
+            -> rank[i + h] fetched from its owner (request / reply all_to_all_v)
+            -> global stable sort by (dense group id, rank[i + h])
+            -> new positions / heads inside each group, cross-rank carries
+               through all_gather; new ranks to their owners
+  end       (SA position, suffix) pairs all_to_all_v'd to the SA slice owners.
+
+This replaces the reference's MPI strategy (src/mpi/manber_myers_mpi.c:
+108-144: qsort per rank, Gatherv of all records to rank 0, serial qsort
+there, Bcast of the whole rank array every round), which is centralised and
+does not scale; here no rank ever holds more than its share plus buckets.
+
+The same code runs under gloo on CPU with the CPU stand-in of the local
+operations in tests/ (test infrastructure); the product path is HipOps and
+fails loudly without the HIP library.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import _native as N
+
+I64 = torch.int64
+SAMPLES = 64
+
+
+def bit_width(x: int) -> int:
+    return int(x).bit_length()
+
+
+def choose_chars(sigma: int, n: int, limit_bits: int = 63) -> Tuple[int, int]:
+    """(K, base) for the packed first key, as sa_build.hip choose_chars but
+    with base^K <= 2^limit_bits so keys stay non-negative int64."""
+    base = sigma + 1
+    kmax = 0
+    while base ** (kmax + 1) <= (1 << limit_bits):
+        kmax += 1
+    if sigma <= 1:
+        return max(kmax, 1), base
+    kmin = 1
+    while sigma ** kmin < 512 * n and kmin < kmax:
+        kmin += 1
+    passes = (bit_width(base ** kmin - 1) + 7) // 8
+    K = kmin
+    while K + 1 <= kmax and bit_width(base ** (K + 1) - 1) <= 8 * passes:
+        K += 1
+    return K, base
+
+
+class HipOps:
+    """Local per-rank operations on the GPU through libsa_hip's C ABI."""
+
+    def __init__(self, max_n: int, device: int):
+        from .builder import DeviceBuilder
+        self.dev = torch.device("cuda", device)
+        self.b = DeviceBuilder(max_n, device=device)
+        self.L = N.lib()
+
+    def _stream(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def alphabet(self, text: torch.Tensor) -> List[int]:
+        out = (ctypes.c_uint32 * 8)()
+        N.check(self.L.sa_alphabet_device(text.data_ptr(), text.numel(), out, self._stream()), "sa_alphabet_device")
+        return list(out)
+
+    def pack_keys(self, text: torch.Tensor, n: int, lo: int, hi: int, codes: Sequence[int], base: int,
+                  K: int) -> torch.Tensor:
+        keys = torch.empty(hi - lo, dtype=I64, device=self.dev)
+        code = (ctypes.c_uint16 * 256)(*codes)
+        N.check(self.L.sa_pack_keys_device(self.b.ctx, text.data_ptr(), n, lo, hi, code, base, K, keys.data_ptr(),
+                                           self._stream()), "sa_pack_keys_device")
+        return keys
+
+    def argsort(self, keys: torch.Tensor, bits: int) -> Tuple[torch.Tensor, torch.Tensor]:
+        m = keys.numel()
+        if m == 0:
+            return keys, torch.empty(0, dtype=I64, device=keys.device)
+        vals = torch.arange(m, dtype=torch.int32, device=keys.device)
+        ko = torch.empty_like(keys)
+        vo = torch.empty_like(vals)
+        N.check(self.L.sa_sort_pairs_device(self.b.ctx, keys.data_ptr(), vals.data_ptr(), m, max(bits, 1),
+                                            ko.data_ptr(), vo.data_ptr(), self._stream()), "sa_sort_pairs_device")
+        return ko, vo.to(I64)
+
+
+class DistributedSA:
+    """Distributed builder over an initialised process group."""
+
+    def __init__(self, ops, group=None):
+        self.ops = ops
+        self.group = group
+        self.G = dist.get_world_size(group)
+        self.r = dist.get_rank(group)
+        self.stats = {}
+
+    # -- collectives ---------------------------------------------------------
+    def _gather(self, t: torch.Tensor) -> torch.Tensor:
+        out = [torch.empty_like(t) for _ in range(self.G)]
+        dist.all_gather(out, t.contiguous(), group=self.group)
+        return torch.stack(out)
+
+    def _sum(self, x: int, dev) -> int:
+        t = torch.tensor([x], dtype=I64, device=dev)
+        dist.all_reduce(t, group=self.group)
+        return int(t.item())
+
+    def _alltoallv(self, tensors: List[torch.Tensor], send: List[int]) -> Tuple[List[torch.Tensor], List[int]]:
+        dev = tensors[0].device
+        sc = torch.tensor(send, dtype=I64, device=dev)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(rc, sc, group=self.group)
+        recv = rc.tolist()
+        outs = []
+        for t in tensors:
+            o = torch.empty(sum(recv), dtype=t.dtype, device=dev)
+            dist.all_to_all_single(o, t.contiguous(), recv, list(send), group=self.group)
+            outs.append(o)
+        return outs, recv
+
+    def _route(self, dest: torch.Tensor, tensors: List[torch.Tensor]):
+        order = torch.argsort(dest, stable=True)
+        send = torch.bincount(dest, minlength=self.G).tolist()
+        outs, recv = self._alltoallv([t[order] for t in tensors], send)
+        return outs, recv, order, send
+
+    # -- sorting ---------------------------------------------------------------
+    def _dist_sort(self, keys: torch.Tensor, payloads: List[torch.Tensor], bits: int):
+        """Global stable sort by key (order of equal keys: source rank, then
+        source position).  Returns sorted keys/payloads of this rank's
+        segment and the segment's global offset."""
+        dev = keys.device
+        keys, perm = self.ops.argsort(keys, bits)
+        payloads = [p[perm] for p in payloads]
+        m = keys.numel()
+        # samples (key, rank, position, valid)
+        s = min(SAMPLES, m)
+        samp = torch.zeros(SAMPLES, 4, dtype=I64, device=dev)
+        if s:
+            pos = torch.arange(s, dtype=I64, device=dev) * m // s
+            samp[:s, 0] = keys[pos]
+            samp[:s, 1] = self.r
+            samp[:s, 2] = pos
+            samp[:s, 3] = 1
+        allsamp = self._gather(samp).reshape(-1, 4).cpu()
+        allsamp = allsamp[allsamp[:, 3] == 1].tolist()
+        allsamp.sort()
+        cuts = []
+        for j in range(1, self.G):
+            if not allsamp:
+                cuts.append(m)
+                continue
+            ks, rs, ps, _ = allsamp[min(len(allsamp) - 1, j * len(allsamp) // self.G)]
+            lo = int(torch.searchsorted(keys, torch.tensor([ks], dtype=I64, device=dev), right=False).item())
+            hi = int(torch.searchsorted(keys, torch.tensor([ks], dtype=I64, device=dev), right=True).item())
+            if self.r < rs:
+                c = hi
+            elif self.r > rs:
+                c = lo
+            else:
+                c = min(max(ps, lo), hi)
+            cuts.append(c)
+        bounds = [0] + cuts + [m]
+        for j in range(1, len(bounds)):      # splitters are sorted, cuts must be too
+            bounds[j] = max(bounds[j], bounds[j - 1])
+        send = [bounds[j + 1] - bounds[j] for j in range(self.G)]
+        outs, _ = self._alltoallv([keys] + payloads, send)
+        keys, payloads = outs[0], outs[1:]
+        keys, perm = self.ops.argsort(keys, bits)
+        payloads = [p[perm] for p in payloads]
+        sizes = self._gather(torch.tensor([keys.numel()], dtype=I64, device=dev)).reshape(-1).tolist()
+        off = sum(sizes[: self.r])
+        return keys, payloads, off, sizes
+
+    # -- segment helpers --------------------------------------------------------
+    def _neighbours(self, cols: List[torch.Tensor], m: int, dev):
+        """Values of `cols` at the last element of the nearest non-empty
+        previous rank and the first element of the nearest non-empty next
+        rank (None when there is none)."""
+        k = len(cols)
+        info = torch.zeros(1 + 2 * k, dtype=I64, device=dev)
+        info[0] = m
+        if m:
+            for j, c in enumerate(cols):
+                info[1 + j] = c[0]
+                info[1 + k + j] = c[-1]
+        allinfo = self._gather(info).cpu().tolist()
+        prev = nxt = None
+        for q in range(self.r - 1, -1, -1):
+            if allinfo[q][0]:
+                prev = allinfo[q][1 + k: 1 + 2 * k]
+                break
+        for q in range(self.r + 1, self.G):
+            if allinfo[q][0]:
+                nxt = allinfo[q][1: 1 + k]
+                break
+        return prev, nxt
+
+    def _run_flags(self, cols: List[torch.Tensor], dev):
+        """head[s]: element s starts a run of equal cols; single[s]: the run
+        has one element (runs may span ranks)."""
+        m = cols[0].numel()
+        prev, nxt = self._neighbours(cols, m, dev)
+        if m == 0:
+            e = torch.zeros(0, dtype=torch.bool, device=dev)
+            return e, e
+        diff = torch.zeros(m - 1, dtype=torch.bool, device=dev)
+        for c in cols:
+            diff |= c[1:] != c[:-1]
+        first = prev is None or any(int(c[0]) != p for c, p in zip(cols, prev))
+        last = nxt is None or any(int(c[-1]) != q for c, q in zip(cols, nxt))
+        head = torch.cat([torch.tensor([first], device=dev), diff])
+        nhead = torch.cat([diff, torch.tensor([last], device=dev)])
+        return head, head & nhead
+
+    def _carry_start(self, head: torch.Tensor, idx: torch.Tensor, dev) -> torch.Tensor:
+        """For each element the value of idx at the last head at or before it
+        (scanning across ranks)."""
+        m = head.numel()
+        local_last = int(idx[head].max().item()) if m and bool(head.any()) else -1
+        lasts = self._gather(torch.tensor([local_last], dtype=I64, device=dev)).reshape(-1).tolist()
+        carry = max([-1] + lasts[: self.r])
+        if m == 0:
+            return idx
+        v = torch.where(head, idx, torch.full_like(idx, -1))
+        v, _ = torch.cummax(v, dim=0)
+        return torch.where(v < 0, torch.full_like(v, carry), v)
+
+    # -- the build ----------------------------------------------------------------
+    def build(self, text: torch.Tensor, n: int) -> torch.Tensor:
+        """SA[lo:hi] of this rank (int64), lo/hi = r n / G, (r+1) n / G."""
+        G, r = self.G, self.r
+        dev = text.device
+        bnd = [n * q // G for q in range(G + 1)]
+        lo, hi = bnd[r], bnd[r + 1]
+        bnd_t = torch.tensor(bnd[1:-1], dtype=I64, device=dev)
+
+        def owner(x):
+            return torch.searchsorted(bnd_t, x, right=True)
+
+        pres = torch.tensor(self.ops.alphabet(text), dtype=I64, device=dev)
+        dist.all_reduce(pres, op=dist.ReduceOp.BOR, group=self.group)
+        words = pres.tolist()
+        codes, sigma = [], 0
+        for b in range(256):
+            if (words[b >> 5] >> (b & 31)) & 1:
+                sigma += 1
+                codes.append(sigma)
+            else:
+                codes.append(0)
+        K, base = choose_chars(max(sigma, 1), n)
+        bits1 = bit_width(base ** K - 1)
+        self.stats = {"K": K, "sigma": sigma, "rounds": 0, "distinct": [], "unsorted": []}
+
+        # round 1: global sort of the packed K-prefixes
+        keys = self.ops.pack_keys(text, n, lo, hi, codes, base, K)
+        idx = torch.arange(lo, hi, dtype=I64, device=dev)
+        keys, (idx,), off, _ = self._dist_sort(keys, [idx], bits1)
+        m = keys.numel()
+        gpos = off + torch.arange(m, dtype=I64, device=dev)
+        head, single = self._run_flags([keys], dev)
+        hpos = self._carry_start(head, gpos, dev)
+        rank_local = torch.zeros(hi - lo, dtype=I64, device=dev)
+        (ri, rv), _, _, _ = self._route(owner(idx), [idx, hpos + 1])
+        rank_local[ri - lo] = rv
+        fin_pos, fin_idx = [gpos[single]], [idx[single]]
+        keep = ~single
+        upos, uidx, uhead = gpos[keep], idx[keep], hpos[keep]
+        D = self._sum(int(head.sum().item()), dev)
+        self.stats["rounds"] = 1
+        self.stats["distinct"].append(D)
+        wr = bit_width(n)
+        h = K
+        while True:
+            total_u = self._sum(uidx.numel(), dev)
+            self.stats["unsorted"].append(total_u)
+            if total_u == 0:
+                break
+            if h >= 2 * n:
+                raise RuntimeError("distributed doubling did not converge")
+            # rank[i + h] from its owner
+            q = uidx + h
+            valid = q < n
+            r1 = torch.zeros_like(uidx)
+            qv = q[valid]
+            (rq,), recv, order, send = self._route(owner(qv), [qv])
+            (ans,), _ = self._alltoallv([rank_local[rq - lo]], recv)
+            tmp = torch.empty_like(qv)
+            tmp[order] = ans
+            r1[valid] = tmp
+            # dense group id (groups are contiguous in SA order across ranks)
+            ghead, _ = self._run_flags([uhead], dev)
+            gcount = int(ghead.sum().item())
+            gcounts = self._gather(torch.tensor([gcount], dtype=I64, device=dev)).reshape(-1).tolist()
+            g = torch.cumsum(ghead.to(I64), 0) - 1 + sum(gcounts[:r])
+            ngroups = sum(gcounts)
+            wg = bit_width(max(ngroups - 1, 0))
+            if wg + wr <= 63:
+                key = (g << wr) | r1
+                key, (uidx, uhead, g, r1), uoff, _ = self._dist_sort(key, [uidx, uhead, g, r1], wg + wr)
+            else:   # two stable passes: by rank[i+h], then by group
+                r1, (uidx, uhead, g), _, _ = self._dist_sort(r1, [uidx, uhead, g], wr)
+                g, (uidx, uhead, r1), uoff, _ = self._dist_sort(g, [uidx, uhead, r1], max(wg, 1))
+            mu = uidx.numel()
+            uindex = uoff + torch.arange(mu, dtype=I64, device=dev)
+            gstart_flag, _ = self._run_flags([g], dev)
+            gstart = self._carry_start(gstart_flag, uindex, dev)
+            rhead, rsingle = self._run_flags([g, r1], dev)
+            rstart = self._carry_start(rhead, uindex, dev)
+            pos = uhead + (uindex - gstart)
+            newhead = uhead + (rstart - gstart)
+            (ri, rv), _, _, _ = self._route(owner(uidx), [uidx, newhead + 1])
+            rank_local[ri - lo] = rv
+            fin_pos.append(pos[rsingle])
+            fin_idx.append(uidx[rsingle])
+            keep = ~rsingle
+            D = (n - total_u) + self._sum(int(rhead.sum().item()), dev)
+            self.stats["rounds"] += 1
+            self.stats["distinct"].append(D)
+            upos, uidx, uhead = pos[keep], uidx[keep], newhead[keep]
+            h *= 2
+        fp = torch.cat(fin_pos)
+        fi = torch.cat(fin_idx)
+        (sp, si), _, _, _ = self._route(owner(fp), [fp, fi])
+        sa = torch.full((hi - lo,), -1, dtype=I64, device=dev)
+        sa[sp - lo] = si
+        return sa
+
+
+def gather_sa(sa_local: torch.Tensor, n: int, group=None) -> torch.Tensor:
+    """Concatenate the SA slices of all ranks (every rank gets the full SA)."""
+    G = dist.get_world_size(group)
+    sizes = [n * (q + 1) // G - n * q // G for q in range(G)]
+    m = max(sizes)
+    buf = torch.full((m,), -1, dtype=I64, device=sa_local.device)
+    buf[: sa_local.numel()] = sa_local
+    out = [torch.empty_like(buf) for _ in range(G)]
+    dist.all_gather(out, buf, group=group)
+    return torch.cat([o[: sizes[q]] for q, o in enumerate(out)])

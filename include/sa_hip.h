@@ -111,6 +111,25 @@ int sa_check_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const ui
                     void* stream);
 int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width);
 
+/* ---- building blocks of the range-partitioned multi-GPU build ----------
+ * (hpc_suffix_array_amd/distributed.py drives these per rank; the exchange
+ * steps between them are RCCL collectives over xGMI.)                      */
+
+/* 256-bit byte-presence mask of the n device bytes (host out: 8 words). */
+int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8], void* stream);
+
+/* Packed K-symbol keys of positions [lo, hi) of the n-byte text:
+ * key(i) = sum_t code[text[i+t]] * base^(K-1-t) (0 past the end);
+ * code = 256 dense symbol codes (host array), base^K <= 2^64. */
+int sa_pack_keys_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t hi,
+                        const uint16_t code[256], uint64_t base, uint32_t K, uint64_t* d_keys_out,
+                        void* stream);
+
+/* Stable LSD radix sort of m (u64 key, u32 value) pairs by key bits
+ * [0, bits) into keys_out / vals_out (may not alias the inputs). */
+int sa_sort_pairs_device(sa_context* ctx, const uint64_t* d_keys_in, const uint32_t* d_vals_in, uint64_t m,
+                         uint32_t bits, uint64_t* d_keys_out, uint32_t* d_vals_out, void* stream);
+
 /* Seeded synthetic text in device memory: the splitmix64 generator of
  * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
  * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */

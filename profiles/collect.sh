@@ -19,3 +19,4 @@ timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch"
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o write -- \
     python3 bench.py --no-cpu-baseline --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/write.log" 2>&1
 python3 profiles/summarize.py "$tag" "$out" "${args[@]}"
+cp profiles/"$tag"_summary.json profiles/"$tag"_kernel_stats.csv "$out"/ 2>/dev/null || true

@@ -6,8 +6,9 @@ and WRITE_SIZE per launch (rocprofv3 --pmc, KiB -> bytes), and HBM traffic
 per launch corrected as MI355X_MICROARCH.md section HBM prescribes: on gfx950
 FETCH_SIZE under-reads wide coalesced streams (x2 for 16-B/lane reads) and
 other access widths must be calibrated on a known byte count.  The read
-calibration here is k_hist<SrcKeys>, which reads exactly 8 bytes per suffix
-(its u64 keys) and writes 1 KiB of counts: read_factor = 8n / FETCH bytes.
+calibration here is the first (full-n) k_seg_count launch, which reads
+exactly 8 bytes per suffix (the sorted u64 keys) and writes 16 bytes per
+4096-suffix tile: read_factor = 8n / FETCH bytes of that launch.
 WRITE_SIZE is reported as measured (exact for 16-B/lane streaming stores per
 the guide; the scatter's 8-B / 4-B run stores are uncalibrated).
 """
@@ -24,9 +25,13 @@ KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist
          ("k_scan_rows", "scan"), ("k_scatter<sa::SrcRank>", "scatter_rank"),
          ("k_scatter<sa::SrcText>", "scatter_text"), ("k_scatter<sa::SrcU", "scatter_u"),
          ("k_scatter<sa::SrcKeysIota>", "scatter_iota"), ("k_pack_text", "pack"),
-         ("k_scatter<sa::SrcKeys>", "scatter_keys"), ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
+         ("k_scatter<sa::SrcKeys>", "scatter_keys_rs"),
+         ("k_onesweep<sa::SrcKeysIota", "scatter_iota"), ("k_onesweep<sa::SrcKeys,", "scatter_keys"),
+         ("k_onesweep<sa::SrcU", "scatter_u"), ("k_onesweep<sa::SrcRank", "scatter_rank"),
+         ("k_global_hist", "global_hist"), ("k_digit_base", "digit_base"), ("k_alphabet", "alphabet"),
+         ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
          ("k_rerank", "rerank"), ("k_seg_count", "seg_count"), ("k_seg_scan", "seg_scan"),
-         ("k_seg_write", "seg_write"), ("k_byte_hist", "alphabet"), ("k_gen_text", "gen_text"),
+         ("k_seg_write", "seg_write"), ("k_gen_text", "gen_text"),
          ("k_check_isa", "check_isa"), ("k_check_pairs", "check_pairs"), ("k_fill_u32", "fill")]
 
 
@@ -54,18 +59,26 @@ def main():
             kind = args[i + 1]
     stats_csv = find(os.path.join(out, "trace"), "kernel_stats.csv")
     trace_csv = find(os.path.join(out, "trace"), "kernel_trace.csv")
-    per = defaultdict(lambda: {"calls": 0, "total_ns": 0.0})
+
+    def grid(row):
+        return int(float(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
+
+    # per kind: all launches, and the full-size ones (largest grid of the
+    # kind: the launches over all n suffixes, not the small unsorted-set ones)
+    per = defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "full": defaultdict(list)})
     if trace_csv:
         with open(trace_csv) as f:
             for row in csv.DictReader(f):
                 k = kind_of(row.get("Kernel_Name", ""))
                 if k:
+                    d = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
                     per[k]["calls"] += 1
-                    per[k]["total_ns"] += float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
+                    per[k]["total_ns"] += d
+                    per[k]["full"][grid(row)].append(d)
     pmc = {}
     for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         c = find(os.path.join(out, sub), "counter_collection.csv")
-        acc = defaultdict(lambda: [0.0, 0])
+        acc = defaultdict(lambda: defaultdict(list))
         if c:
             with open(c) as f:
                 for row in csv.DictReader(f):
@@ -73,17 +86,18 @@ def main():
                         continue
                     k = kind_of(row.get("Kernel_Name", ""))
                     if k:
-                        acc[k][0] += float(row["Counter_Value"]) * 1024.0   # KiB -> bytes
-                        acc[k][1] += 1
-        pmc[name] = {k: v[0] / v[1] for k, v in acc.items() if v[1]}
+                        acc[k][grid(row)].append(float(row["Counter_Value"]) * 1024.0)   # KiB -> bytes
+        pmc[name] = {k: sum(v[max(v)]) / len(v[max(v)]) for k, v in acc.items() if v}
     fetch, write = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
     read_factor = None
-    if fetch.get("hist_keys"):
-        read_factor = 8.0 * n / fetch["hist_keys"]
+    if fetch.get("seg_count"):
+        read_factor = 8.0 * n / fetch["seg_count"]
     kernels = {}
     for k, v in per.items():
+        full = v["full"][max(v["full"])]
         e = {"calls": v["calls"], "avg_ms": v["total_ns"] / max(v["calls"], 1) / 1e6,
-             "total_ms": v["total_ns"] / 1e6}
+             "total_ms": v["total_ns"] / 1e6, "full_size_calls": len(full),
+             "full_size_avg_ms": sum(full) / len(full) / 1e6}
         if k in fetch:
             e["fetch_bytes_raw"] = fetch[k]
         if k in write:
@@ -99,9 +113,10 @@ def main():
             bench = json.loads(f.read())
     summary = {
         "tag": tag, "n": n, "kind": kind, "args": args,
-        "read_calibration": {"kernel": "hist_keys", "known_read_bytes": 8 * n, "factor": read_factor},
+        "read_calibration": {"kernel": "seg_count (full-n launch)", "known_read_bytes": 8 * n,
+                             "factor": read_factor},
         "kernels": kernels,
-        "traffic_bytes_per_launch": {"k_scatter_keys": kernels.get("scatter_keys", {}).get("traffic_bytes_corrected")},
+        "traffic_bytes_per_launch": {"scatter_keys": kernels.get("scatter_keys", {}).get("traffic_bytes_corrected")},
         "bench": bench,
     }
     here = os.path.dirname(os.path.abspath(__file__))

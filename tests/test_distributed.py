@@ -1,0 +1,87 @@
+"""Multi-rank path under gloo on CPU: the range-partitioned
+driver with the CPU stand-in of its local operations, world sizes 2 and 3,
+checked against the oracle.  The same driver runs with HipOps + RCCL on the
+GPU box (tests/test_gpu_parity.py::test_distributed_hip_single_rank and
+bench.py --gpus N)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _texts():
+    import sys
+    sys.path.insert(0, ROOT)
+    from oracle import oracle as O
+    return {
+        "dna": O.gen_text("dna", 20_011, seed=3),
+        "binary": O.gen_text("binary", 9_001, seed=4),
+        "byte256": O.gen_text("byte256", 7_000, seed=5),
+        "degenerate": np.full(1_500, ord("a"), np.uint8),
+        "periodic": np.tile(np.frombuffer(b"abaababa", np.uint8), 700),
+        "tiny1": np.frombuffer(b"x", np.uint8),
+        "tiny2": np.frombuffer(b"ba", np.uint8),
+        "banana": np.frombuffer(b"banana", np.uint8),
+    }
+
+
+def _worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from dist_cpu_ops import CpuOps
+    from hpc_suffix_array_amd.distributed import DistributedSA, gather_sa
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        res = {}
+        for name, t in _texts().items():
+            text = torch.from_numpy(t.copy())
+            d = DistributedSA(CpuOps())
+            sa_local = d.build(text, len(t))
+            sa = gather_sa(sa_local, len(t))
+            res[name] = (sa.numpy(), d.stats)
+        if rank == 0:
+            q.put(res)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_gloo(oracle, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for name, t in _texts().items():
+        sa, st = res[name]
+        want = oracle.sa_c(t)
+        assert (sa == want.astype(np.int64)).all(), (name, world)
+        assert st["distinct"][-1] == len(t), name
+
+
+def test_choose_chars_keeps_int64_keys():
+    from hpc_suffix_array_amd.distributed import choose_chars
+    for sigma in (1, 2, 3, 4, 26, 62, 127, 255, 256):
+        K, base = choose_chars(sigma, 1 << 30)
+        assert base ** K <= 1 << 63 and K >= 1
+    assert choose_chars(4, 1 << 30) == (20, 5)

@@ -191,3 +191,29 @@ def test_config3_1gib_minus_1_known_answer(gpu, oracle, golden):
     sa = d_sa.cpu().numpy()
     assert oracle.sha256(sa) == k["sa_sha256_i32"]
     b.close()
+
+
+def test_distributed_hip_single_rank(gpu, oracle):
+    """The multi-GPU driver with the HIP local operations and RCCL
+    collectives, at world size 1 (the box has one GPU; world sizes 2-3 run
+    under gloo in tests/test_distributed.py)."""
+    import socket
+
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, gather_sa
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
+                            device_id=torch.device("cuda", 0))
+    try:
+        ops = HipOps(1 << 22, 0)
+        for t in (oracle.gen_text("dna", 3_000_017, seed=8), np.full(70_000, ord("a"), np.uint8),
+                  np.tile(np.frombuffer(b"abaababa", np.uint8), 9_000), oracle.gen_text("byte256", 500_000, seed=2)):
+            text = torch.from_numpy(t.copy()).cuda()
+            d = DistributedSA(ops)
+            sa = gather_sa(d.build(text, len(t)), len(t)).cpu().numpy()
+            assert (sa == oracle.sa_c(t).astype(np.int64)).all()
+    finally:
+        dist.destroy_process_group()
