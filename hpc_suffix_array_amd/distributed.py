@@ -259,9 +259,12 @@ class DistributedSA:
         def owner(x):
             return torch.searchsorted(bnd_t, x, right=True)
 
+        # alphabet: OR of the ranks' presence masks (torch's NCCL backend has
+        # no BOR reduction, so gather the 8 words and OR them here)
         pres = torch.tensor(self.ops.alphabet(text), dtype=I64, device=dev)
-        dist.all_reduce(pres, op=dist.ReduceOp.BOR, group=self.group)
-        words = pres.tolist()
+        words = [0] * 8
+        for row in self._gather(pres).tolist():
+            words = [x | y for x, y in zip(words, row)]
         codes, sigma = [], 0
         for b in range(256):
             if (words[b >> 5] >> (b & 31)) & 1:
