@@ -17,7 +17,8 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 
 SA_MAX_ROUNDS = 64
 KERNEL_KINDS = ["init", "hist_first", "hist_keys", "scan", "scatter_first", "scatter_keys",
-                "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet", "pack"]
+                "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet", "pack",
+                "sort_u"]
 SCHEDULE_PACKED = 0
 SCHEDULE_REFERENCE = 1
 SA_K_COUNT = len(KERNEL_KINDS)

@@ -317,9 +317,15 @@ static void onesweep_pass(sa_context* c, const Src& src, uint64_t n, uint32_t sh
 template <class Src>
 static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, const Chunking& ch, uint32_t bits,
                       uint32_t* vals_final, uint32_t* vals_other, uint64_t* kb0, uint64_t* kb1, hipStream_t s,
-                      Timer& tm, sa_stats* st, uint64_t** sorted_keys, uint32_t* passes, bool hist0_ready = false) {
+                      Timer& tm, sa_stats* st, uint64_t** sorted_keys, uint32_t* passes, bool hist0_ready = false,
+                      bool usort = false) {
     const uint32_t P = (bits + 7) / 8;
     if (P > kMaxPasses) return set_err(SA_E_INTERNAL, "%u radix passes", P);
+    // an unsorted-set sort (later rounds, few suffixes) is accounted apart so
+    // the per-kind averages of the full-n passes stay per-launch comparable
+    const int k_hist = usort ? SA_K_SORT_U : SA_K_HIST_FIRST;
+    const int k_first = usort ? SA_K_SORT_U : SA_K_SCATTER_FIRST;
+    const int k_keys = usort ? SA_K_SORT_U : SA_K_SCATTER_KEYS;
     if (c->radix == 0) {
         const uint64_t n = ch.n;
         uint32_t* vb[2];
@@ -329,11 +335,11 @@ static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, con
         if (!hist0_ready) {
             int rc = onesweep_prepare(c, s);
             if (rc) return rc;
-            tm.begin(SA_K_HIST_FIRST);
+            tm.begin(k_hist);
             const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 2048);
             hipLaunchKernelGGL(k_global_hist<Src>, dim3(grid), dim3(kBlock), 0, s, first, n, P, os_ghist(c));
             tm.end();
-            add_bytes(st, SA_K_HIST_FIRST, first_bytes);
+            add_bytes(st, k_hist, first_bytes);
         }
         tm.begin(SA_K_SCAN);
         hipLaunchKernelGGL(k_digit_base, dim3(P), dim3(kBlock), 0, s, (const uint32_t*)os_ghist(c), os_base(c));
@@ -342,17 +348,17 @@ static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, con
             const uint32_t shift = 8 * p;
             const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
             if (p == 0) {
-                tm.begin(SA_K_SCATTER_FIRST);
+                tm.begin(k_first);
                 onesweep_pass(c, first, n, shift, nbits, os_base(c), os_tickets(c), kb[0], vb[0], s);
                 tm.end();
-                add_bytes(st, SA_K_SCATTER_FIRST, first_bytes + 12 * n);
+                add_bytes(st, k_first, first_bytes + 12 * n);
             } else {
                 SrcKeys src{kb[(p - 1) & 1], vb[(p - 1) & 1]};
-                tm.begin(SA_K_SCATTER_KEYS);
+                tm.begin(k_keys);
                 onesweep_pass(c, src, n, shift, nbits, os_base(c) + p * kRadix, os_tickets(c) + p, kb[p & 1],
                               vb[p & 1], s);
                 tm.end();
-                add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);
+                add_bytes(st, k_keys, 24 * n);
             }
         }
         SA_HIP(hipGetLastError());
@@ -369,12 +375,12 @@ static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, con
         const uint32_t nbits = std::min<uint32_t>(8, bits - shift);
         int rc;
         if (p == 0) {
-            rc = radix_pass(c, first, ch, shift, nbits, kb[0], vb[0], s, tm, st, SA_K_HIST_FIRST,
-                            SA_K_SCATTER_FIRST, first_bytes, hist0_ready);
+            rc = radix_pass(c, first, ch, shift, nbits, kb[0], vb[0], s, tm, st, k_hist, k_first, first_bytes,
+                            hist0_ready);
         } else {
             SrcKeys src{kb[(p - 1) & 1], vb[(p - 1) & 1]};
-            rc = radix_pass(c, src, ch, shift, nbits, kb[p & 1], vb[p & 1], s, tm, st, SA_K_HIST_KEYS,
-                            SA_K_SCATTER_KEYS, 12 * ch.n);
+            rc = radix_pass(c, src, ch, shift, nbits, kb[p & 1], vb[p & 1], s, tm, st,
+                            usort ? SA_K_SORT_U : SA_K_HIST_KEYS, k_keys, 12 * ch.n);
         }
         if (rc) return rc;
     }
@@ -632,10 +638,12 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         uint64_t* sorted;
         if (sparse) {
             SrcU<true> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
-            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P);
+            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P,
+                            false, true);
         } else {
             SrcU<false> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
-            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P);
+            rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P,
+                            false, true);
         }
         if (rc) return rc;
         uint64_t Du, m2, G2;

@@ -48,7 +48,8 @@ enum sa_kernel_kind {
     SA_K_SEG_WRITE = 11,     /* rank + SA update, unsorted-set compaction */
     SA_K_ALPHABET = 12,      /* byte histogram of the text */
     SA_K_PACK = 13,          /* packed K-symbol keys + first digit histogram */
-    SA_K_COUNT = 14
+    SA_K_SORT_U = 14,        /* every pass of an unsorted-set (later round) sort */
+    SA_K_COUNT = 15
 };
 
 /* doubling schedules */
