@@ -27,7 +27,7 @@ SA_K_COUNT = len(KERNEL_KINDS)
 DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_array",
                   "build_lcp_array", "find_longest_repeated_substring", "is_valid_suffix_array"]
 EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", "sa_build_device",
-               "sa_build_ex", "sa_check_device", "sa_check", "sa_generate_text_device",
+               "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device",
                "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
 
@@ -123,6 +123,10 @@ def lib() -> ctypes.CDLL:
     L.sa_check_device.restype = i32
     L.sa_check.argtypes = [vp, u64, vp, i32]
     L.sa_check.restype = i32
+    L.sa_lcp_device.argtypes = [vp, vp, u64, vp, vp, ctypes.POINTER(u64), ctypes.POINTER(u64), vp]
+    L.sa_lcp_device.restype = i32
+    L.sa_lcp.argtypes = [vp, u64, vp, i32, vp, ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    L.sa_lcp.restype = i32
     L.sa_alphabet_device.argtypes = [vp, u64, ctypes.POINTER(ctypes.c_uint32), vp]
     L.sa_alphabet_device.restype = i32
     L.sa_pack_keys_device.argtypes = [vp, vp, u64, u64, u64, ctypes.POINTER(ctypes.c_uint16), u64,

@@ -82,6 +82,30 @@ def check_suffix_array(text, sa) -> bool:
     return bool(r)
 
 
+def lcp_array(text, sa, width: int = 4):
+    """LCP array of a valid suffix array on the GPU plus the longest repeated
+    substring (replaces build_lcp_array, manber_myers.c:135-157, and
+    find_longest_repeated_substring, :159-182).
+
+    Returns (lcp, lrs) with lcp[0] = 0, lcp[r] = lcp(SA[r-1], SA[r]) as uint32
+    (width 4) or int64 (width 8), and lrs = (length, SA position) of the first
+    r with the strictly largest lcp ((0, 0) when nothing repeats)."""
+    t = _as_bytes_array(text)
+    s = np.ascontiguousarray(sa)
+    if s.dtype not in (np.uint32, np.int32, np.int64):
+        s = s.astype(np.int64)
+    n = int(t.size)
+    if s.size != n:
+        raise ValueError(f"SA has {s.size} entries for a text of {n} bytes")
+    N.require_device()
+    out = np.empty(max(n, 1), dtype=np.uint32 if width == 4 else np.int64)
+    ln, pos = ctypes.c_uint64(), ctypes.c_uint64()
+    N.check(N.lib().sa_lcp(t.ctypes.data if n else None, n, s.ctypes.data if n else None,
+                           8 if s.dtype == np.int64 else 4, out.ctypes.data, ctypes.byref(ln), ctypes.byref(pos)),
+            "sa_lcp")
+    return out[:n], (int(ln.value), int(pos.value))
+
+
 class SuffixArray:
     """The reference's SuffixArray object (suffix_array.h:16-21) driven
     through the drop-in C symbols of libsa_hip.so.
@@ -189,6 +213,15 @@ class DeviceBuilder:
         s = None if stream is None else ctypes.c_void_p(int(stream))
         return bool(N.check(self.L.sa_check_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s),
                             "sa_check_device"))
+
+    def lcp(self, d_text, n: int, d_sa, d_lcp, stream=None) -> tuple:
+        """LCP of the SA at d_sa into the n uint32 at d_lcp; returns the longest
+        repeated substring as (length, SA position)."""
+        s = None if stream is None else ctypes.c_void_p(int(stream))
+        ln, pos = ctypes.c_uint64(), ctypes.c_uint64()
+        N.check(self.L.sa_lcp_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), self._ptr(d_lcp),
+                                     ctypes.byref(ln), ctypes.byref(pos), s), "sa_lcp_device")
+        return int(ln.value), int(pos.value)
 
     def close(self) -> None:
         if self.ctx:

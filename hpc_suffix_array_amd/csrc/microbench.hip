@@ -59,6 +59,14 @@ __global__ __launch_bounds__(BLOCK) void k_copy_striped(const uint64_t* __restri
     }
 }
 
+__global__ void k_mismatch(const uint64_t* a, const uint32_t* av, const uint64_t* b, const uint32_t* bv, uint64_t n,
+                           unsigned long long* out) {
+    unsigned long long c = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+        c += (a[i] != b[i]) | (av[i] != bv[i]);
+    if (c) atomicAdd(out, c);
+}
+
 // 16 bytes per lane per access
 __global__ __launch_bounds__(256) void k_copy_vec(const uint4* __restrict__ a, uint4* __restrict__ b, uint64_t m) {
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m; i += (uint64_t)gridDim.x * 256) b[i] = a[i];
@@ -109,8 +117,8 @@ int main(int argc, char** argv) {
     uint32_t* ghist = ws;
     uint32_t* base = ws + 4096;
     uint32_t* tick = ws + 8192;
-    uint32_t* hist = ws + 16384;   // reduce-then-scan: 256 x 1024 chunks
-    uint32_t* totals = ws + 16384 + 262144;
+    uint32_t* hist = ws + 16384;   // reduce-then-scan: 256 x up to 2048 chunks
+    uint32_t* totals = ws + 16384 + 524288;
     CK(hipMemset(ghist, 0, 4096 * 4));
     SrcKeys src{k0, v0};
     hipLaunchKernelGGL(k_global_hist<SrcKeys>, dim3(2048), dim3(kBlock), 0, 0, src, n, 1u, ghist);
@@ -139,34 +147,60 @@ int main(int argc, char** argv) {
                                (const uint32_t*)base, states, tick, epoch, k1, v1, err);
         };
     };
-    report("onesweep_256x16", T.ms(onesweep(k_onesweep<SrcKeys, 256, 16, 0>, 256, 4096), reps));
-    report("onesweep_256x16_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 256, 16, 1>, 256, 4096), reps));
-    report("onesweep_256x16_nolookback_xcd", T.ms(onesweep(k_onesweep<SrcKeys, 256, 16, 9>, 256, 4096), reps));
-    report("onesweep_256x8", T.ms(onesweep(k_onesweep<SrcKeys, 256, 8, 0>, 256, 2048), reps));
-    report("onesweep_512x8", T.ms(onesweep(k_onesweep<SrcKeys, 512, 8, 0>, 512, 4096), reps));
-    report("onesweep_512x8_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 512, 8, 1>, 512, 4096), reps));
-    report("onesweep_512x8_nolookback_xcd", T.ms(onesweep(k_onesweep<SrcKeys, 512, 8, 9>, 512, 4096), reps));
-    report("onesweep_512x7", T.ms(onesweep(k_onesweep<SrcKeys, 512, 7, 0>, 512, 3584), reps));
-    report("onesweep_512x7_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 512, 7, 1>, 512, 3584), reps));
     report("onesweep_1024x4", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 4, 0>, 1024, 4096), reps));
     report("onesweep_1024x4_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 4, 1>, 1024, 4096), reps));
-    report("onesweep_1024x8", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 8, 0>, 1024, 8192), reps));
-    report("onesweep_1024x8_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 8, 1>, 1024, 8192), reps));
-    report("onesweep_512x16", T.ms(onesweep(k_onesweep<SrcKeys, 512, 16, 0>, 512, 8192), reps));
-    {
+    // the onesweep output is the reference the chunked variants are compared with
+    uint64_t* kref;
+    uint32_t* vref;
+    unsigned long long* mism;
+    CK(hipMalloc(&kref, n * 8));
+    CK(hipMalloc(&vref, n * 4));
+    CK(hipMalloc(&mism, 8));
+    CK(hipMemcpy(kref, k1, n * 8, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(vref, v1, n * 4, hipMemcpyDeviceToDevice));
+    auto verify = [&](const char* name) {
+        CK(hipMemset(mism, 0, 8));
+        hipLaunchKernelGGL(k_mismatch, dim3(4096), dim3(256), 0, 0, (const uint64_t*)k1, (const uint32_t*)v1,
+                           (const uint64_t*)kref, (const uint32_t*)vref, n, mism);
+        unsigned long long h = 0;
+        CK(hipMemcpy(&h, mism, 8, hipMemcpyDeviceToHost));
+        std::printf("{\"verify\": \"%s\", \"mismatches\": %llu}\n", name, h);
+        std::fflush(stdout);
+        CK(hipMemset(k1, 0, n * 8));
+        CK(hipMemset(v1, 0, n * 4));
+    };
+    for (uint32_t want : {512u, 1024u, 2048u}) {
         Chunking ch;
         ch.n = n;
         const uint64_t tiles = (n + kTile - 1) / kTile;
-        const uint64_t tpc = (tiles + 1023) / 1024;
+        const uint64_t tpc = (tiles + want - 1) / want;
         ch.tiles_per_chunk = (uint32_t)tpc;
         ch.chunks = (uint32_t)((tiles + tpc - 1) / tpc);
-        report("reduce_scan_hist", T.ms([&] {
+        char name[64];
+        std::snprintf(name, sizeof name, "reduce_scan_hist_c%u", ch.chunks);
+        report(name, T.ms([&] {
             hipLaunchKernelGGL(k_hist<SrcKeys>, dim3(ch.chunks), dim3(kBlock), 0, 0, src, ch, 0u, 255u, hist);
         }, reps));
-        report("reduce_scan_scatter", T.ms([&] {
+        hipLaunchKernelGGL(k_scan_rows, dim3(kRadix), dim3(kBlock), 0, 0, hist, ch.chunks, totals);
+        CK(hipDeviceSynchronize());
+        std::snprintf(name, sizeof name, "reduce_scan_scatter_c%u", ch.chunks);
+        report(name, T.ms([&] {
             hipLaunchKernelGGL(k_scatter<SrcKeys>, dim3(ch.chunks), dim3(kBlock), 0, 0, src, ch, 0u, 8u,
                                (const uint32_t*)hist, (const uint32_t*)totals, k1, v1);
         }, reps));
+        verify(name);
+        std::snprintf(name, sizeof name, "scatter_pipe_1024x4_c%u", ch.chunks);
+        report(name, T.ms([&] {
+            hipLaunchKernelGGL((k_scatter_pipe<SrcKeys, 1024, 4>), dim3(ch.chunks), dim3(1024), 0, 0, src, ch, 0u, 8u,
+                               (const uint32_t*)hist, (const uint32_t*)totals, k1, v1);
+        }, reps));
+        verify(name);
+        std::snprintf(name, sizeof name, "scatter_pipe_512x8_c%u", ch.chunks);
+        report(name, T.ms([&] {
+            hipLaunchKernelGGL((k_scatter_pipe<SrcKeys, 512, 8>), dim3(ch.chunks), dim3(512), 0, 0, src, ch, 0u, 8u,
+                               (const uint32_t*)hist, (const uint32_t*)totals, k1, v1);
+        }, reps));
+        verify(name);
     }
     uint32_t herr = 0;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));

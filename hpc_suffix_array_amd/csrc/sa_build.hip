@@ -25,6 +25,7 @@
 
 #include "../../include/sa_hip.h"
 #include "sa_kernels.h"
+#include "sa_lcp.h"
 #include "sa_onesweep.h"
 
 namespace sa {
@@ -765,6 +766,71 @@ static int check_device(sa_context* c, const uint8_t* d_text, uint64_t n, const 
 }
 
 // ---------------------------------------------------------------------------
+// LCP + LRS (sa_lcp.h).  Workspace: PHI lives in d_lcp until the gather
+// overwrites it, v / PLCP in rank, the cooperative pair lists in keys[0..1],
+// their first-mismatch words in vals_alt, pair counts in counts, chunk maxima
+// in hist, the LRS key in words[8..9].
+// ---------------------------------------------------------------------------
+static int lcp_device(sa_context* c, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, uint32_t* d_lcp,
+                      uint64_t* lrs_len, uint64_t* lrs_pos, hipStream_t s) {
+    if (lrs_len) *lrs_len = 0;
+    if (lrs_pos) *lrs_pos = 0;
+    if (n == 0) return SA_OK;
+    if (!d_text || !d_sa || !d_lcp) return set_err(SA_E_INVALID, "NULL device pointer");
+    if ((const void*)d_sa == (const void*)d_lcp) return set_err(SA_E_INVALID, "d_lcp may not alias d_sa");
+    if (n > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "n too large");
+    SA_HIP(hipSetDevice(c->device));
+    int rc = ensure_capacity(c, n);
+    if (rc) return rc;
+    uint32_t* phi = d_lcp;
+    uint32_t* v = c->rank;
+    uint32_t* cnt = c->counts;   // [k] = pairs in list k
+    unsigned long long* best = reinterpret_cast<unsigned long long*>(c->words + 8);
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 16384);
+    SA_HIP(hipMemsetAsync(cnt, 0, (kLongRounds + 1) * 4, s));
+    SA_HIP(hipMemsetAsync(best, 0, 8, s));
+    hipLaunchKernelGGL(k_phi, dim3(grid), dim3(kBlock), 0, s, d_sa, n, phi);
+    hipLaunchKernelGGL(k_plcp_irreducible, dim3(grid), dim3(kBlock), 0, s, d_text, n, (const uint32_t*)phi, v,
+                       c->keys[0], c->vals_alt, cnt);
+    uint64_t lo = kDirect;
+    for (int k = 0; k < kLongRounds && lo < n; ++k, lo *= 4) {
+        const uint64_t* list = c->keys[k & 1];
+        uint64_t* next = c->keys[(k + 1) & 1];
+        hipLaunchKernelGGL(k_plcp_long, dim3(4096), dim3(kBlock), 0, s, d_text, n, list,
+                           (const uint32_t*)(cnt + k), lo, std::min<uint64_t>(4 * lo, n), c->vals_alt);
+        hipLaunchKernelGGL(k_plcp_settle, dim3(1024), dim3(kBlock), 0, s, list, (const uint32_t*)(cnt + k),
+                           c->vals_alt, v, next, cnt + k + 1);
+    }
+    const Chunking ch = plan_chunks(n);
+    hipLaunchKernelGGL(k_chunk_max, dim3(ch.chunks), dim3(kBlock), 0, s, (const uint32_t*)v, ch, c->hist);
+    hipLaunchKernelGGL(k_scan_chunk_max, dim3(1), dim3(kBlock), 0, s, c->hist, ch.chunks);
+    hipLaunchKernelGGL(k_plcp_apply, dim3(ch.chunks), dim3(kBlock), 0, s, v, ch, (const uint32_t*)c->hist);
+    hipLaunchKernelGGL(k_lcp_gather, dim3(grid), dim3(kBlock), 0, s, d_sa, n, (const uint32_t*)v, d_lcp, best);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(c->host_words + 8, best, 8, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words + 16, cnt, (kLongRounds + 1) * 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    // every pair resolves by the last window (it reaches n); a pair left over is a bug
+    uint64_t lo_end = kDirect;
+    int rounds = 0;
+    while (rounds < kLongRounds && lo_end < n) { lo_end *= 4; ++rounds; }
+    if (c->host_words[16 + rounds] != 0)
+        return set_err(SA_E_INTERNAL, "%u LCP pairs unresolved", c->host_words[16 + rounds]);
+    SA_TRACE("lcp: direct-overflow pairs %u, rounds %d", c->host_words[16], rounds);
+    unsigned long long b;
+    std::memcpy(&b, c->host_words + 8, 8);
+    const uint64_t len = b >> 32;
+    if (len) {
+        const uint64_t r = 0xFFFFFFFFull - (b & 0xFFFFFFFFull);
+        uint32_t pos = 0;
+        SA_HIP(hipMemcpy(&pos, d_sa + r, 4, hipMemcpyDeviceToHost));
+        if (lrs_len) *lrs_len = len;
+        if (lrs_pos) *lrs_pos = pos;
+    }
+    return SA_OK;
+}
+
+// ---------------------------------------------------------------------------
 // seeded synthetic input on the device (SURVEY.md 8(d) splitmix64 spec), so
 // benchmarks do not push gigabytes over PCIe
 // ---------------------------------------------------------------------------
@@ -880,6 +946,75 @@ int sa_build_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint32_t
 int sa_check_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, void* stream) {
     if (!ctx) return set_err(SA_E_INVALID, "context is NULL");
     return check_device(ctx, d_text, n, d_sa, (hipStream_t)stream);
+}
+
+int sa_lcp_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, uint32_t* d_lcp,
+                  uint64_t* lrs_len, uint64_t* lrs_pos, void* stream) {
+    if (!ctx) return set_err(SA_E_INVALID, "context is NULL");
+    return lcp_device(ctx, d_text, n, d_sa, d_lcp, lrs_len, lrs_pos, (hipStream_t)stream);
+}
+
+int sa_lcp(const uint8_t* text, uint64_t n, const void* sa, int sa_width, void* lcp_out, uint64_t* lrs_len,
+           uint64_t* lrs_pos) {
+    if (lrs_len) *lrs_len = 0;
+    if (lrs_pos) *lrs_pos = 0;
+    if (sa_width != 4 && sa_width != 8) return set_err(SA_E_INVALID, "sa_width must be 4 or 8");
+    if (n == 0) return SA_OK;
+    if (!text || !sa || !lcp_out) return set_err(SA_E_INVALID, "NULL host pointer");
+    if (n > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "n too large");
+    std::vector<uint32_t> narrow;
+    const void* src = sa;
+    if (sa_width == 8) {
+        narrow.resize(n);
+        const int64_t* w = (const int64_t*)sa;
+        for (uint64_t i = 0; i < n; ++i) {
+            if (w[i] < 0 || (uint64_t)w[i] >= n) return set_err(SA_E_INVALID, "SA entry out of range");
+            narrow[i] = (uint32_t)w[i];
+        }
+        src = narrow.data();
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    sa_context* c = nullptr;
+    int rc = global_ctx(n, &c);
+    if (rc) return rc;
+    uint8_t* d_text = nullptr;
+    uint32_t* d_sa = nullptr;
+    uint32_t* d_lcp = nullptr;
+    if (hipMalloc(&d_text, align_up(n, 256)) != hipSuccess || hipMalloc(&d_sa, align_up(n, 64) * 4) != hipSuccess ||
+        hipMalloc(&d_lcp, align_up(n, 64) * 4) != hipSuccess) {
+        hipFree(d_text);
+        hipFree(d_sa);
+        (void)hipGetLastError();
+        return set_err(SA_E_NOMEM, "device allocation failed");
+    }
+    if (hipMemcpy(d_text, text, n, hipMemcpyHostToDevice) != hipSuccess ||
+        hipMemcpy(d_sa, src, n * 4, hipMemcpyHostToDevice) != hipSuccess)
+        rc = set_err(SA_E_HIP, "H2D copy failed");
+    // the checker rejects a non-permutation before PHI would scatter through it
+    if (rc == SA_OK) {
+        rc = check_device(c, d_text, n, d_sa, nullptr);
+        if (rc == 0) rc = set_err(SA_E_INVALID, "not a valid suffix array of the text");
+        else if (rc == 1) rc = SA_OK;
+    }
+    if (rc == SA_OK) rc = lcp_device(c, d_text, n, d_sa, d_lcp, lrs_len, lrs_pos, nullptr);
+    if (rc == SA_OK) {
+        if (sa_width == 4) {
+            if (hipMemcpy(lcp_out, d_lcp, n * 4, hipMemcpyDeviceToHost) != hipSuccess)
+                rc = set_err(SA_E_HIP, "D2H copy failed");
+        } else {
+            std::vector<uint32_t> tmp(n);
+            if (hipMemcpy(tmp.data(), d_lcp, n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
+                rc = set_err(SA_E_HIP, "D2H copy failed");
+            } else {
+                int64_t* o = (int64_t*)lcp_out;
+                for (uint64_t i = 0; i < n; ++i) o[i] = tmp[i];
+            }
+        }
+    }
+    hipFree(d_text);
+    hipFree(d_sa);
+    hipFree(d_lcp);
+    return rc;
 }
 
 int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, const sa_opts* opts,

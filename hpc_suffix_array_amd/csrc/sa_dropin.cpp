@@ -5,9 +5,9 @@
 // extended ABI (sa_build_ex / sa_check).  There is no CPU fallback: on any
 // failure the reason is printed to stderr and the process aborts, the same
 // contract as the reference's assert on allocation failure (manber_myers.c:85).
-// build_lcp_array / find_longest_repeated_substring are host code in this
-// round (Kasai + max scan, manber_myers.c:135-182); they are downstream of
-// the hot path.
+// build_lcp_array runs on the GPU too (sa_lcp); find_longest_repeated_substring
+// keeps the reference's O(n) scan of the caller's lcp array (manber_myers.c:
+// 159-182) -- the device path reports the same answer from sa_lcp_device.
 #include <cstddef>
 #include <cstdint>
 #include <cstdio>
@@ -69,23 +69,12 @@ void build_suffix_array(SuffixArray* sa) {
         die("build_suffix_array");
 }
 
-// Kasai (manber_myers.c:135-157)
+// manber_myers.c:135-157 on the GPU (sa_lcp: PHI / irreducible-LCP method,
+// the values of the reference's Kasai loop); lcp[0] = 0.
 void build_lcp_array(SuffixArray* sa) {
     if (!sa || sa->n <= 0) return;
-    const int n = sa->n;
-    std::vector<int> rank((size_t)n);
-    for (int r = 0; r < n; ++r) rank[(size_t)sa->sa[r]] = r;
-    const unsigned char* t = (const unsigned char*)sa->str;
-    int h = 0;
-    sa->lcp[0] = 0;
-    for (int i = 0; i < n; ++i) {
-        if (rank[(size_t)i] > 0) {
-            const int j = sa->sa[rank[(size_t)i] - 1];
-            while (i + h < n && j + h < n && t[i + h] == t[j + h]) ++h;
-            sa->lcp[rank[(size_t)i]] = h;
-            if (h > 0) --h;
-        }
-    }
+    if (sa_lcp((const uint8_t*)sa->str, (uint64_t)sa->n, sa->sa, 4, sa->lcp, nullptr, nullptr) != SA_OK)
+        die("build_lcp_array");
 }
 
 // manber_myers.c:159-182: first position of the strictly largest LCP.

@@ -253,4 +253,136 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     }
 }
 
+// ---------------------------------------------------------------------------
+// Chunked stable scatter with a one-tile register prefetch (reduce-then-scan
+// radix, the alternative to k_onesweep): the workgroup walks its chunk's
+// tiles in order, so its running per-digit offsets (from k_hist + k_scan_rows)
+// replace the look-back, and the next tile's loads are in flight while the
+// current tile is ranked, staged and written.  BLOCK x ITEMS = kTile, so the
+// chunking and the histogram layout are those of k_hist.
+// ---------------------------------------------------------------------------
+template <class Src, int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK, BLOCK / 128) void k_scatter_pipe(Src src, Chunking ch, uint32_t shift,
+                                                                    uint32_t nbits,
+                                                                    const uint32_t* __restrict__ hist,
+                                                                    const uint32_t* __restrict__ totals,
+                                                                    uint64_t* __restrict__ out_keys,
+                                                                    uint32_t* __restrict__ out_vals) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int TILE = BLOCK * ITEMS;
+    constexpr int WTILE = kWave * ITEMS;
+    static_assert(TILE == kTile, "chunking and histograms assume kTile");
+    static_assert(BLOCK >= kRadix, "one thread per digit");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_vals[TILE];
+    __shared__ uint16_t s_wcnt[WAVES][kRadix];
+    __shared__ uint16_t s_start[kRadix];
+    __shared__ uint32_t s_run[kRadix];
+    __shared__ uint32_t s_tmp[kWaves];
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t mask = (1u << nbits) - 1u;
+    const uint32_t c = blockIdx.x;
+    const uint32_t dg = threadIdx.x;
+    // running global offset of each digit for this chunk
+    {
+        const uint32_t x = dg < (uint32_t)kRadix ? totals[dg] : 0u;
+        const uint32_t inc = wave_inclusive_sum(x);
+        if (lane == kWave - 1 && wave < (uint32_t)kWaves) s_tmp[wave] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+#pragma unroll
+        for (int w = 0; w < kWaves; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+        if (dg < (uint32_t)kRadix) s_run[dg] = off + inc - x + hist[(uint64_t)dg * ch.chunks + c];
+    }
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    uint64_t k[ITEMS], kn[ITEMS];
+    uint32_t v[ITEMS], vn[ITEMS];
+    auto load = [&](uint64_t tb, uint64_t* kk, uint32_t* vv) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + wave * WTILE + j * kWave + lane;
+            const bool ok = e < e1;
+            kk[j] = ok ? src.key(e) : 0ull;
+            vv[j] = ok ? src.val(e) : 0u;
+        }
+    };
+    if (e0 < e1) load(e0, k, v);
+    for (uint64_t tb = e0; tb < e1; tb += TILE) {
+        const uint32_t valid = (uint32_t)((e1 - tb) < (uint64_t)TILE ? (e1 - tb) : (uint64_t)TILE);
+        if (tb + TILE < e1) load(tb + TILE, kn, vn);      // in flight during this tile
+        for (int i = threadIdx.x; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
+        __syncthreads();
+        uint32_t d[ITEMS], r[ITEMS];
+        uint16_t* wc = s_wcnt[wave];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const bool ok = le < valid;
+            d[j] = ok ? (uint32_t)(k[j] >> shift) & mask : kRadix;
+            uint64_t peers = __ballot(ok);
+            for (uint32_t b = 0; b < nbits; ++b) {
+                const bool bit = (d[j] >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            uint32_t cnt = 0;
+            if (ok) cnt = wc[d[j]];
+            const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+            r[j] = cnt + below;
+            if (ok && below == 0) wc[d[j]] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
+        }
+        __syncthreads();
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)kRadix) {
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                const uint32_t x = s_wcnt[w][dg];
+                s_wcnt[w][dg] = (uint16_t)tile_cnt;
+                tile_cnt += x;
+            }
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)kRadix) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)kWaves) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < kWaves; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)kRadix) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            if (d[j] < (uint32_t)kRadix) {
+                const uint32_t pos = s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
+                s_keys[pos] = k[j];
+                s_vals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * BLOCK + threadIdx.x;
+            if (q < valid) {
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = (uint32_t)(key >> shift) & mask;
+                const uint64_t g = (uint64_t)s_run[dd] + (q - s_start[dd]);
+                if (g < ch.n) {
+                    out_keys[g] = key;
+                    out_vals[g] = s_vals[q];
+                }
+            }
+        }
+        __syncthreads();
+        if (dg < (uint32_t)kRadix) s_run[dg] += tile_cnt;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            k[j] = kn[j];
+            v[j] = vn[j];
+        }
+    }
+}
+
 }  // namespace sa

@@ -112,6 +112,19 @@ int sa_check_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const ui
                     void* stream);
 int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width);
 
+/* LCP array and longest repeated substring on the GPU (replaces
+ * build_lcp_array, manber_myers.c:135-157, and the lcp scan of
+ * find_longest_repeated_substring, :159-182).  d_lcp[0] = 0 and
+ * d_lcp[r] = lcp(SA[r-1], SA[r]) (n uint32 in device memory, may not alias
+ * d_sa).  lrs_len / lrs_pos (optional) receive the first r >= 1 with the
+ * strictly largest lcp: its length and SA[r] (0, 0 when nothing repeats).
+ * Synchronises `stream` before returning. */
+int sa_lcp_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, uint32_t* d_lcp,
+                  uint64_t* lrs_len, uint64_t* lrs_pos, void* stream);
+/* Host in, host out: sa and lcp_out have width sa_width (4 or 8). */
+int sa_lcp(const uint8_t* text, uint64_t n, const void* sa, int sa_width, void* lcp_out, uint64_t* lrs_len,
+           uint64_t* lrs_pos);
+
 /* ---- building blocks of the range-partitioned multi-GPU build ----------
  * (hpc_suffix_array_amd/distributed.py drives these per rank; the exchange
  * steps between them are RCCL collectives over xGMI.)                      */
