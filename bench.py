@@ -47,6 +47,16 @@ ALPHABETS = {
 }
 
 
+# bench kernel kind -> the HIP kernel it times (sa_build.hip Timer kinds)
+KERNEL_NAMES = {
+    "scatter_keys": "k_onesweep<SrcKeys|SrcBucketKeys,1024,4> (single-pass radix scatter, stored keys)",
+    "scatter_first": "k_onesweep<SrcKeysIota|SrcBucketIota,1024,4> (single-pass radix scatter, text-order keys)",
+    "local_sort": "k_bucket_sort<1024,18> (per-window LDS radix sort)",
+    "pack": "k_pack_text|k_pack_bucket (packed first-round keys)",
+    "seg_count": "k_seg_count", "seg_write": "k_seg_write", "sort_u": "unsorted-set sorts (k_onesweep<SrcU|SrcKeys>)",
+}
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -61,6 +71,7 @@ def parse():
     ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("--init-chars", type=int, default=0)
     ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
+    ap.add_argument("--round1", default="auto", choices=["auto", "lsd", "bucketed"])
     ap.add_argument("--mode", default="distributed", choices=["distributed", "replicas"],
                     help="N > 1: one string over all ranks, or one string per rank")
     ap.add_argument("--json-out", default=None)
@@ -137,7 +148,8 @@ def run_single(a, torch, dev, world, rank, barrier):
     d_sa = torch.empty(n, dtype=torch.int32, device=dev)
     torch.cuda.synchronize(dev)
     profile = not a.no_profile
-    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars, radix=a.radix)
+    bkw = dict(stream=sptr, profile=profile, schedule=a.schedule, init_chars=a.init_chars, radix=a.radix,
+               round1=a.round1)
     elapsed, stats = timed(a.steps, a.warmup, lambda: b.build(d_text, n, d_sa, **bkw), barrier)
     verified = b.check(d_text, n, d_sa, stream=sptr)
 
@@ -146,20 +158,33 @@ def run_single(a, torch, dev, world, rank, barrier):
     kern = {}
     for k in stats[-1]["kernels"]:
         kern[k] = {key: sum(s["kernels"][k][key] for s in stats) for key in ("ms", "launches", "bytes")}
-    dom = "scatter_keys"
+    bucketed = stats[-1].get("round1") == "bucketed"
     roofline = None
-    if profile and kern[dom]["launches"]:
-        avg_s = kern[dom]["ms"] / kern[dom]["launches"] / 1e3
-        per_launch = kern[dom]["bytes"] / kern[dom]["launches"]
-        ach = per_launch / avg_s / 1e9
-        traffic = None
-        pmc = pmc_summary()
-        if pmc and pmc.get("n") == n and pmc.get("kind") == a.kind:
-            traffic = pmc.get("traffic_bytes_per_launch", {}).get("scatter_keys")
-        roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
-                    "kernel": "k_onesweep<SrcKeys,1024,4> (single-pass radix scatter, stored keys)",
-                    "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
+    per_kernel = None
+    if profile:
+        # achieved GB/s of every kind: algorithmic bytes per launch / mean
+        # HIP-event duration of its launches (all on the build's stream)
+        per_kernel = {}
+        for k, v in kern.items():
+            if v["launches"] and v["ms"] > 0 and v["bytes"]:
+                per_kernel[k] = {"ms_per_step": round(v["ms"] / a.steps, 3), "launches_per_step": v["launches"] / a.steps,
+                                 "gbs": round(v["bytes"] / (v["ms"] / 1e3) / 1e9, 1)}
+        # the dominant kernel: most time per step
+        cand = {k: v for k, v in kern.items() if k not in ("scan",) and v["launches"] and v["bytes"]}
+        dom = max(cand, key=lambda k: cand[k]["ms"]) if cand else None
+        if dom:
+            avg_s = kern[dom]["ms"] / kern[dom]["launches"] / 1e3
+            per_launch = kern[dom]["bytes"] / kern[dom]["launches"]
+            ach = per_launch / avg_s / 1e9
+            traffic = None
+            pmc = pmc_summary()
+            if pmc and pmc.get("n") == n and pmc.get("kind") == a.kind:
+                skind = {"scatter_first": "scatter_first" if bucketed else "scatter_iota"}.get(dom, dom)
+                traffic = pmc.get("traffic_bytes_per_launch", {}).get(skind)
+            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "kernel": KERNEL_NAMES.get(dom, dom) + (" [bucketed round 1]" if bucketed else ""),
+                        "kind": dom, "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
     extra = {
         "ms_per_round": [round(x, 3) for x in round_ms],
         "rounds": rounds,
@@ -172,8 +197,11 @@ def run_single(a, torch, dev, world, rank, barrier):
         "sigma": stats[-1]["sigma"],
         "sparse_ranks": stats[-1]["sparse_ranks"],
         "model_bytes": stats[-1]["model_bytes"],
+        "round1": stats[-1].get("round1"),
+        "largest_window": stats[-1].get("largest_window"),
         "verified": verified,
         "roofline": roofline,
+        "kernels_gbs": per_kernel,
         "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
     }
     b.close()

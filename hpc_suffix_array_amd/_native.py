@@ -18,9 +18,12 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 SA_MAX_ROUNDS = 64
 KERNEL_KINDS = ["init", "hist_first", "hist_keys", "scan", "scatter_first", "scatter_keys",
                 "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet", "pack",
-                "sort_u"]
+                "sort_u", "windows", "local_sort"]
 SCHEDULE_PACKED = 0
 SCHEDULE_REFERENCE = 1
+ROUND1_AUTO = 0
+ROUND1_LSD = 1
+ROUND1_BUCKETED = 2
 SA_K_COUNT = len(KERNEL_KINDS)
 
 # every symbol include/*.h declares
@@ -38,7 +41,7 @@ class SAError(RuntimeError):
 
 class SaOpts(ctypes.Structure):
     _fields_ = [("profile", ctypes.c_int32), ("schedule", ctypes.c_int32), ("init_chars", ctypes.c_int32),
-                ("radix", ctypes.c_int32), ("reserved", ctypes.c_int32 * 4)]
+                ("radix", ctypes.c_int32), ("round1", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
 
 
 class SaStats(ctypes.Structure):
@@ -57,6 +60,8 @@ class SaStats(ctypes.Structure):
         ("init_chars", ctypes.c_int32),
         ("sigma", ctypes.c_int32),
         ("sparse_ranks", ctypes.c_int32),
+        ("round1", ctypes.c_int32),
+        ("largest_window", ctypes.c_int32),
         ("model_bytes", ctypes.c_uint64),
         ("kern_ms", ctypes.c_double * SA_K_COUNT),
         ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
@@ -79,6 +84,8 @@ class SaStats(ctypes.Structure):
             "init_chars": self.init_chars,
             "sigma": self.sigma,
             "sparse_ranks": bool(self.sparse_ranks),
+            "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed"}.get(self.round1, "lsd"),
+            "largest_window": self.largest_window,
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

@@ -32,20 +32,23 @@ def _as_bytes_array(text) -> np.ndarray:
 
 SCHEDULES = {"packed": N.SCHEDULE_PACKED, "reference": N.SCHEDULE_REFERENCE}
 RADIX = {"onesweep": 0, "reduce_scan": 1}
+ROUND1 = {"auto": N.ROUND1_AUTO, "lsd": N.ROUND1_LSD, "bucketed": N.ROUND1_BUCKETED}
 
 
 def _opts(profile: bool = False, schedule: str = "packed", init_chars: int = 0,
-          radix: str = "onesweep") -> N.SaOpts:
+          radix: str = "onesweep", round1: str = "auto") -> N.SaOpts:
     o = N.SaOpts()
     o.profile = 1 if profile else 0
     o.schedule = SCHEDULES[schedule]
     o.init_chars = int(init_chars)
     o.radix = RADIX[radix]
+    o.round1 = ROUND1[round1]
     return o
 
 
 def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False,
-                       schedule: str = "packed", init_chars: int = 0, radix: str = "onesweep"):
+                       schedule: str = "packed", init_chars: int = 0, radix: str = "onesweep",
+                       round1: str = "auto"):
     """Suffix array of ``text`` (bytes / uint8 array), built on the GPU.
 
     Unsigned-byte order, end of string smallest (== the reference's order on
@@ -53,7 +56,9 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     int64 (width 8); with ``return_stats`` also the per-round statistics.
     ``schedule``: "packed" (default; packed K-symbol first round, later rounds
     re-sort unsorted groups only) or "reference" (h = 1, 2, 4, ... over all
-    n suffixes, round for round as manber_myers.c:94-125)."""
+    n suffixes, round for round as manber_myers.c:94-125).  ``round1``
+    (packed): "auto", "lsd" (full radix sort of the packed first key) or
+    "bucketed" (two bucket passes + per-window LDS sort)."""
     t = _as_bytes_array(text)
     n = int(t.size)
     N.require_device()
@@ -61,7 +66,7 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     st = N.SaStats()
     L = N.lib()
     N.check(L.sa_build_ex(t.ctypes.data if n else None, n, out.ctypes.data, width,
-                          ctypes.byref(_opts(profile, schedule, init_chars, radix)), ctypes.byref(st)),
+                          ctypes.byref(_opts(profile, schedule, init_chars, radix, round1)), ctypes.byref(st)),
             "sa_build_ex")
     out = out[:n]
     return (out, st.to_dict()) if return_stats else out
@@ -193,12 +198,12 @@ class DeviceBuilder:
         return x if isinstance(x, int) else int(x.data_ptr())
 
     def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False, schedule: str = "packed",
-              init_chars: int = 0, radix: str = "onesweep") -> dict:
+              init_chars: int = 0, radix: str = "onesweep", round1: str = "auto") -> dict:
         """Build the SA of the n bytes at d_text into the n uint32 at d_sa."""
         st = N.SaStats()
         s = None if stream is None else ctypes.c_void_p(int(stream))
         N.check(self.L.sa_build_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s,
-                                       ctypes.byref(_opts(profile, schedule, init_chars, radix)),
+                                       ctypes.byref(_opts(profile, schedule, init_chars, radix, round1)),
                                        ctypes.byref(st)),
                 "sa_build_device")
         return st.to_dict()

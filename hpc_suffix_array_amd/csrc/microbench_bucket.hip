@@ -1,0 +1,122 @@
+// microbench_bucket.hip -- the bucketed first round's local sort in
+// isolation: n synthetic key1-like keys already in bucket order (bucket =
+// top 16 bits, rising with the position; low bits random), the window
+// kernels of sa_bucket.h, then k_bucket_sort variants against a streaming
+// copy of the same 12 bytes per suffix in and out.  Not part of libsa_hip.
+//   build: make -C hpc_suffix_array_amd/csrc microbench_bucket
+//   run:   hpc_suffix_array_amd/csrc/build/microbench_bucket [log2 n] [reps]
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "sa_bucket.h"
+
+using namespace sa;
+
+#define CK(x)                                                                                 \
+    do {                                                                                      \
+        hipError_t e_ = (x);                                                                  \
+        if (e_ != hipSuccess) {                                                               \
+            std::fprintf(stderr, "%s: %s (%s:%d)\n", #x, hipGetErrorString(e_), __FILE__, __LINE__); \
+            std::exit(1);                                                                     \
+        }                                                                                     \
+    } while (0)
+
+// key = bucket << rb | random rb bits, bucket = (i << 16) / n; rb = 28
+__global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        keys[i] = ((i << 16) / n << rb) | (z & ((1ull << rb) - 1));
+        vals[i] = (uint32_t)(z >> 32);
+    }
+}
+
+__global__ void k_copy12(const uint64_t* __restrict__ a, const uint32_t* __restrict__ av, uint64_t n,
+                         uint64_t* __restrict__ b, uint32_t* __restrict__ bv) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        b[i] = a[i];
+        bv[i] = av[i];
+    }
+}
+
+int main(int argc, char** argv) {
+    const int lg = argc > 1 ? std::atoi(argv[1]) : 30;
+    const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
+    const uint64_t n = 1ull << lg;
+    const uint32_t rb = 28, ib = lg;
+    uint64_t *keys, *okeys;
+    uint32_t *vals, *ovals, *ws, *words;
+    CK(hipMalloc(&keys, n * 8));
+    CK(hipMalloc(&okeys, n * 8));
+    CK(hipMalloc(&vals, n * 4));
+    CK(hipMalloc(&ovals, n * 4));
+    const uint64_t nw = (n + kWinStride - 1) / kWinStride;
+    CK(hipMalloc(&ws, (3 * nw + 2) * 4));
+    CK(hipMalloc(&words, 64));
+    uint32_t* list = ws + nw + 1;
+    uint32_t* skew = list + nw;
+    hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, n, rb);
+    CK(hipMemset(words, 0, 64));
+    const uint64_t cmul = 1ull << 32;   // bucket = D (16 bits)
+    hipLaunchKernelGGL(k_window_starts, dim3((uint32_t)std::min<uint64_t>((nw + 256) / 256, 8192)), dim3(256), 0, 0,
+                       (const uint64_t*)keys, n, nw, rb, cmul, ws);
+    hipLaunchKernelGGL(k_window_list, dim3((uint32_t)std::min<uint64_t>((nw + 255) / 256, 1024)), dim3(256), 0, 0,
+                       (const uint32_t*)ws, nw, list, words);
+    CK(hipDeviceSynchronize());
+    uint32_t hw[16];
+    CK(hipMemcpy(hw, words, 64, hipMemcpyDeviceToHost));
+    std::printf("n=2^%d windows=%u largest=%u\n", lg, hw[7], hw[5]);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    auto timeit = [&](const char* name, auto launch) {
+        launch();
+        CK(hipDeviceSynchronize());
+        float best = 1e30f;
+        for (int r = 0; r < reps; ++r) {
+            CK(hipEventRecord(e0));
+            launch();
+            CK(hipEventRecord(e1));
+            CK(hipEventSynchronize(e1));
+            float ms;
+            CK(hipEventElapsedTime(&ms, e0, e1));
+            best = std::min(best, ms);
+        }
+        std::printf("%-40s %8.3f ms  %7.1f GB/s (24 B/suffix)\n", name, best, 24.0 * n / best / 1e6);
+    };
+    timeit("copy 12 B in + out", [&] {
+        hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
+    });
+    for (uint32_t g : {256u, 512u, 1024u}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               words, ib, okeys, ovals, skew);
+        });
+        std::snprintf(nm, sizeof nm, "bucket_sort no-sort grid %u", g);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 1>), dim3(g), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               words, ib, okeys, ovals, skew);
+        });
+    }
+    CK(hipMemcpy(hw, words, 64, hipMemcpyDeviceToHost));
+    std::printf("flags=%u skewed=%u\n", hw[6], hw[10]);
+    // check: output sorted within each window, keys monotone overall
+    std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(256), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
+                       (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew);
+    CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
+    size_t bad = 0;
+    for (size_t i = 1; i < h.size(); ++i) bad += h[i] < h[i - 1];
+    std::printf("unsorted adjacent pairs in the first %zu: %zu\n", h.size(), bad);
+    return 0;
+}

@@ -1,0 +1,571 @@
+// sa_bucket.h -- bucketed first round of the packed schedule: two global
+// radix passes over a 16-bit bucket of each suffix's prefix, then one
+// workgroup sorts each bucket window in LDS.
+//
+// The first round sorts every suffix by its first K symbols (it replaces
+// rounds h = 1 .. K/2 of manber_myers.c:97-125).  A full LSD sort of a
+// 47-bit key is six 24-byte-per-suffix passes over HBM; here the key is
+// laid out so that its order is (bucket, rest):
+//
+//   D(i)   = sum_{t<s} dc(i+t) sigma^(s-1-t)     dense s-symbol prefix,
+//            dc = code - 1 (codes 1..sigma), 0 past the end
+//   low(i) = L - 1                        if L = n - i < s  (shorter than s)
+//            s + E(i) (R+1) + min(R, L-s)  otherwise, E(i) = the next R symbols
+//            as dense digits dc (0 past the end) and min(R, L-s) how many of
+//            them precede the end
+//   key1(i) = D(i) << rb | low(i)
+//
+// key1 orders suffixes exactly as their first K = s + R symbols (end
+// smallest) and two suffixes get equal key1 iff those K symbols are equal.
+// The end digit is clamped onto the smallest symbol's digit, so a suffix
+// that ends inside a window shares its dense value with the suffixes that
+// continue it with the smallest symbol; the count of symbols before the end
+// (for L < s: L - 1 < s, below every longer suffix) puts it, and shorter
+// ones first, ahead of them.  Both fields are dense, so for random text the
+// 16-bit bucket = (D * cmul) >> 32 (sigma^s >= 2^16) and the top bits of
+// low are near-uniform.
+//
+//   k_pack_bucket     text -> key1 in text order (+ the digit totals of the
+//                     two bucket passes)
+//   2 x k_onesweep    stable LSD passes over the bucket's two bytes
+//                     (SrcBucketIota, SrcBucketKeys)
+//   k_window_starts   window j starts at the first bucket boundary >= j*W
+//   k_window_max      largest window (the host checks it against the LDS
+//                     capacity; oversize windows fall back to the full sort)
+//   k_bucket_sort     one workgroup per window: LSD radix in LDS over the
+//                     bits of key1 - min(window) (ascending idx packed below)
+//                     -> sorted key1 + SA, both written coalesced
+#pragma once
+#include "sa_kernels.h"
+
+namespace sa {
+
+constexpr int kBsBlock = 1024;               // local sort workgroup (16 waves)
+constexpr int kBsItems = 18;                 // per thread
+constexpr int kBsCap = kBsBlock * kBsItems;  // 18432 suffixes per window (147 KiB of LDS)
+constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
+constexpr uint32_t kBsGrid = 256;            // one local-sort workgroup per CU (LDS-bound)
+constexpr uint64_t kBucketMinN = 1ull << 20; // auto: bucketed first round from 1 Mi suffixes
+
+__device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64_t cmul) {
+    return (uint32_t)(((key1 >> rb) * cmul) >> 32);
+}
+
+// radix sources of the two bucket passes (digits of bucket_of(key))
+struct SrcBucketIota {
+    const uint64_t* __restrict__ keys;
+    uint32_t rb;
+    uint64_t cmul;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
+    __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
+        return (bucket_of(k, rb, cmul) >> shift) & mask;
+    }
+};
+
+struct SrcBucketKeys {
+    const uint64_t* __restrict__ keys;
+    const uint32_t* __restrict__ vals;
+    uint32_t rb;
+    uint64_t cmul;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return vals[e]; }
+    __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
+        return (bucket_of(k, rb, cmul) >> shift) & mask;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// key1 in text order.  Like k_pack_text: a tile of codes (+ K-1 halo) staged
+// in LDS, 16 consecutive keys per lane (Horner for the first, rolling
+// updates of D and of the remainder for the rest), staged again in LDS for a
+// coalesced store; LDS histograms of the two bucket bytes -> ghist[2][256].
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restrict__ text, uint64_t n,
+                                                        const uint16_t* __restrict__ code, Chunking ch,
+                                                        BucketSpec b, uint64_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ ghist) {
+    __shared__ uint16_t s_code[256];
+    __shared__ uint16_t s_c[kTile + kMaxK];
+    __shared__ uint32_t s_hist[2][kRadix];
+    __shared__ uint64_t s_k[kTile + kTile / kPackRun];
+    s_code[threadIdx.x] = code[threadIdx.x];
+    s_hist[0][threadIdx.x] = 0;
+    s_hist[1][threadIdx.x] = 0;
+    const uint32_t K = b.s + b.R;
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    __syncthreads();
+    for (uint64_t tb = e0; tb < e1; tb += kTile) {
+        {
+            const uint64_t i = tb + (uint64_t)threadIdx.x * 16;
+            uint16_t* dst = s_c + threadIdx.x * 16;
+            if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
+                const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) dst[4 * q + y] = s_code[(w4[q] >> (8 * y)) & 0xFFu];
+            } else {
+                for (int q = 0; q < 16; ++q) dst[q] = (i + q < n) ? s_code[text[i + q]] : (uint16_t)0;
+            }
+            if (threadIdx.x < K) {
+                const uint64_t h = tb + kTile + threadIdx.x;
+                s_c[kTile + threadIdx.x] = (h < n) ? s_code[text[h]] : (uint16_t)0;
+            }
+        }
+        __syncthreads();
+        const uint32_t l0 = threadIdx.x * kPackRun;
+        auto dc = [](uint32_t x) -> uint64_t { return x ? x - 1u : 0u; };
+        uint64_t D = 0, r = 0;
+        for (uint32_t t = 0; t < b.s; ++t) D = D * b.sigma + dc(s_c[l0 + t]);
+        for (uint32_t t = 0; t < b.R; ++t) r = r * b.sigma + dc(s_c[l0 + b.s + t]);
+        uint64_t* kd = s_k + threadIdx.x * (kPackRun + 1);
+#pragma unroll
+        for (int j = 0; j < kPackRun; ++j) {
+            if (j > 0) {
+                const uint64_t xi = dc(s_c[l0 + j - 1 + b.s]);
+                D = (D - dc(s_c[l0 + j - 1]) * b.pow_s1) * b.sigma + xi;
+                r = (r - xi * b.powR1) * b.sigma + dc(s_c[l0 + j - 1 + b.s + b.R]);
+            }
+            const uint64_t i = tb + l0 + j;
+            const uint64_t L = n - i;   // wraps past the end: never stored
+            const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+            const uint64_t low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
+            const uint64_t key = (D << b.rb) | low;
+            kd[j] = key;
+            if (i < e1) {
+                const uint32_t bk = bucket_of(key, b.rb, b.cmul);
+                atomicAdd(&s_hist[0][bk & 0xFFu], 1u);
+                atomicAdd(&s_hist[1][(bk >> 8) & 0xFFu], 1u);
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < kPackRun; ++j) {
+            const uint32_t q = j * kBlock + threadIdx.x;
+            const uint64_t g = tb + q;
+            if (g < e1) keys[g] = s_k[q + q / kPackRun];
+        }
+        __syncthreads();
+    }
+    for (int p = 0; p < 2; ++p) {
+        const uint32_t v = s_hist[p][threadIdx.x];
+        if (v) atomicAdd(&ghist[p * kRadix + threadIdx.x], v);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// window starts over the bucket-sorted keys: ws[j] = first g >= j*W with
+// g == 0, g == n or bucket(g) != bucket(g-1) (gallop, then bisect); j <= nw.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_window_starts(const uint64_t* __restrict__ keys, uint64_t n,
+                                                          uint64_t nw, uint32_t rb, uint64_t cmul,
+                                                          uint32_t* __restrict__ ws) {
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j <= nw; j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t x = j * kWinStride;
+        uint64_t res;
+        if (x >= n) {
+            res = n;
+        } else if (x == 0) {
+            res = 0;
+        } else {
+            const uint32_t bx = bucket_of(keys[x - 1], rb, cmul);
+            if (bucket_of(keys[x], rb, cmul) != bx) {
+                res = x;
+            } else {
+                uint64_t lo = x, hi, step = 1;   // bucket(lo) == bx
+                for (;;) {
+                    hi = lo + step;
+                    if (hi >= n) {
+                        hi = n;
+                        break;
+                    }
+                    if (bucket_of(keys[hi], rb, cmul) != bx) break;
+                    lo = hi;
+                    step *= 2;
+                }
+                while (hi - lo > 1) {   // first index in (lo, hi] past bucket bx (n counts)
+                    const uint64_t mid = lo + (hi - lo) / 2;
+                    if (bucket_of(keys[mid], rb, cmul) != bx) hi = mid;
+                    else lo = mid;
+                }
+                res = hi;
+            }
+        }
+        ws[j] = (uint32_t)res;
+    }
+}
+
+// Non-empty windows -> list (any order: windows are independent), their
+// number -> words[7] (one atomic per workgroup), the largest -> words[5].
+__global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restrict__ ws, uint64_t nw,
+                                                        uint32_t* __restrict__ list, uint32_t* __restrict__ words) {
+    __shared__ uint32_t s_n[kWaves], s_base;
+    __shared__ uint32_t s_mx[kWaves];
+    const uint32_t lane = lane_id(), wave = wave_id();
+    const uint64_t per = ((nw + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
+    const uint64_t j0 = (uint64_t)blockIdx.x * per, j1 = j0 + per < nw ? j0 + per : nw;
+    uint32_t mx = 0;
+    for (uint64_t jb = j0; jb < j1; jb += kBlock) {
+        const uint64_t j = jb + threadIdx.x;
+        const uint32_t d = j < j1 ? ws[j + 1] - ws[j] : 0u;
+        mx = d > mx ? d : mx;
+        const uint64_t bal = __ballot(d != 0);
+        if (lane == 0) s_n[wave] = (uint32_t)__popcll(bal);
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int x = 0; x < kWaves; ++x) {
+                const uint32_t c = s_n[x];
+                s_n[x] = t;
+                t += c;
+            }
+            s_base = t ? atomicAdd(&words[7], t) : 0u;
+        }
+        __syncthreads();
+        if (d) list[s_base + s_n[wave] + (uint32_t)__popcll(bal & lanemask_lt())] = (uint32_t)j;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const uint32_t y = __shfl_xor(mx, o, kWave);
+        mx = y > mx ? y : mx;
+    }
+    if (lane == 0) s_mx[wave] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int x = 0; x < kWaves; ++x) t = s_mx[x] > t ? s_mx[x] : t;
+        if (t) atomicMax(&words[5], t);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Local sort of each listed window [ws[j], ws[j+1]) (whole buckets, at most
+// CAP suffixes).  w = (key1 - min) << ib | idx (ib = bit width of n - 1) is
+// unique per suffix, so no step has to be stable:
+//   1. counting scatter on the top kSubBits of the key span: LDS histogram
+//      (16-bit counters packed in pairs, atomics), scan, atomic cursors ->
+//      s_w holds 2^kSubBits sub-buckets of a few suffixes each (random text);
+//   2. each suffix counts the smaller keys of its sub-bucket (its rank in
+//      it), then all move to their final slots;
+//   3. s_w is written out in order: sorted key1 and SA, coalesced.
+// A window with a sub-bucket above kMaxSub (many equal or clustered keys) is
+// appended to `skew` (count in words[10]) and left to k_bucket_sort_lsd.
+// err bit 0: window larger than the LDS tile; bit 1: key span too wide.
+// ---------------------------------------------------------------------------
+constexpr int kSubBits = 12;
+constexpr int kSubBuckets = 1 << kSubBits;
+constexpr uint32_t kMaxSub = 64;
+
+// window j's keys -> registers as w = (key1 - min) << ib | idx; false (and the
+// error flag) when the key span does not fit beside the index bits
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ bool load_window(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+                                            uint64_t a, uint32_t m, uint32_t ib, uint64_t (&w)[ITEMS], uint64_t& mn,
+                                            uint32_t& bits, uint64_t (*s_red)[BLOCK / kWave],
+                                            uint32_t* __restrict__ err) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int WT = kWave * ITEMS;
+    const uint32_t wave = wave_id(), lane = lane_id();
+    uint32_t v[ITEMS];
+    uint64_t mx = 0;
+    mn = ~0ull;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t le = wave * WT + i * kWave + lane;
+        if (le < m) {
+            w[i] = keys_in[a + le];
+            v[i] = vals_in[a + le];
+            mn = w[i] < mn ? w[i] : mn;
+            mx = w[i] > mx ? w[i] : mx;
+        } else {
+            w[i] = 0;
+            v[i] = 0;
+        }
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const uint64_t y0 = __shfl_xor(mn, o, kWave), y1 = __shfl_xor(mx, o, kWave);
+        mn = y0 < mn ? y0 : mn;
+        mx = y1 > mx ? y1 : mx;
+    }
+    if (lane == 0) {
+        s_red[0][wave] = mn;
+        s_red[1][wave] = mx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int x = 0; x < WAVES; ++x) {
+        mn = s_red[0][x] < mn ? s_red[0][x] : mn;
+        mx = s_red[1][x] > mx ? s_red[1][x] : mx;
+    }
+    bits = (mx - mn) ? 64u - (uint32_t)__clzll(mx - mn) : 0u;
+    if (bits + ib > 64) {   // uniform over the block
+        if (threadIdx.x == 0) atomicOr(err, 2u);
+        return false;
+    }
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) w[i] = ((w[i] - mn) << ib) | v[i];
+    return true;
+}
+
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ void store_window(const uint64_t* __restrict__ s_w, uint64_t a, uint32_t m, uint32_t ib,
+                                             uint64_t mn, uint64_t* __restrict__ keys_out,
+                                             uint32_t* __restrict__ sa_out) {
+    constexpr int WT = kWave * ITEMS;
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t le = wave * WT + i * kWave + lane;
+        if (le < m) {
+            const uint64_t x = s_w[le];
+            keys_out[a + le] = (x >> ib) + mn;
+            sa_out[a + le] = (uint32_t)(x & imask);
+        }
+    }
+}
+
+// kVariant (microbenchmarks only; 0 in the product): 1 skips the sort (the
+// loaded window is written back in input order)
+template <int BLOCK, int ITEMS, int kVariant = 0>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
+                                                       const uint32_t* __restrict__ vals_in,
+                                                       const uint32_t* __restrict__ ws,
+                                                       const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
+                                                       uint32_t ib, uint64_t* __restrict__ keys_out,
+                                                       uint32_t* __restrict__ sa_out, uint32_t* __restrict__ skew) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int CAP = BLOCK * ITEMS;
+    constexpr int WT = kWave * ITEMS;
+    __shared__ uint64_t s_w[CAP];
+    __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
+    __shared__ uint32_t s_tmp[WAVES];
+    __shared__ uint64_t s_red[2][WAVES];
+    static_assert(kSubBuckets == 4 * BLOCK, "four sub-buckets (two words) per thread");
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    uint32_t* err = words + 6;
+    const uint32_t nlist = words[7];
+    auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
+    for (uint32_t q = blockIdx.x; q < nlist; q += gridDim.x) {
+        const uint32_t j = list[q];
+        const uint64_t a = ws[j];
+        const uint32_t m = (uint32_t)(ws[j + 1] - a);
+        if (m > (uint32_t)CAP) {
+            if (threadIdx.x == 0) atomicOr(err, 1u);
+            continue;
+        }
+        for (int i = threadIdx.x; i < kSubBuckets / 2; i += BLOCK) s_cnt[i] = 0;
+        uint64_t w[ITEMS];
+        uint64_t mn;
+        uint32_t bits;
+        if (!load_window<BLOCK, ITEMS>(keys_in, vals_in, a, m, ib, w, mn, bits, s_red, err)) {
+            __syncthreads();
+            continue;
+        }
+        const uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
+        if constexpr ((kVariant & 1) != 0) {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i)
+                if (wave * WT + i * kWave + lane < m) s_w[wave * WT + i * kWave + lane] = w[i];
+            __syncthreads();
+            store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+            __syncthreads();
+            continue;
+        }
+        // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            if (wave * WT + i * kWave + lane < m) {
+                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+            }
+        }
+        __syncthreads();
+        // exclusive scan of the 4096 counts (four per thread) and their maximum
+        uint32_t big = 0;
+        {
+            const uint32_t p0 = s_cnt[2 * dg], p1 = s_cnt[2 * dg + 1];
+            const uint32_t c0 = p0 & 0xFFFFu, c1 = p0 >> 16, c2 = p1 & 0xFFFFu, c3 = p1 >> 16;
+            const uint32_t sum = c0 + c1 + c2 + c3;
+            const uint32_t inc = wave_inclusive_sum(sum);
+            uint32_t cm = c0 > c1 ? c0 : c1;
+            cm = c2 > cm ? c2 : cm;
+            cm = c3 > cm ? c3 : cm;
+#pragma unroll
+            for (int o = kWave / 2; o > 0; o >>= 1) {
+                const uint32_t y = __shfl_xor(cm, o, kWave);
+                cm = y > cm ? y : cm;
+            }
+            if (lane == kWave - 1) s_tmp[wave] = inc;
+            if (lane == 0) s_red[0][wave] = cm;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int x = 0; x < WAVES; ++x) {
+                off += (x < (int)wave) ? s_tmp[x] : 0u;
+                big = (uint32_t)s_red[0][x] > big ? (uint32_t)s_red[0][x] : big;
+            }
+            const uint32_t b0 = off + inc - sum, b1 = b0 + c0, b2 = b1 + c1, b3 = b2 + c2;
+            s_cnt[2 * dg] = b0 | (b1 << 16);
+            s_cnt[2 * dg + 1] = b2 | (b3 << 16);
+        }
+        __syncthreads();
+        if (big > kMaxSub) {   // uniform: clustered keys, leave the window to the LSD kernel
+            if (threadIdx.x == 0) skew[atomicAdd(&words[10], 1u)] = j;
+            __syncthreads();
+            continue;
+        }
+        // 2. scatter into sub-buckets (any order inside one) ...
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            if (wave * WT + i * kWave + lane < m) {
+                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                s_w[(old >> (16 * (sb & 1))) & 0xFFFFu] = w[i];
+            }
+        }
+        __syncthreads();
+        // ... rank inside the sub-bucket by counting smaller keys ...
+        uint32_t pos[ITEMS];
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            pos[i] = 0;
+            if (wave * WT + i * kWave + lane < m) {
+                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
+                uint32_t r = lo;
+                for (uint32_t y = lo; y < hi; ++y) r += s_w[y] < w[i] ? 1u : 0u;
+                pos[i] = r;
+            }
+        }
+        __syncthreads();
+        // ... and move to the final slot
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i)
+            if (wave * WT + i * kWave + lane < m) s_w[pos[i]] = w[i];
+        __syncthreads();
+        // 3. out, in order
+        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+        __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
+    }
+}
+
+// The skewed windows: stable LSD passes of 8 bits over the key span, each an
+// in-wave ranking (match-any from 8 ballots, wave-major input order), per-
+// digit wave prefixes, digit offsets, scatter into LDS, read back in order.
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __restrict__ keys_in,
+                                                           const uint32_t* __restrict__ vals_in,
+                                                           const uint32_t* __restrict__ ws,
+                                                           const uint32_t* __restrict__ skew,
+                                                           uint32_t* __restrict__ words, uint32_t ib,
+                                                           uint64_t* __restrict__ keys_out,
+                                                           uint32_t* __restrict__ sa_out) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int CAP = BLOCK * ITEMS;
+    constexpr int WT = kWave * ITEMS;
+    static_assert(BLOCK >= kRadix, "one thread per digit");
+    static_assert(CAP <= 65535, "16-bit LDS offsets");
+    __shared__ uint64_t s_w[CAP];
+    __shared__ uint16_t s_wcnt[WAVES][kRadix];
+    __shared__ uint16_t s_start[kRadix];
+    __shared__ uint32_t s_tmp[kWaves];
+    __shared__ uint64_t s_red[2][WAVES];
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    uint32_t* err = words + 6;
+    const uint32_t nskew = words[10];
+    for (uint32_t q = blockIdx.x; q < nskew; q += gridDim.x) {
+        const uint32_t j = skew[q];
+        const uint64_t a = ws[j];
+        const uint32_t m = (uint32_t)(ws[j + 1] - a);
+        uint64_t w[ITEMS];
+        uint64_t mn;
+        uint32_t bits;
+        if (!load_window<BLOCK, ITEMS>(keys_in, vals_in, a, m, ib, w, mn, bits, s_red, err)) {
+            __syncthreads();
+            continue;
+        }
+        const uint32_t passes = (bits + 7) / 8;
+        for (uint32_t p = 0; p < passes; ++p) {
+            const uint32_t sh = ib + 8 * p;
+            for (int i = threadIdx.x; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
+            __syncthreads();
+            uint32_t r[ITEMS];
+            uint16_t* wc = s_wcnt[wave];
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t le = wave * WT + i * kWave + lane;
+                const bool ok = le < m;
+                const uint32_t d = ok ? (uint32_t)(w[i] >> sh) & 0xFFu : (uint32_t)kRadix;
+                uint64_t peers = __ballot(ok);
+#pragma unroll
+                for (uint32_t bt = 0; bt < 8; ++bt) {
+                    const bool bit = (d >> bt) & 1u;
+                    const uint64_t bal = __ballot(bit);
+                    peers &= bit ? bal : ~bal;
+                }
+                uint32_t cnt = 0;
+                if (ok) cnt = wc[d];
+                const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+                r[i] = cnt + below;
+                if (ok && below == 0) wc[d] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
+            }
+            __syncthreads();
+            uint32_t tot = 0;
+            if (dg < (uint32_t)kRadix) {
+#pragma unroll
+                for (int x = 0; x < WAVES; ++x) {
+                    const uint32_t y = s_wcnt[x][dg];
+                    s_wcnt[x][dg] = (uint16_t)tot;
+                    tot += y;
+                }
+            }
+            {
+                const uint32_t x = (dg < (uint32_t)kRadix) ? tot : 0u;
+                const uint32_t inc = wave_inclusive_sum(x);
+                if (lane == kWave - 1 && wave < (uint32_t)kWaves) s_tmp[wave] = inc;
+                __syncthreads();
+                uint32_t off = 0;
+#pragma unroll
+                for (int x2 = 0; x2 < kWaves; ++x2) off += (x2 < (int)wave) ? s_tmp[x2] : 0u;
+                if (dg < (uint32_t)kRadix) s_start[dg] = (uint16_t)(off + inc - x);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                if (wave * WT + i * kWave + lane < m) {
+                    const uint32_t d = (uint32_t)(w[i] >> sh) & 0xFFu;
+                    s_w[s_start[d] + s_wcnt[wave][d] + r[i]] = w[i];
+                }
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t le = wave * WT + i * kWave + lane;
+                if (le < m) w[i] = s_w[le];
+            }
+            __syncthreads();
+        }
+        if (passes == 0) {   // one key: input order
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t le = wave * WT + i * kWave + lane;
+                if (le < m) s_w[le] = w[i];
+            }
+            __syncthreads();
+        }
+        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+        __syncthreads();
+    }
+}
+
+}  // namespace sa

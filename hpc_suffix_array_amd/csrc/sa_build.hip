@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "../../include/sa_hip.h"
+#include "sa_bucket.h"
 #include "sa_kernels.h"
 #include "sa_lcp.h"
 #include "sa_onesweep.h"
@@ -390,6 +391,8 @@ static int radix_sort(sa_context* c, const Src& first, uint64_t first_bytes, con
     return SA_OK;
 }
 
+#include "sa_round1.h"
+
 static void record_round(sa_stats* st, float ms, uint64_t D, uint32_t P, uint64_t sorted_n, uint64_t h) {
     if (!st) return;
     const int r = st->rounds;
@@ -579,35 +582,53 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
-    const uint32_t K = choose_chars(sigma, n, opts ? opts->init_chars : 0);
+    uint32_t K = choose_chars(sigma, n, opts ? opts->init_chars : 0);
     const uint64_t base = (uint64_t)sigma + 1;
-    const uint32_t bits1 = key_bits(base, K);
+    const Chunking ch = plan_chunks(n);
+    uint64_t* keys1 = nullptr;
+    uint32_t P = 0;
+
+    // round 1: sort every suffix by its first K symbols -- bucketed (two
+    // global passes + per-window LDS sort) when the text allows it, else the
+    // LSD sort of the packed key
+    BucketPlan bp;
+    bool bucketed = plan_bucketed(sigma, n, K, opts ? opts->round1 : SA_ROUND1_AUTO, c->radix, &bp);
+    if (bucketed) {
+        bool done = false;
+        rc = round1_bucketed(c, d_text, n, d_sa, bp, s, tm, st, &done);
+        if (rc) return rc;
+        bucketed = done;
+        if (done) {
+            keys1 = c->keys[0];
+            P = 2;
+            K = bp.K;
+        }
+    }
+    if (!bucketed) {
+        const uint32_t bits1 = key_bits(base, K);
+        SA_TRACE("packed: sigma=%u K=%u bits=%u", sigma, K, bits1);
+        uint64_t top = 1;   // B^(K-1)
+        for (uint32_t t = 1; t < K; ++t) top *= base;
+        if (c->radix == 0) {
+            rc = onesweep_prepare(c, s);
+            if (rc) return rc;
+        }
+        tm.begin(SA_K_PACK);
+        hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
+                           base, top, K, c->keys[1], c->hist, c->radix == 0 ? (bits1 + 7) / 8 : 0u, os_ghist(c));
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_PACK, 9 * n);
+        SrcKeysIota src{c->keys[1]};
+        rc = radix_sort(c, src, 8 * n, ch, bits1, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &keys1, &P,
+                        true);
+        if (rc) return rc;
+    }
     if (st) {
         st->init_chars = (int32_t)K;
         st->sigma = (int32_t)sigma;
+        st->round1 = bucketed ? SA_ROUND1_BUCKETED : SA_ROUND1_LSD;
     }
-    SA_TRACE("packed: sigma=%u K=%u bits=%u", sigma, K, bits1);
-
-    // round 1: sort the packed K-prefix of every suffix
-    const Chunking ch = plan_chunks(n);
-    uint64_t top = 1;   // B^(K-1)
-    for (uint32_t t = 1; t < K; ++t) top *= base;
-    if (c->radix == 0) {
-        rc = onesweep_prepare(c, s);
-        if (rc) return rc;
-    }
-    tm.begin(SA_K_PACK);
-    hipLaunchKernelGGL(k_pack_text, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
-                       base, top, K, c->keys[1], c->hist, c->radix == 0 ? (bits1 + 7) / 8 : 0u, os_ghist(c));
-    tm.end();
-    SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_PACK, 9 * n);
-    SrcKeysIota src{c->keys[1]};
-    uint64_t* keys1;
-    uint32_t P;
-    rc = radix_sort(c, src, 8 * n, ch, bits1, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &keys1, &P,
-                    true);
-    if (rc) return rc;
     uint64_t D, m, G;
     int uo = 0;
     bool sparse = false;
@@ -616,7 +637,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // later rounds sort in the two buffers that do not hold the round-1 keys
     uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
     uint64_t* ukb1 = c->keys_u;
-    const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K};
+    const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K,
+                        bucketed ? 1u : 0u, bp.bs};
     if (st) st->sparse_ranks = sparse ? 1 : 0;
     SA_HIP(hipEventRecord(ev.e[1], s));
     SA_HIP(hipEventSynchronize(ev.e[1]));

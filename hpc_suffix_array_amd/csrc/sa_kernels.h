@@ -82,6 +82,41 @@ struct SrcText {
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
 };
 
+// Key layout of the bucketed first round (sa_bucket.h): key1 = D << rb | low
+// with D the dense s-symbol prefix and low the dense next R symbols times
+// (R + 1) plus the number of them before the end (or L - 1 for a suffix of
+// length L < s).
+struct BucketSpec {
+    uint64_t pow_s1;   // sigma^(s-1)
+    uint64_t powR1;    // sigma^(R-1)
+    uint64_t cmul;     // floor(2^48 / sigma^s): bucket = (D * cmul) >> 32
+    uint32_t sigma, s, R, rb;
+};
+
+// key1 of position i, computed from the text (rank look-ups of later rounds)
+__device__ __forceinline__ uint64_t key1_at(const uint8_t* __restrict__ text, const uint16_t* __restrict__ code,
+                                            uint64_t n, const BucketSpec& b, uint64_t i) {
+    uint64_t D = 0;
+    for (uint32_t t = 0; t < b.s; ++t) {
+        const uint32_t c = (i + t < n) ? code[text[i + t]] : 0u;
+        D = D * b.sigma + (c ? c - 1u : 0u);
+    }
+    const uint64_t L = n - i;
+    uint64_t low;
+    if (L < b.s) {
+        low = L - 1;
+    } else {
+        uint64_t r = 0;
+        for (uint32_t t = 0; t < b.R; ++t) {
+            const uint32_t c = (i + b.s + t < n) ? code[text[i + b.s + t]] : 0u;
+            r = r * b.sigma + (c ? c - 1u : 0u);
+        }
+        const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+        low = b.s + r * (b.R + 1) + tl;
+    }
+    return (D << b.rb) | low;
+}
+
 // Packed schedule, later rounds: only the suffixes whose group is not yet a
 // singleton (compacted in SA order: idx, dense group id g).  key =
 // (g << wr) | rank[idx + h]; rank is the group-head position + 1 (0 = past
@@ -101,10 +136,15 @@ struct RankLookup {
     uint64_t n;
     uint64_t base;
     uint32_t K;
+    uint32_t bucketed;                     // 1: keys1 holds key1 (BucketSpec layout)
+    BucketSpec bs;
     __device__ __forceinline__ uint32_t sparse(uint64_t j) const {
         if ((member[j >> 5] >> (j & 31)) & 1u) return rank[j];
         uint64_t x = 0;
-        for (uint32_t t = 0; t < K; ++t) x = x * base + ((j + t < n) ? code[text[j + t]] : 0u);
+        if (bucketed)
+            x = key1_at(text, code, n, bs, j);
+        else
+            for (uint32_t t = 0; t < K; ++t) x = x * base + ((j + t < n) ? code[text[j + t]] : 0u);
         uint64_t lo = 0, len = n;      // lower_bound(keys1, x)
         while (len > 0) {
             const uint64_t half = len >> 1;
@@ -149,6 +189,19 @@ struct SrcKeysIota {
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
 };
+
+// Radix digit of a key, bits [shift, shift + nbits): a source may define
+// digit() (the bucketed first round sorts by a function of the key, see
+// sa_bucket.h); otherwise the digit is the key's own bits.
+template <class S>
+__device__ __forceinline__ auto src_digit(const S& s, uint64_t k, uint32_t shift, uint32_t mask, int)
+    -> decltype(s.digit(k, shift, mask)) {
+    return s.digit(k, shift, mask);
+}
+template <class S>
+__device__ __forceinline__ uint32_t src_digit(const S&, uint64_t k, uint32_t shift, uint32_t mask, long) {
+    return (uint32_t)(k >> shift) & mask;
+}
 
 struct Chunking {
     uint64_t n;

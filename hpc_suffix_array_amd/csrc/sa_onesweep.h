@@ -117,7 +117,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         const bool ok = le < valid;
         k[j] = ok ? src.key(tb + le) : 0ull;
         v[j] = ok ? src.val(tb + le) : 0u;
-        d[j] = ok ? (uint32_t)(k[j] >> shift) & mask : kRadix;
+        d[j] = ok ? src_digit(src, k[j], shift, mask, 0) : kRadix;
     }
     uint32_t r[ITEMS];
     uint16_t* wc = s_wcnt[wave];
@@ -243,7 +243,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         const uint32_t q = j * BLOCK + threadIdx.x;
         if (q < valid) {
             const uint64_t key = s_keys[q];
-            const uint32_t dd = (uint32_t)(key >> shift) & mask;
+            const uint32_t dd = src_digit(src, key, shift, mask, 0);
             const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
             if (g < n) {
                 out_keys[g] = key;

@@ -1,0 +1,132 @@
+// sa_round1.h -- host side of the bucketed first round (kernels: sa_bucket.h).
+// Included by sa_build.hip inside namespace sa, after the radix helpers.
+//
+// plan_bucketed() decides whether the text's alphabet and size allow the
+// key1 layout; round1_bucketed() runs pack -> 2 bucket passes -> window
+// starts -> local sort and leaves the sorted key1 in keys[0] and the SA in
+// d_sa.  When a window exceeds the LDS tile (skewed text: a long run, a short
+// period) or its key span is too wide, it reports !done and the caller runs
+// the full LSD sort of the packed K-symbol key instead.
+#pragma once
+
+struct BucketPlan {
+    BucketSpec bs{};
+    uint32_t ib = 0;   // bit width of n - 1 (index bits packed under the key in the local sort)
+    uint32_t K = 0;    // s + R: symbols the first round sorts by
+};
+
+// round1: SA_ROUND1_AUTO / SA_ROUND1_LSD / SA_ROUND1_BUCKETED (sa_opts.round1)
+static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p) {
+    if (round1 == SA_ROUND1_LSD || radix != 0 || sigma < 2 || n < 2) return false;
+    if (round1 == SA_ROUND1_AUTO && n < kBucketMinN) return false;
+    uint64_t ps = 1;   // sigma^s >= 2^16: the 16-bit bucket is dense
+    uint32_t s = 0;
+    while (ps < 65536) {
+        ps *= sigma;
+        ++s;
+    }
+    if (K <= s || K > (uint32_t)kMaxK) return false;
+    const uint32_t ib = bit_width(n - 1);
+    const uint32_t bd = bit_width(ps - 1);
+    // D values per bucket, +1 bit for a window holding two buckets
+    const uint32_t span = bit_width((ps + 65535) / 65536) + 1;
+    for (uint32_t R = K - s; R >= 1; --R) {
+        unsigned __int128 pr = 1;   // sigma^R
+        for (uint32_t t = 0; t < R; ++t) pr *= sigma;
+        unsigned __int128 lowmax = s + (pr - 1) * (R + 1) + R;
+        uint32_t rb = 0;
+        while (lowmax) {
+            ++rb;
+            lowmax >>= 1;
+        }
+        if (bd + rb > 64 || rb + span + ib > 64) continue;
+        p->bs.pow_s1 = ps / sigma;
+        p->bs.powR1 = (uint64_t)(pr / sigma);
+        p->bs.cmul = (1ull << 48) / ps;
+        p->bs.sigma = sigma;
+        p->bs.s = s;
+        p->bs.R = R;
+        p->bs.rb = rb;
+        p->ib = ib;
+        p->K = s + R;
+        return true;
+    }
+    return false;
+}
+
+static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
+                           hipStream_t s, Timer& tm, sa_stats* st, bool* done) {
+    *done = false;
+    const Chunking ch = plan_chunks(n);
+    int rc = onesweep_prepare(c, s);
+    if (rc) return rc;
+    // [5] largest window, [6] local-sort flags, [7] windows, [10] skewed windows
+    SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
+    tm.begin(SA_K_PACK);
+    hipLaunchKernelGGL(k_pack_bucket, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
+                       bp.bs, c->keys[1], os_ghist(c));
+    tm.end();
+    add_bytes(st, SA_K_PACK, 9 * n);
+    tm.begin(SA_K_SCAN);
+    hipLaunchKernelGGL(k_digit_base, dim3(2), dim3(kBlock), 0, s, (const uint32_t*)os_ghist(c), os_base(c));
+    tm.end();
+    // two stable passes over the bucket's bytes: text order -> bucket order
+    tm.begin(SA_K_SCATTER_FIRST);
+    onesweep_pass(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.cmul}, n, 0, 8, os_base(c), os_tickets(c), c->keys[0],
+                  c->vals_alt, s);
+    tm.end();
+    add_bytes(st, SA_K_SCATTER_FIRST, 20 * n);
+    tm.begin(SA_K_SCATTER_KEYS);
+    onesweep_pass(c, SrcBucketKeys{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.cmul}, n, 8, 8, os_base(c) + kRadix,
+                  os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+    tm.end();
+    add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);
+    SA_HIP(hipGetLastError());
+    // windows of whole buckets; ws lives in vals_alt (free again; nw + 1 <= n)
+    const uint64_t nw = (n + kWinStride - 1) / kWinStride;
+    uint32_t* ws = c->vals_alt;
+    uint32_t* list = c->vals_alt + nw + 1;   // non-empty windows (2 nw + 1 <= n)
+    tm.begin(SA_K_WINDOWS);
+    {
+        const uint32_t g1 = (uint32_t)std::min<uint64_t>((nw + kBlock) / kBlock, 8192);
+        hipLaunchKernelGGL(k_window_starts, dim3(g1), dim3(kBlock), 0, s, (const uint64_t*)c->keys_u, n, nw, bp.bs.rb,
+                           bp.bs.cmul, ws);
+        const uint32_t g2 = (uint32_t)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024);
+        hipLaunchKernelGGL(k_window_list, dim3(g2), dim3(kBlock), 0, s, (const uint32_t*)ws, nw, list, c->words);
+    }
+    tm.end();
+    add_bytes(st, SA_K_WINDOWS, 8 * nw);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 32, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
+    if (st) st->largest_window = (int32_t)std::min<uint32_t>(c->host_words[5], INT32_MAX);
+    if (c->host_words[5] > (uint32_t)kBsCap) {
+        SA_TRACE("  bucketed round 1: window of %u > %d suffixes, full sort instead", c->host_words[5], kBsCap);
+        return SA_OK;
+    }
+    tm.begin(SA_K_LOCAL_SORT);
+    {
+        uint32_t* skew = list + nw;   // windows with clustered keys (3 nw + 1 <= capacity)
+        const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
+        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
+                           (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
+                           (const uint32_t*)list, c->words, bp.ib, c->keys[0], d_sa, skew);
+        hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
+                           (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
+                           (const uint32_t*)skew, c->words, bp.ib, c->keys[0], d_sa);
+    }
+    tm.end();
+    add_bytes(st, SA_K_LOCAL_SORT, 24 * n);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(c->host_words + 6, c->words + 6, 20, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    if (c->host_words[6]) {
+        SA_TRACE("  bucketed round 1: local sort flags %u, full sort instead", c->host_words[6]);
+        return SA_OK;
+    }
+    SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R, bp.bs.rb,
+             c->host_words[7], c->host_words[10], c->host_words[5]);
+    *done = true;
+    return SA_OK;
+}

@@ -49,8 +49,16 @@ enum sa_kernel_kind {
     SA_K_ALPHABET = 12,      /* byte histogram of the text */
     SA_K_PACK = 13,          /* packed K-symbol keys + first digit histogram */
     SA_K_SORT_U = 14,        /* every pass of an unsorted-set (later round) sort */
-    SA_K_COUNT = 15
+    SA_K_WINDOWS = 15,       /* bucketed round 1: window starts over the bucket-sorted keys */
+    SA_K_LOCAL_SORT = 16,    /* bucketed round 1: per-window LDS sort */
+    SA_K_COUNT = 17
 };
+
+/* first round of the packed schedule */
+#define SA_ROUND1_AUTO 0      /* bucketed when n >= 2^20 and it fits, else LSD */
+#define SA_ROUND1_LSD 1       /* LSD radix sort of the packed K-symbol key */
+#define SA_ROUND1_BUCKETED 2  /* two bucket passes + per-window LDS sort (falls
+                                 back to LSD when a window exceeds the LDS tile) */
 
 /* doubling schedules */
 #define SA_SCHEDULE_PACKED 0     /* default: first round sorts a packed K-symbol
@@ -66,7 +74,8 @@ typedef struct {
     int32_t init_chars;     /* packed schedule: symbols in the first key, 0 = auto */
     int32_t radix;          /* 0: single-pass radix (decoupled look-back, default);
                                1: reduce-then-scan radix (3 kernels per pass) */
-    int32_t reserved[4];
+    int32_t round1;         /* SA_ROUND1_* (packed schedule, onesweep radix) */
+    int32_t reserved[3];
 } sa_opts;
 
 typedef struct {
@@ -83,6 +92,8 @@ typedef struct {
     int32_t init_chars;                  /* K of the packed schedule */
     int32_t sigma;                       /* distinct symbols in the text */
     int32_t sparse_ranks;                /* 1: round-1 ranks kept for unsorted suffixes only */
+    int32_t round1;                      /* SA_ROUND1_LSD or SA_ROUND1_BUCKETED: first round taken */
+    int32_t largest_window;              /* bucketed round 1: largest window (suffixes) */
     uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
     double kern_ms[SA_K_COUNT];          /* profile only */
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */

@@ -27,6 +27,9 @@ KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist
          ("k_scatter<sa::SrcKeysIota>", "scatter_iota"), ("k_pack_text", "pack"),
          ("k_scatter<sa::SrcKeys>", "scatter_keys_rs"),
          ("k_onesweep<sa::SrcKeysIota", "scatter_iota"), ("k_onesweep<sa::SrcKeys,", "scatter_keys"),
+         ("k_onesweep<sa::SrcBucketIota", "scatter_first"), ("k_onesweep<sa::SrcBucketKeys", "scatter_keys"),
+         ("k_pack_bucket", "pack"), ("k_window_starts", "windows"), ("k_window_max", "windows"),
+         ("k_bucket_sort", "local_sort"),
          ("k_onesweep<sa::SrcU", "scatter_u"), ("k_onesweep<sa::SrcRank", "scatter_rank"),
          ("k_global_hist", "global_hist"), ("k_digit_base", "digit_base"), ("k_alphabet", "alphabet"),
          ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
@@ -116,7 +119,9 @@ def main():
         "read_calibration": {"kernel": "seg_count (full-n launch)", "known_read_bytes": 8 * n,
                              "factor": read_factor},
         "kernels": kernels,
-        "traffic_bytes_per_launch": {"scatter_keys": kernels.get("scatter_keys", {}).get("traffic_bytes_corrected")},
+        # per full-size launch, keyed like bench.py's kernel kinds
+        "traffic_bytes_per_launch": {k: v["traffic_bytes_corrected"] for k, v in kernels.items()
+                                     if v.get("traffic_bytes_corrected") is not None},
         "bench": bench,
     }
     here = os.path.dirname(os.path.abspath(__file__))

@@ -217,3 +217,60 @@ def test_distributed_hip_single_rank(gpu, oracle):
             assert (sa == oracle.sa_c(t).astype(np.int64)).all()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("kind", ["dna", "alnum", "ascii127", "byte256", "binary"])
+@pytest.mark.parametrize("n", [2, 3, 17, 4097, 65537, 1_000_003, 2_500_001])
+def test_bucketed_round1_vs_oracle(gpu, oracle, kind, n):
+    """First round as two bucket passes + per-window LDS sort (sa_bucket.h),
+    forced at every size: short texts (every suffix shorter than the bucket
+    prefix), many tiny windows, and 1-2.5 M suffixes (the auto threshold)."""
+    from hpc_suffix_array_amd import build_suffix_array
+    t = oracle.gen_text(kind, n, seed=7 * n + len(kind))
+    got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+    assert (got == oracle.sa_c(t)).all()
+    assert st["distinct"][-1] == n
+    if n >= 65537:
+        assert st["round1"] == "bucketed" and st["passes"][0] == 2, st
+
+
+@pytest.mark.parametrize("round1", ["lsd", "bucketed"])
+def test_round1_variants_agree(gpu, oracle, round1):
+    """Both first-round sorts give the same round-1 groups (D_1, unsorted
+    count) and the same SA, including the sparse-rank look-ups of later
+    rounds through the bucketed key layout."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for kind, n in (("dna", 3_000_017), ("alnum", 1_500_007), ("byte256", 1 << 21)):
+        t = oracle.gen_text(kind, n, seed=n)
+        got, st = build_suffix_array(t, return_stats=True, round1=round1)
+        ref, st_ref = build_suffix_array(t, return_stats=True, round1="lsd")
+        assert (got == ref).all() and (got == oracle.sa_c(t)).all(), (kind, round1)
+        assert st["round1"] == round1
+        assert st["distinct"] == st_ref["distinct"], (kind, st["distinct"], st_ref["distinct"])
+
+
+def test_bucketed_round1_fallback(gpu, oracle):
+    """Skewed texts overflow a window (one bucket > the LDS tile): the first
+    round falls back to the full LSD sort and the SA stays exact."""
+    from hpc_suffix_array_amd import build_suffix_array
+    n = 1 << 20
+    for t in (np.full(n, ord("a"), np.uint8),
+              np.tile(np.frombuffer(b"abaababa", np.uint8), n // 8),
+              np.concatenate([oracle.gen_text("dna", n // 2, seed=3), np.full(n // 2, ord("C"), np.uint8)])):
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        assert st["round1"] == "lsd"
+        if len(np.unique(t)) > 1:   # one symbol: no bucketing at all (sigma < 2)
+            assert st["largest_window"] > 18432, st["largest_window"]
+        assert (got == oracle.sa_c(t)).all()
+
+
+def test_bucketed_round1_known_answers(gpu, oracle, golden):
+    """The default (auto) path at 1 MiB and 64 MiB takes the bucketed first
+    round; SHA-256 known answers of SURVEY.md 8(c)."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for key in ("alnum_1MiB", "ascii127_1MiB", "dna_1MiB", "byte256_1MiB", "dna_64MiB"):
+        k = golden["known"][key]
+        t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
+        got, st = build_suffix_array(t, return_stats=True)
+        assert st["round1"] == "bucketed", key
+        assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"], key

@@ -1,0 +1,71 @@
+"""CPU check of the bucketed first round's key layout (sa_bucket.h, the
+BucketSpec/key1_at of sa_kernels.h), restated in Python: key1 must order
+suffixes exactly as their first K = s + R symbols with the end of the text
+smallest (manber_myers.c:91,122 sentinel), give equal keys exactly to equal
+K-prefixes, and its 16-bit bucket must be monotone in key1.  Both fields
+are dense (digits code - 1, the end clamped onto the smallest symbol's
+digit), and the count of symbols before the end separates the suffixes that
+the clamp merges.  Small alphabets
+and small s make every corner (suffixes shorter than s, shorter than K)
+common."""
+import itertools
+import random
+
+import pytest
+
+
+def key1(text, i, sigma, s, R, code):
+    n = len(text)
+    D = 0
+    for t in range(s):
+        c = code[text[i + t]] if i + t < n else 0
+        D = D * sigma + (c - 1 if c else 0)
+    L = n - i
+    if L < s:
+        low = L - 1
+    else:
+        r = 0
+        for t in range(R):
+            c = code[text[i + s + t]] if i + s + t < n else 0
+            r = r * sigma + (c - 1 if c else 0)
+        low = s + r * (R + 1) + min(R, L - s)
+    rb = (s + (sigma ** R - 1) * (R + 1) + R).bit_length()
+    return (D << rb) | low, rb
+
+
+def prefix(text, i, K):
+    # K-prefix with the end smallest: symbols shifted by one, 0 past the end
+    return tuple((text[i + t] + 1) if i + t < len(text) else 0 for t in range(K))
+
+
+@pytest.mark.parametrize("sigma,s,R", [(2, 3, 2), (2, 1, 4), (3, 2, 2), (4, 3, 1), (5, 2, 3), (2, 2, 5)])
+def test_key1_orders_like_k_prefix(sigma, s, R):
+    rng = random.Random(sigma * 100 + s * 10 + R)
+    code = {b: b + 1 for b in range(sigma)}   # dense codes 1..sigma
+    K = s + R
+    for _ in range(60):
+        n = rng.randint(1, 14)
+        text = [rng.randrange(sigma) for _ in range(n)]
+        if rng.random() < 0.3:
+            text = [0] * n   # runs of the smallest symbol collide with shorter suffixes under the clamp
+        keys = [key1(text, i, sigma, s, R, code)[0] for i in range(n)]
+        pre = [prefix(text, i, K) for i in range(n)]
+        for a, b in itertools.combinations(range(n), 2):
+            assert (keys[a] < keys[b]) == (pre[a] < pre[b]), (text, a, b)
+            assert (keys[a] == keys[b]) == (pre[a] == pre[b]), (text, a, b)
+
+
+def test_bucket_monotone():
+    # bucket = (D * cmul) >> 32 with cmul = floor(2^48 / sigma^s) < 2^16
+    for sigma in (2, 3, 4, 62, 127, 256):
+        ps, s = 1, 0
+        while ps < 65536:
+            ps *= sigma
+            s += 1
+        cmul = (1 << 48) // ps
+        prev = -1
+        for D in list(range(0, min(ps, 5000))) + list(range(max(0, ps - 5000), ps)):
+            b = (D * cmul) >> 32
+            assert 0 <= b < 65536 and b >= prev
+            prev = b
+        assert (((ps - 1) * cmul) >> 32) > 65000   # the 16 bits are used
