@@ -25,14 +25,19 @@ using namespace sa;
         }                                                                                     \
     } while (0)
 
-// key = bucket << rb | random rb bits, bucket = (i << 16) / n; rb = 28
-__global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb) {
+// key = bucket << rb | random rbits bits, bucket = (i << 16) / n (rb = 28;
+// fewer random bits make equal keys: unsorted groups for the segments)
+__global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb, uint32_t rbits) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         z ^= z >> 31;
-        keys[i] = ((i << 16) / n << rb) | (z & ((1ull << rb) - 1));
+        if (rbits == 0) {   // DNA-like: low = 20 + 13 E, E uniform in [0, 4^12) (s = 8, R = 12)
+            keys[i] = ((i << 16) / n << rb) | (20 + 13 * (z % (1ull << 24)));
+        } else {
+            keys[i] = ((i << 16) / n << rb) | ((z & ((1ull << rbits) - 1)) << (rb - rbits));
+        }
         vals[i] = (uint32_t)(z >> 32);
     }
 }
@@ -48,6 +53,7 @@ __global__ void k_copy12(const uint64_t* __restrict__ a, const uint32_t* __restr
 int main(int argc, char** argv) {
     const int lg = argc > 1 ? std::atoi(argv[1]) : 30;
     const int reps = argc > 2 ? std::atoi(argv[2]) : 3;
+    const uint32_t rbits = argc > 3 ? (uint32_t)std::atoi(argv[3]) : 28;
     const uint64_t n = 1ull << lg;
     const uint32_t rb = 28, ib = lg;
     uint64_t *keys, *okeys;
@@ -61,7 +67,15 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&words, 64));
     uint32_t* list = ws + nw + 1;
     uint32_t* skew = list + nw;
-    hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, n, rb);
+    hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, n, rb, rbits);
+    // segments outputs (as round1_bucketed lays them out)
+    uint32_t *rank, *member, *tmp;
+    CK(hipMalloc(&rank, n * 4));
+    CK(hipMalloc(&member, n / 8 + 64));
+    CK(hipMalloc(&tmp, n * 12));
+    uint32_t* cnt;
+    CK(hipMalloc(&cnt, (2 * nw + 2) * 4));
+    const SegOut so{rank, member, tmp, tmp + n, tmp + 2 * n, cnt, cnt + nw + 1};
     CK(hipMemset(words, 0, 64));
     const uint64_t cmul = 1ull << 32;   // bucket = D (16 bits)
     hipLaunchKernelGGL(k_window_starts, dim3((uint32_t)std::min<uint64_t>((nw + 256) / 256, 8192)), dim3(256), 0, 0,
@@ -71,7 +85,7 @@ int main(int argc, char** argv) {
     CK(hipDeviceSynchronize());
     uint32_t hw[16];
     CK(hipMemcpy(hw, words, 64, hipMemcpyDeviceToHost));
-    std::printf("n=2^%d windows=%u largest=%u\n", lg, hw[7], hw[5]);
+    std::printf("n=2^%d random key bits=%u windows=%u largest=%u\n", lg, rbits, hw[7], hw[5]);
     hipEvent_t e0, e1;
     CK(hipEventCreate(&e0));
     CK(hipEventCreate(&e1));
@@ -93,27 +107,33 @@ int main(int argc, char** argv) {
     timeit("copy 12 B in + out", [&] {
         hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
     });
-    for (uint32_t g : {256u, 512u, 1024u}) {
+    for (uint32_t g : {256u}) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
         timeit(nm, [&] {
             hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
-                               words, ib, okeys, ovals, skew);
+                               words, ib, okeys, ovals, skew, SegOut{});
+        });
+        std::snprintf(nm, sizeof nm, "bucket_sort + segments grid %u", g);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               words, ib, okeys, ovals, skew, so);
         });
         std::snprintf(nm, sizeof nm, "bucket_sort no-sort grid %u", g);
         timeit(nm, [&] {
             hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 1>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
-                               words, ib, okeys, ovals, skew);
+                               words, ib, okeys, ovals, skew, SegOut{});
         });
     }
     CK(hipMemcpy(hw, words, 64, hipMemcpyDeviceToHost));
-    std::printf("flags=%u skewed=%u\n", hw[6], hw[10]);
+    std::printf("flags=%u skewed=%u heads=%u unsorted=%u groups=%u (accumulated over runs)\n", hw[6], hw[10], hw[0], hw[1], hw[2]);
     // check: output sorted within each window, keys monotone overall
     std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
     hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(256), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
-                       (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew);
+                       (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
     CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (size_t i = 1; i < h.size(); ++i) bad += h[i] < h[i - 1];

@@ -249,8 +249,7 @@ __global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restri
 //   1. counting scatter on the top kSubBits of the key span: LDS histogram
 //      (16-bit counters packed in pairs, atomics), scan, atomic cursors ->
 //      s_w holds 2^kSubBits sub-buckets of a few suffixes each (random text);
-//   2. each suffix counts the smaller keys of its sub-bucket (its rank in
-//      it), then all move to their final slots;
+//   2. each thread insertion-sorts its four sub-buckets in LDS;
 //   3. s_w is written out in order: sorted key1 and SA, coalesced.
 // A window with a sub-bucket above kMaxSub (many equal or clustered keys) is
 // appended to `skew` (count in words[10]) and left to k_bucket_sort_lsd.
@@ -273,18 +272,18 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ keys_in
     uint32_t v[ITEMS];
     uint64_t mx = 0;
     mn = ~0ull;
+    // unpredicated loads (slots past m re-read the last suffix: no per-item
+    // exec masks, which cost SGPRs and spills at 128 VGPRs); later phases
+    // skip those slots by le < m
+    const uint32_t l0 = wave * WT + lane;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
-        const uint32_t le = wave * WT + i * kWave + lane;
-        if (le < m) {
-            w[i] = keys_in[a + le];
-            v[i] = vals_in[a + le];
-            mn = w[i] < mn ? w[i] : mn;
-            mx = w[i] > mx ? w[i] : mx;
-        } else {
-            w[i] = 0;
-            v[i] = 0;
-        }
+        const uint32_t le = l0 + i * kWave;
+        const uint64_t e = a + (le < m ? le : m - 1);
+        w[i] = keys_in[e];
+        v[i] = vals_in[e];
+        mn = w[i] < mn ? w[i] : mn;
+        mx = w[i] > mx ? w[i] : mx;
     }
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
@@ -319,13 +318,225 @@ __device__ __forceinline__ void store_window(const uint64_t* __restrict__ s_w, u
     constexpr int WT = kWave * ITEMS;
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
-#pragma unroll
+#pragma unroll 2
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t le = wave * WT + i * kWave + lane;
         if (le < m) {
             const uint64_t x = s_w[le];
             keys_out[a + le] = (x >> ib) + mn;
             sa_out[a + le] = (uint32_t)(x & imask);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Round-1 segments of a sorted window (replaces k_seg_count + k_seg_write of
+// the LSD first round, which re-read every sorted key twice): a window holds
+// whole groups, so its heads (key differs from the previous: the re-rank of
+// manber_myers.c:101-110), singletons and unsorted members (U) are found in
+// LDS.  For every U member x at SA position p: rank[x] = (its group's head
+// position) + 1, its member bit, and (p, x, local U-group id) at its
+// window-local U index in tmp; cnt_u[j] / cnt_g[j] = the window's U members
+// and U groups (scanned and gathered in SA order by k_scan_windows +
+// k_u_gather).  Returns (heads, U, U groups) to thread 0.
+// s_pre: WAVES * ITEMS u64 of scratch LDS (per-row running values).
+// ---------------------------------------------------------------------------
+struct SegOut {
+    uint32_t* rank;
+    uint32_t* member;
+    uint32_t* tmp_pos;
+    uint32_t* tmp_idx;
+    uint32_t* tmp_g;
+    uint32_t* cnt_u;
+    uint32_t* cnt_g;
+};
+
+template <int BLOCK, int ITEMS>
+__device__ __forceinline__ void window_segments(const uint64_t* __restrict__ s_w, uint64_t* __restrict__ s_pre,
+                                                uint64_t (*s_red)[BLOCK / kWave], uint64_t a, uint32_t m, uint32_t ib,
+                                                uint32_t j, const SegOut& so, uint64_t& tot_h, uint64_t& tot_u,
+                                                uint64_t& tot_g) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int WT = kWave * ITEMS;
+    const uint32_t wave = wave_id(), lane = lane_id();
+    // head / unsorted / unsorted-head masks of row rb0 (s = rb0 + lane)
+    auto masks = [&](uint32_t rb0, uint64_t& mh, uint64_t& mu, uint64_t& muh) {
+        const uint32_t le = rb0 + lane;
+        const bool ok = le < m;
+        const uint64_t cur = ok ? s_w[le] >> ib : 0ull;
+        const bool head = ok && (le == 0 || (s_w[le - 1] >> ib) != cur);
+        const bool nhead = ok && (le + 1 == m || (s_w[le + 1] >> ib) != cur);
+        const bool in_u = ok && !(head && nhead);
+        mh = __ballot(head);
+        mu = __ballot(in_u);
+        muh = __ballot(head && in_u);
+    };
+    // 1. per row: the wave's running (last head, U, U heads) before it; per
+    // wave: which rows hold U members, and the totals
+    int32_t last_h = -1;
+    uint32_t nh = 0, nu = 0, ng = 0;
+    uint32_t urows = 0;
+#pragma unroll 1
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t rb0 = wave * WT + i * kWave;
+        if (rb0 >= m) break;   // uniform per wave
+        uint64_t mh, mu, muh;
+        masks(rb0, mh, mu, muh);
+        if (lane == 0) s_pre[wave * ITEMS + i] = (uint64_t)(uint32_t)last_h | ((uint64_t)nu << 32) | ((uint64_t)ng << 48);
+        if (mu) urows |= 1u << i;
+        if (mh) last_h = (int32_t)(rb0 + 63 - __clzll(mh));
+        nh += __popcll(mh);
+        nu += __popcll(mu);
+        ng += __popcll(muh);
+    }
+    if (lane == 0) {
+        s_red[0][wave] = (uint64_t)(uint32_t)last_h | ((uint64_t)nh << 32);
+        s_red[1][wave] = (uint64_t)nu | ((uint64_t)ng << 32);
+    }
+    __syncthreads();
+    // 2. carries from the earlier waves, then only the rows holding U members
+    int32_t cw = -1;
+    uint32_t bu = 0, bg = 0, th = 0, tu = 0, tg = 0;
+#pragma unroll
+    for (int x = 0; x < WAVES; ++x) {
+        const uint64_t v0 = s_red[0][x], v1 = s_red[1][x];
+        if (x < (int)wave) {
+            if ((int32_t)(uint32_t)v0 >= 0) cw = (int32_t)(uint32_t)v0;
+            bu += (uint32_t)v1;
+            bg += (uint32_t)(v1 >> 32);
+        }
+        th += (uint32_t)(v0 >> 32);
+        tu += (uint32_t)v1;
+        tg += (uint32_t)(v1 >> 32);
+    }
+    if (threadIdx.x == 0) {
+        so.cnt_u[j] = tu;
+        so.cnt_g[j] = tg;
+        tot_h += th;
+        tot_u += tu;
+        tot_g += tg;
+    }
+    const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
+    const uint64_t lt = lanemask_lt(), lem = lt | (1ull << lane);
+    while (urows) {   // uniform per wave
+        const uint32_t i = (uint32_t)__builtin_ctz(urows);
+        urows &= urows - 1;
+        const uint32_t rb0 = wave * WT + i * kWave;
+        uint64_t mh, mu, muh;
+        masks(rb0, mh, mu, muh);
+        const uint64_t pre = s_pre[wave * ITEMS + i];
+        const int32_t ph = (int32_t)(uint32_t)pre;
+        const int32_t ch = ph >= 0 ? ph : cw;
+        if ((mu >> lane) & 1ull) {
+            const uint64_t hl = mh & lem;
+            const uint32_t hpos = hl ? rb0 + 63 - (uint32_t)__clzll(hl) : (uint32_t)ch;
+            const uint32_t ku = bu + (uint32_t)((pre >> 32) & 0xFFFFu) + (uint32_t)__popcll(mu & lt);
+            const uint32_t kg = bg + (uint32_t)(pre >> 48) + (uint32_t)__popcll(muh & lem) - 1u;
+            const uint32_t x = (uint32_t)(s_w[rb0 + lane] & imask);
+            so.rank[x] = (uint32_t)(a + hpos) + 1u;
+            atomicOr(&so.member[x >> 5], 1u << (x & 31));
+            so.tmp_pos[a + ku] = (uint32_t)(a + rb0 + lane);
+            so.tmp_idx[a + ku] = x;
+            so.tmp_g[a + ku] = kg;
+        }
+    }
+}
+
+// per-workgroup totals of window_segments -> words[0..2] (D, m, G)
+__device__ __forceinline__ void flush_totals(uint32_t* __restrict__ words, uint64_t th, uint64_t tu, uint64_t tg) {
+    if (threadIdx.x == 0) {
+        if (th) atomicAdd(&words[0], (uint32_t)th);
+        if (tu) atomicAdd(&words[1], (uint32_t)tu);
+        if (tg) atomicAdd(&words[2], (uint32_t)tg);
+    }
+}
+
+// Exclusive scan in place of cnt_u[0..nw] and cnt_g[0..nw] (entry nw enters
+// as 0 and leaves as the total), in blocks of kWsBlock entries:
+// k_wscan_reduce (block sums) -> k_wscan_top (their scan, one workgroup) ->
+// k_wscan_apply (each block rescanned from its offset).
+constexpr int kWsPer = 8;
+constexpr int kWsBlock = kBlock * kWsPer;   // 2048 entries per workgroup
+
+__device__ __forceinline__ void wscan_load(const uint32_t* __restrict__ c, uint64_t nw, uint64_t b0, uint32_t (&x)[kWsPer],
+                                           uint32_t& sum) {
+    sum = 0;
+#pragma unroll
+    for (int k = 0; k < kWsPer; ++k) {
+        const uint64_t i = b0 + threadIdx.x * kWsPer + k;
+        x[k] = i <= nw ? c[i] : 0u;
+        sum += x[k];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wscan_reduce(const uint32_t* __restrict__ cu, const uint32_t* __restrict__ cg,
+                                                         uint64_t nw, uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kWsBlock;
+    uint32_t x[kWsPer], su, sg, tu, tg;
+    wscan_load(cu, nw, b0, x, su);
+    wscan_load(cg, nw, b0, x, sg);
+    block_exclusive_sum(su, s_tmp, &tu);
+    block_exclusive_sum(sg, s_tmp, &tg);
+    if (threadIdx.x == 0) {
+        part[2 * blockIdx.x] = tu;
+        part[2 * blockIdx.x + 1] = tg;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wscan_top(uint32_t* __restrict__ part, uint32_t blocks) {
+    __shared__ uint32_t s_tmp[kWaves];
+    uint32_t carry_u = 0, carry_g = 0;
+    for (uint32_t b0 = 0; b0 < blocks; b0 += kBlock) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t u = b < blocks ? part[2 * b] : 0u, g = b < blocks ? part[2 * b + 1] : 0u;
+        uint32_t tu, tg;
+        const uint32_t eu = block_exclusive_sum(u, s_tmp, &tu) + carry_u;
+        const uint32_t eg = block_exclusive_sum(g, s_tmp, &tg) + carry_g;
+        if (b < blocks) {
+            part[2 * b] = eu;
+            part[2 * b + 1] = eg;
+        }
+        carry_u += tu;
+        carry_g += tg;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_wscan_apply(uint32_t* __restrict__ cu, uint32_t* __restrict__ cg, uint64_t nw,
+                                                        const uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kWsBlock;
+    for (int a = 0; a < 2; ++a) {
+        uint32_t* c = a ? cg : cu;
+        uint32_t x[kWsPer], sum;
+        wscan_load(c, nw, b0, x, sum);
+        uint32_t off = block_exclusive_sum(sum, s_tmp, nullptr) + part[2 * blockIdx.x + a];
+#pragma unroll
+        for (int k = 0; k < kWsPer; ++k) {
+            const uint64_t i = b0 + threadIdx.x * kWsPer + k;
+            if (i <= nw) c[i] = off;
+            off += x[k];
+        }
+    }
+}
+
+// each listed window's U members from tmp (window-local order) to their
+// compacted SA-order slots; one wave per window
+__global__ __launch_bounds__(kBlock) void k_u_gather(const uint32_t* __restrict__ list,
+                                                     const uint32_t* __restrict__ words,
+                                                     const uint32_t* __restrict__ ws, const uint32_t* __restrict__ ou,
+                                                     const uint32_t* __restrict__ og, SegOut so,
+                                                     uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
+                                                     uint32_t* __restrict__ u_g) {
+    const uint32_t nlist = words[7];
+    const uint32_t lane = lane_id();
+    for (uint64_t q = (uint64_t)blockIdx.x * kWaves + wave_id(); q < nlist; q += (uint64_t)gridDim.x * kWaves) {
+        const uint32_t j = list[q];
+        const uint32_t a = ws[j], o = ou[j], c = ou[j + 1] - o, g0 = og[j];
+        for (uint32_t k = lane; k < c; k += kWave) {
+            u_pos[o + k] = so.tmp_pos[a + k];
+            u_idx[o + k] = so.tmp_idx[a + k];
+            u_g[o + k] = so.tmp_g[a + k] + g0;
         }
     }
 }
@@ -338,7 +549,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
                                                        const uint32_t* __restrict__ ws,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
                                                        uint32_t ib, uint64_t* __restrict__ keys_out,
-                                                       uint32_t* __restrict__ sa_out, uint32_t* __restrict__ skew) {
+                                                       uint32_t* __restrict__ sa_out, uint32_t* __restrict__ skew,
+                                                       SegOut so) {
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     constexpr int WT = kWave * ITEMS;
@@ -353,6 +565,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
     uint32_t* err = words + 6;
     const uint32_t nlist = words[7];
     auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
+    static_assert(WAVES * ITEMS * 8 <= kSubBuckets * 2, "per-row segment values fit in s_cnt");
+    uint64_t th = 0, tu = 0, tg = 0;
     for (uint32_t q = blockIdx.x; q < nlist; q += gridDim.x) {
         const uint32_t j = list[q];
         const uint64_t a = ws[j];
@@ -432,29 +646,30 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
             }
         }
         __syncthreads();
-        // ... rank inside the sub-bucket by counting smaller keys ...
-        uint32_t pos[ITEMS];
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            pos[i] = 0;
-            if (wave * WT + i * kWave + lane < m) {
-                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
-                uint32_t r = lo;
-                for (uint32_t y = lo; y < hi; ++y) r += s_w[y] < w[i] ? 1u : 0u;
-                pos[i] = r;
+        // ... then each thread insertion-sorts four sub-buckets in place (a
+        // few suffixes each for random text; no per-item registers needed)
+#pragma unroll 1
+        for (uint32_t sb = dg; sb < (uint32_t)kSubBuckets; sb += BLOCK) {
+            const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
+            for (uint32_t k = lo + 1; k < hi; ++k) {
+                const uint64_t x = s_w[k];
+                uint32_t y = k;
+                while (y > lo && s_w[y - 1] > x) {
+                    s_w[y] = s_w[y - 1];
+                    --y;
+                }
+                s_w[y] = x;
             }
         }
         __syncthreads();
-        // ... and move to the final slot
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i)
-            if (wave * WT + i * kWave + lane < m) s_w[pos[i]] = w[i];
-        __syncthreads();
-        // 3. out, in order
+        // 3. the window's segments, then out in order (the stores go last: on
+        // gfx950 vmcnt counts stores too, so any later vmcnt wait in this
+        // window -- spill reloads included -- would drain them)
+        if (so.rank) window_segments<BLOCK, ITEMS>(s_w, reinterpret_cast<uint64_t*>(s_cnt), s_red, a, m, ib, j, so, th, tu, tg);
         store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
     }
+    flush_totals(words, th, tu, tg);
 }
 
 // The skewed windows: stable LSD passes of 8 bits over the key span, each an
@@ -467,7 +682,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
                                                            const uint32_t* __restrict__ skew,
                                                            uint32_t* __restrict__ words, uint32_t ib,
                                                            uint64_t* __restrict__ keys_out,
-                                                           uint32_t* __restrict__ sa_out) {
+                                                           uint32_t* __restrict__ sa_out, SegOut so) {
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     constexpr int WT = kWave * ITEMS;
@@ -483,6 +698,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
     const uint32_t dg = threadIdx.x;
     uint32_t* err = words + 6;
     const uint32_t nskew = words[10];
+    static_assert(WAVES * ITEMS * 8 <= WAVES * kRadix * 2, "per-row segment values fit in s_wcnt");
+    uint64_t th = 0, tu = 0, tg = 0;
     for (uint32_t q = blockIdx.x; q < nskew; q += gridDim.x) {
         const uint32_t j = skew[q];
         const uint64_t a = ws[j];
@@ -563,9 +780,13 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
             }
             __syncthreads();
         }
+        if (so.rank)
+            window_segments<BLOCK, ITEMS>(s_w, reinterpret_cast<uint64_t*>(&s_wcnt[0][0]), s_red, a, m, ib, j, so, th,
+                                          tu, tg);
         store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
         __syncthreads();
     }
+    flush_totals(words, th, tu, tg);
 }
 
 }  // namespace sa

@@ -593,9 +593,11 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // LSD sort of the packed key
     BucketPlan bp;
     bool bucketed = plan_bucketed(sigma, n, K, opts ? opts->round1 : SA_ROUND1_AUTO, c->radix, &bp);
+    bool fused = false;
+    uint64_t seg1[3] = {0, 0, 0};
     if (bucketed) {
         bool done = false;
-        rc = round1_bucketed(c, d_text, n, d_sa, bp, s, tm, st, &done);
+        rc = round1_bucketed(c, d_text, n, d_sa, bp, s, tm, st, &done, &fused, seg1);
         if (rc) return rc;
         bucketed = done;
         if (done) {
@@ -632,8 +634,15 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint64_t D, m, G;
     int uo = 0;
     bool sparse = false;
-    rc = segments(c, keys1, d_sa, ch, PosIdentity{}, true, &sparse, nullptr, uo, s, tm, st, &D, &m, &G);
-    if (rc) return rc;
+    if (bucketed && fused) {   // segments came with the local sort (sparse ranks)
+        D = seg1[0];
+        m = seg1[1];
+        G = seg1[2];
+        sparse = true;
+    } else {
+        rc = segments(c, keys1, d_sa, ch, PosIdentity{}, true, &sparse, nullptr, uo, s, tm, st, &D, &m, &G);
+        if (rc) return rc;
+    }
     // later rounds sort in the two buffers that do not hold the round-1 keys
     uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
     uint64_t* ukb1 = c->keys_u;

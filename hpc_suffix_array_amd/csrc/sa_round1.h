@@ -54,13 +54,21 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     return false;
 }
 
+// *done: the SA and keys[0] hold the sorted first round.  *fused: the
+// round-1 segments were produced with it (few unsorted suffixes): rank[] for
+// the unsorted set only (member bitmap), the unsorted set compacted in
+// u_pos/u_idx/u_g[0], and seg = {D, m, G}; otherwise the caller runs
+// segments() on keys[0].
 static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
-                           hipStream_t s, Timer& tm, sa_stats* st, bool* done) {
+                           hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused, uint64_t seg[3]) {
     *done = false;
+    *fused = false;
     const Chunking ch = plan_chunks(n);
     int rc = onesweep_prepare(c, s);
     if (rc) return rc;
-    // [5] largest window, [6] local-sort flags, [7] windows, [10] skewed windows
+    // [0..2] D, m, G of the fused segments, [5] largest window, [6] local-sort
+    // flags, [7] windows, [10] skewed windows
+    SA_HIP(hipMemsetAsync(c->words, 0, 12, s));
     SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
     tm.begin(SA_K_PACK);
     hipLaunchKernelGGL(k_pack_bucket, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
@@ -105,25 +113,54 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         SA_TRACE("  bucketed round 1: window of %u > %d suffixes, full sort instead", c->host_words[5], kBsCap);
         return SA_OK;
     }
+    // windows with clustered keys, then per-window U / U-group counts (scanned
+    // in place: nw + 1 each); 5 nw + 3 <= capacity
+    uint32_t* skew = list + nw;
+    uint32_t* cnt_u = skew + nw;
+    uint32_t* cnt_g = cnt_u + nw + 1;
+    SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
+    SA_HIP(hipMemsetAsync(c->member, 0, (n + 31) / 32 * 4, s));
+    const SegOut so{c->rank, c->member, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g};
     tm.begin(SA_K_LOCAL_SORT);
     {
-        uint32_t* skew = list + nw;   // windows with clustered keys (3 nw + 1 <= capacity)
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
-                           (const uint32_t*)list, c->words, bp.ib, c->keys[0], d_sa, skew);
+                           (const uint32_t*)list, c->words, bp.ib, c->keys[0], d_sa, skew, so);
         hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
-                           (const uint32_t*)skew, c->words, bp.ib, c->keys[0], d_sa);
+                           (const uint32_t*)skew, c->words, bp.ib, c->keys[0], d_sa, so);
     }
     tm.end();
     add_bytes(st, SA_K_LOCAL_SORT, 24 * n);
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words + 6, c->words + 6, 20, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     if (c->host_words[6]) {
         SA_TRACE("  bucketed round 1: local sort flags %u, full sort instead", c->host_words[6]);
         return SA_OK;
+    }
+    seg[0] = c->host_words[0];
+    seg[1] = c->host_words[1];
+    seg[2] = c->host_words[2];
+    add_bytes(st, SA_K_LOCAL_SORT, seg[1] * 28);   // unsorted set: rank, member bit, 3 tmp words
+    if (seg[1] <= n / kSparseDiv) {
+        // the unsorted set, in SA order
+        tm.begin(SA_K_SEG_WRITE);
+        const uint32_t wb = (uint32_t)((nw + 1 + kWsBlock - 1) / kWsBlock);
+        uint32_t* part = c->hist;   // 2 words per block (<= 2 * 256 * kMaxChunks)
+        hipLaunchKernelGGL(k_wscan_reduce, dim3(wb), dim3(kBlock), 0, s, (const uint32_t*)cnt_u, (const uint32_t*)cnt_g,
+                           nw, part);
+        hipLaunchKernelGGL(k_wscan_top, dim3(1), dim3(kBlock), 0, s, part, wb);
+        hipLaunchKernelGGL(k_wscan_apply, dim3(wb), dim3(kBlock), 0, s, cnt_u, cnt_g, nw, (const uint32_t*)part);
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((c->host_words[7] + kWaves - 1) / kWaves, 4096));
+        hipLaunchKernelGGL(k_u_gather, dim3(g), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)c->words,
+                           (const uint32_t*)ws, (const uint32_t*)cnt_u, (const uint32_t*)cnt_g, so, c->u_pos[0],
+                           c->u_idx[0], c->u_g[0]);
+        tm.end();
+        add_bytes(st, SA_K_SEG_WRITE, 8 * (2 * nw + 2) + seg[1] * 24);
+        SA_HIP(hipGetLastError());
+        *fused = true;
     }
     SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R, bp.bs.rb,
              c->host_words[7], c->host_words[10], c->host_words[5]);
