@@ -668,7 +668,26 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         const int ui = uo;
         uo ^= 1;
         uint64_t* sorted;
-        if (sparse) {
+        if (c->radix == 0) {
+            // keys (g, rank[i + h]) once into ukb1 -- the first pass reads them
+            // from there and the second overwrites them -- with the digit totals
+            rc = onesweep_prepare(c, s);
+            if (rc) return rc;
+            const uint32_t Pu = (bits + 7) / 8;
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 2048);
+            tm.begin(SA_K_SORT_U);
+            if (sparse)
+                hipLaunchKernelGGL(k_materialize<SrcU<true>>, dim3(grid), dim3(kBlock), 0, s,
+                                   SrcU<true>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, m, Pu, ukb1, os_ghist(c));
+            else
+                hipLaunchKernelGGL(k_materialize<SrcU<false>>, dim3(grid), dim3(kBlock), 0, s,
+                                   SrcU<false>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, m, Pu, ukb1, os_ghist(c));
+            tm.end();
+            SA_HIP(hipGetLastError());
+            add_bytes(st, SA_K_SORT_U, 16 * m);
+            rc = radix_sort(c, SrcKeys{ukb1, c->u_idx[ui]}, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s,
+                            tm, st, &sorted, &P, true, true);
+        } else if (sparse) {
             SrcU<true> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
             rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P,
                             false, true);

@@ -58,6 +58,27 @@ __global__ __launch_bounds__(kBlock) void k_global_hist(Src src, uint64_t n, uin
     }
 }
 
+// keys of a generated source written once (an unsorted-set round's keys cost
+// a binary search each: computing them in both the histogram and the first
+// scatter doubled that), with the digit totals of every pass
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_materialize(Src src, uint64_t n, uint32_t passes,
+                                                        uint64_t* __restrict__ keys, uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t s_h[kMaxPasses][kRadix];
+    for (int i = threadIdx.x; i < (int)(kMaxPasses * kRadix); i += kBlock) (&s_h[0][0])[i] = 0;
+    __syncthreads();
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = src.key(e);
+        keys[e] = k;
+        for (uint32_t p = 0; p < passes; ++p) atomicAdd(&s_h[p][(k >> (8 * p)) & 0xFFu], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t v = s_h[p][threadIdx.x];
+        if (v) atomicAdd(&ghist[p * kRadix + threadIdx.x], v);
+    }
+}
+
 // base[p][d] = sum of ghist[p][d'] for d' < d; one workgroup per pass
 __global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restrict__ ghist,
                                                        uint32_t* __restrict__ base) {
