@@ -25,7 +25,7 @@ using namespace sa;
         }                                                                                     \
     } while (0)
 
-// key = bucket << rb | random rbits bits, bucket = (i << 16) / n (rb = 28;
+// key = bucket << rb | random rbits bits, bucket = (i << 17) / n (rb = 28;
 // fewer random bits make equal keys: unsorted groups for the segments)
 __global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb, uint32_t rbits) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
@@ -34,9 +34,9 @@ __global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb, 
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         z ^= z >> 31;
         if (rbits == 0) {   // DNA-like: low = 20 + 13 E, E uniform in [0, 4^12) (s = 8, R = 12)
-            keys[i] = ((i << 16) / n << rb) | (20 + 13 * (z % (1ull << 24)));
+            keys[i] = ((i << 17) / n << rb) | (20 + 13 * (z % (1ull << 24)));
         } else {
-            keys[i] = ((i << 16) / n << rb) | ((z & ((1ull << rbits) - 1)) << (rb - rbits));
+            keys[i] = ((i << 17) / n << rb) | ((z & ((1ull << rbits) - 1)) << (rb - rbits));
         }
         vals[i] = (uint32_t)(z >> 32);
     }
@@ -64,7 +64,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&ovals, n * 4));
     const uint64_t nw = (n + kWinStride - 1) / kWinStride;
     CK(hipMalloc(&ws, (3 * nw + 2) * 4));
-    CK(hipMalloc(&words, 64));
+    CK(hipMalloc(&words, 256));
     uint32_t* list = ws + nw + 1;
     uint32_t* skew = list + nw;
     hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, n, rb, rbits);
@@ -76,10 +76,10 @@ int main(int argc, char** argv) {
     uint32_t* cnt;
     CK(hipMalloc(&cnt, (2 * nw + 2) * 4));
     const SegOut so{rank, member, tmp, tmp + n, tmp + 2 * n, cnt, cnt + nw + 1};
-    CK(hipMemset(words, 0, 64));
-    const uint64_t cmul = 1ull << 32;   // bucket = D (16 bits)
+    CK(hipMemset(words, 0, 256));
+    const uint64_t cmul = 1;   // bucket = D = key >> rb (17 bits), bsh = 0
     hipLaunchKernelGGL(k_window_starts, dim3((uint32_t)std::min<uint64_t>((nw + 256) / 256, 8192)), dim3(256), 0, 0,
-                       (const uint64_t*)keys, n, nw, rb, cmul, ws);
+                       (const uint64_t*)keys, n, nw, rb, cmul, 0u, ws);
     hipLaunchKernelGGL(k_window_list, dim3((uint32_t)std::min<uint64_t>((nw + 255) / 256, 1024)), dim3(256), 0, 0,
                        (const uint32_t*)ws, nw, list, words);
     CK(hipDeviceSynchronize());
@@ -107,7 +107,7 @@ int main(int argc, char** argv) {
     timeit("copy 12 B in + out", [&] {
         hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
     });
-    for (uint32_t g : {256u}) {
+    for (uint32_t g : {512u}) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
         timeit(nm, [&] {
@@ -128,11 +128,24 @@ int main(int argc, char** argv) {
                                words, ib, okeys, ovals, skew, SegOut{});
         });
     }
+    {   // per-phase clock64 spans of one workgroup's thread 0, per window
+        CK(hipMemset(words + 32, 0, 64));
+        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 2>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
+                           (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
+        CK(hipDeviceSynchronize());
+        unsigned long long t[7];
+        CK(hipMemcpy(t, words + 32, 56, hipMemcpyDeviceToHost));
+        const char* nm[7] = {"load+minmax", "histogram", "scan", "scatter", "net-sort", "U+scan", "store+sync"};
+        double tot = 0;
+        for (int k = 0; k < 7; ++k) tot += (double)t[k];
+        for (int k = 0; k < 7; ++k)
+            std::printf("  phase %-12s %7.0f clk/window (%4.1f %%)\n", nm[k], (double)t[k] / hw[7], 100.0 * t[k] / tot);
+    }
     CK(hipMemcpy(hw, words, 64, hipMemcpyDeviceToHost));
     std::printf("flags=%u skewed=%u heads=%u unsorted=%u groups=%u (accumulated over runs)\n", hw[6], hw[10], hw[0], hw[1], hw[2]);
     // check: output sorted within each window, keys monotone overall
     std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
-    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(256), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
                        (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
     CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
     size_t bad = 0;

@@ -41,37 +41,37 @@
 namespace sa {
 
 constexpr int kBsBlock = 1024;               // local sort workgroup (16 waves)
-constexpr int kBsItems = 18;                 // per thread
-constexpr int kBsCap = kBsBlock * kBsItems;  // 18432 suffixes per window (147 KiB of LDS)
+constexpr int kBsItems = 9;                  // per thread
+constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window (72 KiB of LDS: two workgroups per CU)
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
-constexpr uint32_t kBsGrid = 256;            // one local-sort workgroup per CU (LDS-bound)
+constexpr uint32_t kBsGrid = 512;            // two local-sort workgroups per CU (LDS-bound)
 constexpr uint64_t kBucketMinN = 1ull << 20; // auto: bucketed first round from 1 Mi suffixes
 
-__device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64_t cmul) {
-    return (uint32_t)(((key1 >> rb) * cmul) >> 32);
+__device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64_t cmul, uint32_t bsh) {
+    return (uint32_t)(((key1 >> rb) * cmul) >> bsh);
 }
 
 // radix sources of the two bucket passes (digits of bucket_of(key))
 struct SrcBucketIota {
     const uint64_t* __restrict__ keys;
-    uint32_t rb;
+    uint32_t rb, bsh;
     uint64_t cmul;
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
     __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
-        return (bucket_of(k, rb, cmul) >> shift) & mask;
+        return (bucket_of(k, rb, cmul, bsh) >> shift) & mask;
     }
 };
 
 struct SrcBucketKeys {
     const uint64_t* __restrict__ keys;
     const uint32_t* __restrict__ vals;
-    uint32_t rb;
+    uint32_t rb, bsh;
     uint64_t cmul;
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return vals[e]; }
     __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
-        return (bucket_of(k, rb, cmul) >> shift) & mask;
+        return (bucket_of(k, rb, cmul, bsh) >> shift) & mask;
     }
 };
 
@@ -79,7 +79,8 @@ struct SrcBucketKeys {
 // key1 in text order.  Like k_pack_text: a tile of codes (+ K-1 halo) staged
 // in LDS, 16 consecutive keys per lane (Horner for the first, rolling
 // updates of D and of the remainder for the rest), staged again in LDS for a
-// coalesced store; LDS histograms of the two bucket bytes -> ghist[2][256].
+// coalesced store; LDS histograms of the bucket's low byte -> ghist[0..255]
+// and of its high bb - 8 bits -> ghist[256 ..].
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, Chunking ch,
@@ -87,11 +88,12 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
                                                         uint32_t* __restrict__ ghist) {
     __shared__ uint16_t s_code[256];
     __shared__ uint16_t s_c[kTile + kMaxK];
-    __shared__ uint32_t s_hist[2][kRadix];
+    __shared__ uint32_t s_hlo[kRadix];
+    __shared__ uint32_t s_hhi[1024];
     __shared__ uint64_t s_k[kTile + kTile / kPackRun];
     s_code[threadIdx.x] = code[threadIdx.x];
-    s_hist[0][threadIdx.x] = 0;
-    s_hist[1][threadIdx.x] = 0;
+    s_hlo[threadIdx.x] = 0;
+    for (int i = threadIdx.x; i < 1024; i += kBlock) s_hhi[i] = 0;
     const uint32_t K = b.s + b.R;
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
@@ -136,9 +138,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
             const uint64_t key = (D << b.rb) | low;
             kd[j] = key;
             if (i < e1) {
-                const uint32_t bk = bucket_of(key, b.rb, b.cmul);
-                atomicAdd(&s_hist[0][bk & 0xFFu], 1u);
-                atomicAdd(&s_hist[1][(bk >> 8) & 0xFFu], 1u);
+                const uint32_t bk = bucket_of(key, b.rb, b.cmul, b.bsh);
+                atomicAdd(&s_hlo[bk & 0xFFu], 1u);
+                atomicAdd(&s_hhi[bk >> 8], 1u);
             }
         }
         __syncthreads();
@@ -150,10 +152,9 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
         }
         __syncthreads();
     }
-    for (int p = 0; p < 2; ++p) {
-        const uint32_t v = s_hist[p][threadIdx.x];
-        if (v) atomicAdd(&ghist[p * kRadix + threadIdx.x], v);
-    }
+    if (s_hlo[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], s_hlo[threadIdx.x]);
+    for (uint32_t i = threadIdx.x; i < (1u << (b.bb - 8)); i += kBlock)
+        if (s_hhi[i]) atomicAdd(&ghist[kRadix + i], s_hhi[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
 // g == 0, g == n or bucket(g) != bucket(g-1) (gallop, then bisect); j <= nw.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_window_starts(const uint64_t* __restrict__ keys, uint64_t n,
-                                                          uint64_t nw, uint32_t rb, uint64_t cmul,
+                                                          uint64_t nw, uint32_t rb, uint64_t cmul, uint32_t bsh,
                                                           uint32_t* __restrict__ ws) {
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j <= nw; j += (uint64_t)gridDim.x * kBlock) {
         const uint64_t x = j * kWinStride;
@@ -171,8 +172,8 @@ __global__ __launch_bounds__(kBlock) void k_window_starts(const uint64_t* __rest
         } else if (x == 0) {
             res = 0;
         } else {
-            const uint32_t bx = bucket_of(keys[x - 1], rb, cmul);
-            if (bucket_of(keys[x], rb, cmul) != bx) {
+            const uint32_t bx = bucket_of(keys[x - 1], rb, cmul, bsh);
+            if (bucket_of(keys[x], rb, cmul, bsh) != bx) {
                 res = x;
             } else {
                 uint64_t lo = x, hi, step = 1;   // bucket(lo) == bx
@@ -182,13 +183,13 @@ __global__ __launch_bounds__(kBlock) void k_window_starts(const uint64_t* __rest
                         hi = n;
                         break;
                     }
-                    if (bucket_of(keys[hi], rb, cmul) != bx) break;
+                    if (bucket_of(keys[hi], rb, cmul, bsh) != bx) break;
                     lo = hi;
                     step *= 2;
                 }
                 while (hi - lo > 1) {   // first index in (lo, hi] past bucket bx (n counts)
                     const uint64_t mid = lo + (hi - lo) / 2;
-                    if (bucket_of(keys[mid], rb, cmul) != bx) hi = mid;
+                    if (bucket_of(keys[mid], rb, cmul, bsh) != bx) hi = mid;
                     else lo = mid;
                 }
                 res = hi;
@@ -249,13 +250,14 @@ __global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restri
 //   1. counting scatter on the top kSubBits of the key span: LDS histogram
 //      (16-bit counters packed in pairs, atomics), scan, atomic cursors ->
 //      s_w holds 2^kSubBits sub-buckets of a few suffixes each (random text);
-//   2. each thread insertion-sorts its four sub-buckets in LDS;
+//   2. each suffix counts the smaller keys of its sub-bucket (its rank in
+//      it), then all move to their final slots;
 //   3. s_w is written out in order: sorted key1 and SA, coalesced.
 // A window with a sub-bucket above kMaxSub (many equal or clustered keys) is
 // appended to `skew` (count in words[10]) and left to k_bucket_sort_lsd.
 // err bit 0: window larger than the LDS tile; bit 1: key span too wide.
 // ---------------------------------------------------------------------------
-constexpr int kSubBits = 12;
+constexpr int kSubBits = 11;
 constexpr int kSubBuckets = 1 << kSubBits;
 constexpr uint32_t kMaxSub = 64;
 
@@ -363,9 +365,12 @@ __device__ __forceinline__ void window_segments(const uint64_t* __restrict__ s_w
     auto masks = [&](uint32_t rb0, uint64_t& mh, uint64_t& mu, uint64_t& muh) {
         const uint32_t le = rb0 + lane;
         const bool ok = le < m;
-        const uint64_t cur = ok ? s_w[le] >> ib : 0ull;
-        const bool head = ok && (le == 0 || (s_w[le - 1] >> ib) != cur);
-        const bool nhead = ok && (le + 1 == m || (s_w[le + 1] >> ib) != cur);
+        const uint32_t lc = ok ? le : m - 1;   // three independent LDS reads, no branches
+        const uint64_t cur = s_w[lc] >> ib;
+        const uint64_t prv = s_w[lc ? lc - 1 : 0] >> ib;
+        const uint64_t nxt = s_w[lc + 1 < m ? lc + 1 : lc] >> ib;
+        const bool head = ok && (le == 0 || prv != cur);
+        const bool nhead = ok && (le + 1 == m || nxt != cur);
         const bool in_u = ok && !(head && nhead);
         mh = __ballot(head);
         mu = __ballot(in_u);
@@ -376,7 +381,7 @@ __device__ __forceinline__ void window_segments(const uint64_t* __restrict__ s_w
     int32_t last_h = -1;
     uint32_t nh = 0, nu = 0, ng = 0;
     uint32_t urows = 0;
-#pragma unroll 1
+#pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t rb0 = wave * WT + i * kWave;
         if (rb0 >= m) break;   // uniform per wave
@@ -541,8 +546,49 @@ __global__ __launch_bounds__(kBlock) void k_u_gather(const uint32_t* __restrict_
     }
 }
 
+// Batcher's odd-even merge sort of N registers (N a power of two), fully
+// unrolled: (N = 16) 63 compare-exchanges of u64.
+template <int N>
+__device__ __forceinline__ void sort_net(uint64_t (&v)[N]) {
+#pragma unroll
+    for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % p; j + k < N; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; ++i)
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        const uint64_t x = v[i + j], y = v[i + j + k];
+                        const bool sw = y < x;
+                        v[i + j] = sw ? y : x;
+                        v[i + j + k] = sw ? x : y;
+                    }
+}
+
+// The same network on u32 keys: a compare-exchange is one v_min + one v_max.
+template <int N>
+__device__ __forceinline__ void sort_net32(uint32_t (&v)[N]) {
+#pragma unroll
+    for (int p = 1; p < N; p <<= 1)
+#pragma unroll
+        for (int k = p; k >= 1; k >>= 1)
+#pragma unroll
+            for (int j = k % p; j + k < N; j += 2 * k)
+#pragma unroll
+                for (int i = 0; i < k; ++i)
+                    if (i + j + k < N && (i + j) / (2 * p) == (i + j + k) / (2 * p)) {
+                        const uint32_t x = v[i + j], y = v[i + j + k];
+                        v[i + j] = x < y ? x : y;
+                        v[i + j + k] = x < y ? y : x;
+                    }
+}
+
+constexpr int kNet = 16;   // sub-buckets up to this size are sorted in registers
+
 // kVariant (microbenchmarks only; 0 in the product): 1 skips the sort (the
-// loaded window is written back in input order)
+// loaded window is written back in input order); 2 accumulates per-phase
+// clock64() spans of thread 0 into words[16..23] (words must hold 24 u64)
 template <int BLOCK, int ITEMS, int kVariant = 0>
 __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint32_t* __restrict__ vals_in,
@@ -558,7 +604,8 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
     __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
     __shared__ uint32_t s_tmp[WAVES];
     __shared__ uint64_t s_red[2][WAVES];
-    static_assert(kSubBuckets == 4 * BLOCK, "four sub-buckets (two words) per thread");
+    constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
+    static_assert(WPT >= 1 && WPT * 2 * BLOCK == kSubBuckets, "whole counter words per thread");
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -567,7 +614,16 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
     auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
     static_assert(WAVES * ITEMS * 8 <= kSubBuckets * 2, "per-row segment values fit in s_cnt");
     uint64_t th = 0, tu = 0, tg = 0;
+    uint64_t tacc[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
+    auto stamp = [&](int k) {
+        if constexpr ((kVariant & 2) != 0) {
+            const uint64_t now = clock64();
+            if (k >= 0) tacc[k] += now - tlast;
+            tlast = now;
+        }
+    };
     for (uint32_t q = blockIdx.x; q < nlist; q += gridDim.x) {
+        stamp(-1);
         const uint32_t j = list[q];
         const uint64_t a = ws[j];
         const uint32_t m = (uint32_t)(ws[j + 1] - a);
@@ -583,6 +639,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
             __syncthreads();
             continue;
         }
+        stamp(0);
         const uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
         if constexpr ((kVariant & 1) != 0) {
 #pragma unroll
@@ -602,16 +659,24 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
             }
         }
         __syncthreads();
-        // exclusive scan of the 4096 counts (four per thread) and their maximum
+        stamp(1);
+        // exclusive scan of the counts (2 WPT per thread, 16 bits each) and
+        // their maximum
         uint32_t big = 0;
         {
-            const uint32_t p0 = s_cnt[2 * dg], p1 = s_cnt[2 * dg + 1];
-            const uint32_t c0 = p0 & 0xFFFFu, c1 = p0 >> 16, c2 = p1 & 0xFFFFu, c3 = p1 >> 16;
-            const uint32_t sum = c0 + c1 + c2 + c3;
+            uint32_t c[2 * WPT], sum = 0, cm = 0;
+#pragma unroll
+            for (int x = 0; x < WPT; ++x) {
+                const uint32_t pw = s_cnt[WPT * dg + x];
+                c[2 * x] = pw & 0xFFFFu;
+                c[2 * x + 1] = pw >> 16;
+            }
+#pragma unroll
+            for (int x = 0; x < 2 * WPT; ++x) {
+                sum += c[x];
+                cm = c[x] > cm ? c[x] : cm;
+            }
             const uint32_t inc = wave_inclusive_sum(sum);
-            uint32_t cm = c0 > c1 ? c0 : c1;
-            cm = c2 > cm ? c2 : cm;
-            cm = c3 > cm ? c3 : cm;
 #pragma unroll
             for (int o = kWave / 2; o > 0; o >>= 1) {
                 const uint32_t y = __shfl_xor(cm, o, kWave);
@@ -626,11 +691,16 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
                 off += (x < (int)wave) ? s_tmp[x] : 0u;
                 big = (uint32_t)s_red[0][x] > big ? (uint32_t)s_red[0][x] : big;
             }
-            const uint32_t b0 = off + inc - sum, b1 = b0 + c0, b2 = b1 + c1, b3 = b2 + c2;
-            s_cnt[2 * dg] = b0 | (b1 << 16);
-            s_cnt[2 * dg + 1] = b2 | (b3 << 16);
+            uint32_t b = off + inc - sum;
+#pragma unroll
+            for (int x = 0; x < WPT; ++x) {
+                const uint32_t b0 = b, b1 = b + c[2 * x];
+                s_cnt[WPT * dg + x] = b0 | (b1 << 16);
+                b = b1 + c[2 * x + 1];
+            }
         }
         __syncthreads();
+        stamp(2);
         if (big > kMaxSub) {   // uniform: clustered keys, leave the window to the LSD kernel
             if (threadIdx.x == 0) skew[atomicAdd(&words[10], 1u)] = j;
             __syncthreads();
@@ -646,28 +716,137 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restric
             }
         }
         __syncthreads();
-        // ... then each thread insertion-sorts four sub-buckets in place (a
-        // few suffixes each for random text; no per-item registers needed)
+        stamp(3);
+        // ... then each thread sorts its 2 WPT consecutive sub-buckets: up to
+        // kNet suffixes in registers (Batcher network), larger ones by
+        // insertion in LDS.  Equal keys share a sub-bucket, so the sorted
+        // sub-bucket also gives the groups: heads, unsorted members (U, groups
+        // of two or more) and U heads, counted per thread in SA order.
+        uint32_t nh = 0, nu = 0, ng = 0;
+        const uint32_t sb0 = 2 * WPT * dg;
+        const uint32_t low_bits = bits > (uint32_t)kSubBits ? bits - kSubBits : bits;
+        const uint32_t low_mask = low_bits >= 32 ? ~0u : ((1u << low_bits) - 1u);
 #pragma unroll 1
-        for (uint32_t sb = dg; sb < (uint32_t)kSubBuckets; sb += BLOCK) {
-            const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
-            for (uint32_t k = lo + 1; k < hi; ++k) {
-                const uint64_t x = s_w[k];
-                uint32_t y = k;
-                while (y > lo && s_w[y - 1] > x) {
-                    s_w[y] = s_w[y - 1];
-                    --y;
+        for (uint32_t sb = sb0; sb < sb0 + 2 * WPT; ++sb) {
+            const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
+            if (cnt == 0) continue;
+            if (cnt <= (uint32_t)kNet && low_bits <= 28) {
+                // u32 sort keys: the key bits below the sub-bucket's (exact:
+                // equal ⇔ same group) over the slot in the sub-bucket
+                uint32_t v[kNet];
+#pragma unroll
+                for (int t = 0; t < kNet; ++t)
+                    v[t] = (uint32_t)t < cnt ? (((uint32_t)(s_w[lo + t] >> ib) & low_mask) << 4) | (uint32_t)t : ~0u;
+                sort_net32<kNet>(v);
+                uint64_t x[kNet];
+#pragma unroll
+                for (int t = 0; t < kNet; ++t) x[t] = (uint32_t)t < cnt ? s_w[lo + (v[t] & 15u)] : 0ull;
+#pragma unroll
+                for (int t = 0; t < kNet; ++t) {
+                    if ((uint32_t)t < cnt) {
+                        s_w[lo + t] = x[t];
+                        const uint32_t r = v[t] >> 4;
+                        const bool eqp = t > 0 && (v[t > 0 ? t - 1 : 0] >> 4) == r;
+                        const bool eqn = (uint32_t)t + 1 < cnt && (v[t + 1 < kNet ? t + 1 : t] >> 4) == r;
+                        nh += eqp ? 0u : 1u;
+                        nu += (eqp || eqn) ? 1u : 0u;
+                        ng += (!eqp && eqn) ? 1u : 0u;
+                    }
                 }
-                s_w[y] = x;
+            } else {
+                for (uint32_t k = lo + 1; k < hi; ++k) {
+                    const uint64_t x = s_w[k];
+                    uint32_t y = k;
+                    while (y > lo && s_w[y - 1] > x) {
+                        s_w[y] = s_w[y - 1];
+                        --y;
+                    }
+                    s_w[y] = x;
+                }
+                uint64_t pr = ~0ull, cur = s_w[lo] >> ib;
+                for (uint32_t k = lo; k < hi; ++k) {
+                    const uint64_t nx = k + 1 < hi ? (s_w[k + 1] >> ib) : ~0ull;
+                    const bool eqp = k > lo && pr == cur, eqn = k + 1 < hi && nx == cur;
+                    nh += eqp ? 0u : 1u;
+                    nu += (eqp || eqn) ? 1u : 0u;
+                    ng += (!eqp && eqn) ? 1u : 0u;
+                    pr = cur;
+                    cur = nx;
+                }
+            }
+        }
+        stamp(4);
+        // exclusive U / U-group offsets of this thread's sub-buckets in the
+        // window, and the window totals
+        uint32_t bu, bg, th_w, tu_w, tg_w;
+        {
+            const uint32_t iu = wave_inclusive_sum(nu), ig = wave_inclusive_sum(ng), ih = wave_inclusive_sum(nh);
+            __syncthreads();   // s_red / s_tmp reads of the scan above are done
+            if (lane == kWave - 1) {
+                s_tmp[wave] = iu;
+                s_red[0][wave] = (uint64_t)ig | ((uint64_t)ih << 32);
+            }
+            __syncthreads();
+            uint32_t ou = 0, og = 0;
+            th_w = tu_w = tg_w = 0;
+#pragma unroll
+            for (int x = 0; x < WAVES; ++x) {
+                const uint32_t xu = s_tmp[x], xg = (uint32_t)s_red[0][x], xh = (uint32_t)(s_red[0][x] >> 32);
+                if (x < (int)wave) {
+                    ou += xu;
+                    og += xg;
+                }
+                tu_w += xu;
+                tg_w += xg;
+                th_w += xh;
+            }
+            bu = ou + iu - nu;
+            bg = og + ig - ng;
+        }
+        if (so.rank) {
+            if (threadIdx.x == 0) {
+                so.cnt_u[j] = tu_w;
+                so.cnt_g[j] = tg_w;
+                th += th_w;
+                tu += tu_w;
+                tg += tg_w;
+            }
+            // the unsorted members of this thread's sub-buckets (rare): rank =
+            // group head position + 1, member bit, (p, x, U group) at their
+            // window-local U index
+            if (nu) {
+                const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
+                const uint32_t lo0 = sb0 ? end_of(sb0 - 1) : 0u, hi0 = end_of(sb0 + 2 * WPT - 1);
+                uint32_t head = lo0, ku = bu, kg = bg;
+                uint64_t pr = ~0ull;
+                for (uint32_t k = lo0; k < hi0; ++k) {
+                    const uint64_t x = s_w[k], r = x >> ib;
+                    const uint64_t nx = k + 1 < hi0 ? (s_w[k + 1] >> ib) : ~0ull;
+                    const bool eqp = k > lo0 && pr == r, eqn = k + 1 < hi0 && nx == r;
+                    if (!eqp) head = k;
+                    if (!eqp && eqn) ++kg;
+                    if (eqp || eqn) {
+                        const uint32_t xi = (uint32_t)(x & imask);
+                        so.rank[xi] = (uint32_t)(a + head) + 1u;
+                        atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
+                        so.tmp_pos[a + ku] = (uint32_t)(a + k);
+                        so.tmp_idx[a + ku] = xi;
+                        so.tmp_g[a + ku] = kg - 1u;
+                        ++ku;
+                    }
+                    pr = r;
+                }
             }
         }
         __syncthreads();
-        // 3. the window's segments, then out in order (the stores go last: on
-        // gfx950 vmcnt counts stores too, so any later vmcnt wait in this
-        // window -- spill reloads included -- would drain them)
-        if (so.rank) window_segments<BLOCK, ITEMS>(s_w, reinterpret_cast<uint64_t*>(s_cnt), s_red, a, m, ib, j, so, th, tu, tg);
+        stamp(5);
         store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
+        stamp(6);
+    }
+    if constexpr ((kVariant & 2) != 0) {
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 7; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(words + 32) + k, tacc[k]);
     }
     flush_totals(words, th, tu, tg);
 }

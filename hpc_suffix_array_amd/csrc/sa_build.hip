@@ -128,7 +128,10 @@ static uint64_t ws_bytes(uint64_t n) {
     return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + m * 8 + m / 8 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
 }
 
-static uint64_t tile_states_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * kRadix * 8; }
+// tile states for the widest digit (the bucketed first round's high pass
+// uses up to 10 bits)
+constexpr uint64_t kMaxRadix = 1024;
+static uint64_t tile_states_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * kMaxRadix * 8; }
 
 static void free_ctx_buffers(sa_context* c) {
     hipFree(c->rank);
@@ -290,25 +293,25 @@ static int onesweep_prepare(sa_context* c, hipStream_t s) {
     return SA_OK;
 }
 
-static uint32_t next_epoch(sa_context* c, hipStream_t s, uint64_t tiles) {
+static uint32_t next_epoch(sa_context* c, hipStream_t s) {
     if (++c->epoch > kEpochMask) {
-        hipMemsetAsync(c->states, 0, tiles * kRadix * 8, s);
+        hipMemsetAsync(c->states, 0, tile_states_bytes(c->cap), s);
         c->epoch = 1;
     }
     return c->epoch;
 }
 
-template <class Src>
+template <class Src, int RBITS = 8>
 static void onesweep_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits,
                           const uint32_t* base, uint32_t* ticket, uint64_t* out_keys, uint32_t* out_vals,
                           hipStream_t s) {
     const uint64_t tiles = (n + kTile - 1) / kTile;
-    const uint32_t epoch = next_epoch(c, s, tiles);
+    const uint32_t epoch = next_epoch(c, s);
     // 1024 x 4: 16 waves per tile, 2 workgroups (32 waves) per CU -- the
     // fastest shape in microbench.hip (r01: 10.4 ms per 2^30-pair pass)
     static_assert(kOsBlock * kOsItems == kTile, "tile states are sized for kTile");
-    hipLaunchKernelGGL((k_onesweep<Src, kOsBlock, kOsItems>), dim3((uint32_t)tiles), dim3(kOsBlock), 0, s, src, n, shift,
-                       nbits, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
+    hipLaunchKernelGGL((k_onesweep<Src, kOsBlock, kOsItems, 0, RBITS>), dim3((uint32_t)tiles), dim3(kOsBlock), 0, s, src,
+                       n, shift, nbits, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
 }
 
 // Stable LSD sort of ch.n (key, idx) pairs over key bits [0, bits): the first

@@ -89,8 +89,9 @@ struct SrcText {
 struct BucketSpec {
     uint64_t pow_s1;   // sigma^(s-1)
     uint64_t powR1;    // sigma^(R-1)
-    uint64_t cmul;     // floor(2^48 / sigma^s): bucket = (D * cmul) >> 32
+    uint64_t cmul;     // floor(2^48 / sigma^s): bucket = (D * cmul) >> bsh
     uint32_t sigma, s, R, rb;
+    uint32_t bb, bsh;  // bucket bits (16..18), bsh = 48 - bb
 };
 
 // key1 of position i, computed from the text (rank look-ups of later rounds)

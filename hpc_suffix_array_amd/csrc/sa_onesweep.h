@@ -79,6 +79,21 @@ __global__ __launch_bounds__(kBlock) void k_materialize(Src src, uint64_t n, uin
     }
 }
 
+// base[d] = sum of ghist[d'] for d' < d over `bins` <= 1024 entries (a pass
+// of RBITS > 8 spans several 256-entry rows of the ghist / base layout)
+__global__ __launch_bounds__(1024) void k_digit_base_wide(const uint32_t* __restrict__ ghist, uint32_t bins,
+                                                          uint32_t* __restrict__ base) {
+    __shared__ uint32_t s_tmp[16];
+    const uint32_t i = threadIdx.x;
+    const uint32_t x = i < bins ? ghist[i] : 0u;
+    const uint32_t inc = wave_inclusive_sum(x);
+    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+    if (i < bins) base[i] = off + inc - x;
+}
+
 // base[p][d] = sum of ghist[p][d'] for d' < d; one workgroup per pass
 __global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restrict__ ghist,
                                                        uint32_t* __restrict__ base) {
@@ -90,7 +105,9 @@ __global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restric
 // kVariant (microbenchmarks only; 0 in the product): bit 0 skips the look-back
 // (tile offsets faked), bit 1 skips the ranking (identity layout), bit 2
 // skips the LDS staging (writes straight from registers).
-template <class Src, int BLOCK, int ITEMS, int kVariant = 0>
+// RBITS: digit width (8, or 9 for the bucketed first round's high pass);
+// digit_base and states are laid out with 1 << RBITS entries per tile.
+template <class Src, int BLOCK, int ITEMS, int kVariant = 0, int RBITS = 8>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
                                                     const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
@@ -99,14 +116,16 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     constexpr int WAVES = BLOCK / kWave;
     constexpr int TILE = BLOCK * ITEMS;
     constexpr int WTILE = kWave * ITEMS;
-    static_assert(BLOCK >= kRadix, "one thread per digit");
+    constexpr int RADIX = 1 << RBITS;
+    constexpr int RWAVES = RADIX / kWave;   // waves holding one digit per thread
+    static_assert(BLOCK >= RADIX, "one thread per digit");
     static_assert(TILE <= 65535, "16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint32_t s_vals[TILE];
-    __shared__ uint16_t s_wcnt[WAVES][kRadix];   // per-wave digit counts, then wave offsets
-    __shared__ uint16_t s_start[kRadix];         // digit run starts in the tile
-    __shared__ uint32_t s_gofs[kRadix];
-    __shared__ uint32_t s_tmp[kWaves];
+    __shared__ uint16_t s_wcnt[WAVES][RADIX];   // per-wave digit counts, then wave offsets
+    __shared__ uint16_t s_start[RADIX];         // digit run starts in the tile
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile;
 
     const uint32_t wave = wave_id(), lane = lane_id();
@@ -123,7 +142,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         }
         s_tile = tk;
     }
-    for (int i = threadIdx.x; i < WAVES * kRadix; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
+    for (int i = threadIdx.x; i < WAVES * RADIX; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
     const uint64_t t = s_tile;
     const uint64_t tb = t * TILE;
@@ -138,14 +157,14 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         const bool ok = le < valid;
         k[j] = ok ? src.key(tb + le) : 0ull;
         v[j] = ok ? src.val(tb + le) : 0u;
-        d[j] = ok ? src_digit(src, k[j], shift, mask, 0) : kRadix;
+        d[j] = ok ? src_digit(src, k[j], shift, mask, 0) : RADIX;
     }
     uint32_t r[ITEMS];
     uint16_t* wc = s_wcnt[wave];
     if constexpr ((kVariant & 2) == 0) {
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            const bool ok = d[j] < (uint32_t)kRadix;
+            const bool ok = d[j] < (uint32_t)RADIX;
             uint64_t peers = __ballot(ok);
             for (uint32_t b = 0; b < nbits; ++b) {
                 const bool bit = (d[j] >> b) & 1u;
@@ -164,9 +183,9 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     }
     __syncthreads();
 
-    const uint32_t dg = threadIdx.x;   // digit owned by this thread (dg < 256)
+    const uint32_t dg = threadIdx.x;   // digit owned by this thread (dg < RADIX)
     uint32_t tile_cnt = 0;
-    if (dg < (uint32_t)kRadix) {
+    if (dg < (uint32_t)RADIX) {
 #pragma unroll
         for (int w = 0; w < WAVES; ++w) {
             const uint32_t x = s_wcnt[w][dg];
@@ -174,24 +193,24 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
             tile_cnt += x;
         }
         const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
-        st_store(&states[t * kRadix + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+        st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
     }
     // tile layout: exclusive scan of the per-digit counts (threads >= 256 add 0)
     {
-        const uint32_t x = (dg < (uint32_t)kRadix) ? tile_cnt : 0u;
+        const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
         const uint32_t inc = wave_inclusive_sum(x);
-        if (lane == kWave - 1 && wave < (uint32_t)kWaves) s_tmp[wave] = inc;
+        if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
         __syncthreads();
         uint32_t off = 0;
 #pragma unroll
-        for (int w = 0; w < kWaves; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
-        if (dg < (uint32_t)kRadix) s_start[dg] = (uint16_t)(off + inc - x);
+        for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+        if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
     }
     // look back (one thread per digit)
-    if (dg < (uint32_t)kRadix) {
+    if (dg < (uint32_t)RADIX) {
         uint64_t excl = 0;
         if constexpr ((kVariant & 1) != 0) {
-            excl = t * (uint64_t)(TILE / kRadix);
+            excl = t * (uint64_t)(TILE / RADIX);
         } else if (t > 0) {
             // read kLook predecessors per step (independent loads: one
             // fabric round trip per kLook tiles instead of per tile)
@@ -203,7 +222,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
                 uint64_t sv[kLook];
 #pragma unroll
                 for (int i = 0; i < kLook; ++i)
-                    sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * kRadix + dg]) : 0ull;
+                    sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * RADIX + dg]) : 0ull;
                 int used = 0;
                 bool done = false;
 #pragma unroll
@@ -230,7 +249,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
                 }
             }
             const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
-            st_store(&states[t * kRadix + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
+            st_store(&states[t * RADIX + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
         }
         s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
     }
@@ -239,7 +258,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         // no LDS staging: scatter straight from registers
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            if (d[j] < (uint32_t)kRadix) {
+            if (d[j] < (uint32_t)RADIX) {
                 const uint64_t g = (uint64_t)s_gofs[d[j]] + s_wcnt[wave][d[j]] + r[j];
                 if (g < n) {
                     out_keys[g] = k[j];
@@ -251,7 +270,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
-        if (d[j] < (uint32_t)kRadix) {
+        if (d[j] < (uint32_t)RADIX) {
             const uint32_t pos = (kVariant & 2) ? (uint32_t)(wave * WTILE) + r[j]
                                                 : s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
             s_keys[pos] = k[j];

@@ -19,9 +19,12 @@ struct BucketPlan {
 static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p) {
     if (round1 == SA_ROUND1_LSD || radix != 0 || sigma < 2 || n < 2) return false;
     if (round1 == SA_ROUND1_AUTO && n < kBucketMinN) return false;
-    uint64_t ps = 1;   // sigma^s >= 2^16: the 16-bit bucket is dense
+    // bucket bits: windows of about n / 2^bb suffixes must fit the
+    // 9216-suffix LDS tile with room for random fluctuation
+    const uint32_t bb = n <= (1ull << 29) ? 16u : (n <= (1ull << 30) ? 17u : 18u);
+    uint64_t ps = 1;   // sigma^s >= 2^bb: the bb-bit bucket is dense
     uint32_t s = 0;
-    while (ps < 65536) {
+    while (ps < (1ull << bb)) {
         ps *= sigma;
         ++s;
     }
@@ -29,7 +32,7 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     const uint32_t ib = bit_width(n - 1);
     const uint32_t bd = bit_width(ps - 1);
     // D values per bucket, +1 bit for a window holding two buckets
-    const uint32_t span = bit_width((ps + 65535) / 65536) + 1;
+    const uint32_t span = bit_width((ps + (1ull << bb) - 1) >> bb) + 1;
     for (uint32_t R = K - s; R >= 1; --R) {
         unsigned __int128 pr = 1;   // sigma^R
         for (uint32_t t = 0; t < R; ++t) pr *= sigma;
@@ -42,7 +45,9 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
         if (bd + rb > 64 || rb + span + ib > 64) continue;
         p->bs.pow_s1 = ps / sigma;
         p->bs.powR1 = (uint64_t)(pr / sigma);
-        p->bs.cmul = (1ull << 48) / ps;
+        p->bs.cmul = (1ull << 48) / ps;   // bucket = (D * cmul) >> (48 - bb) < 2^bb
+        p->bs.bb = bb;
+        p->bs.bsh = 48u - bb;
         p->bs.sigma = sigma;
         p->bs.s = s;
         p->bs.R = R;
@@ -75,18 +80,31 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                        bp.bs, c->keys[1], os_ghist(c));
     tm.end();
     add_bytes(st, SA_K_PACK, 9 * n);
+    const uint32_t hb = bp.bs.bb - 8;   // high-pass digit bits (8..10)
     tm.begin(SA_K_SCAN);
-    hipLaunchKernelGGL(k_digit_base, dim3(2), dim3(kBlock), 0, s, (const uint32_t*)os_ghist(c), os_base(c));
+    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c), (uint32_t)kRadix,
+                       os_base(c));
+    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c) + kRadix, 1u << hb,
+                       os_base(c) + kRadix);
     tm.end();
-    // two stable passes over the bucket's bytes: text order -> bucket order
+    // two stable passes over the bucket: low byte, then the high bb - 8 bits
+    // (text order -> bucket order)
     tm.begin(SA_K_SCATTER_FIRST);
-    onesweep_pass(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.cmul}, n, 0, 8, os_base(c), os_tickets(c), c->keys[0],
-                  c->vals_alt, s);
+    onesweep_pass(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.bsh, bp.bs.cmul}, n, 0, 8, os_base(c), os_tickets(c),
+                  c->keys[0], c->vals_alt, s);
     tm.end();
     add_bytes(st, SA_K_SCATTER_FIRST, 20 * n);
     tm.begin(SA_K_SCATTER_KEYS);
-    onesweep_pass(c, SrcBucketKeys{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.cmul}, n, 8, 8, os_base(c) + kRadix,
-                  os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+    {
+        const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
+        if (hb == 8)
+            onesweep_pass<SrcBucketKeys, 8>(c, sb, n, 8, 8, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+        else if (hb == 9)
+            onesweep_pass<SrcBucketKeys, 9>(c, sb, n, 8, 9, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+        else
+            onesweep_pass<SrcBucketKeys, 10>(c, sb, n, 8, 10, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u,
+                                             s);
+    }
     tm.end();
     add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);
     SA_HIP(hipGetLastError());
@@ -98,7 +116,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nw + kBlock) / kBlock, 8192);
         hipLaunchKernelGGL(k_window_starts, dim3(g1), dim3(kBlock), 0, s, (const uint64_t*)c->keys_u, n, nw, bp.bs.rb,
-                           bp.bs.cmul, ws);
+                           bp.bs.cmul, bp.bs.bsh, ws);
         const uint32_t g2 = (uint32_t)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(k_window_list, dim3(g2), dim3(kBlock), 0, s, (const uint32_t*)ws, nw, list, c->words);
     }

@@ -6,9 +6,10 @@ and WRITE_SIZE per launch (rocprofv3 --pmc, KiB -> bytes), and HBM traffic
 per launch corrected as MI355X_MICROARCH.md section HBM prescribes: on gfx950
 FETCH_SIZE under-reads wide coalesced streams (x2 for 16-B/lane reads) and
 other access widths must be calibrated on a known byte count.  The read
-calibration here is the first (full-n) k_seg_count launch, which reads
-exactly 8 bytes per suffix (the sorted u64 keys) and writes 16 bytes per
-4096-suffix tile: read_factor = 8n / FETCH bytes of that launch.
+calibration here is the k_alphabet launch, which reads exactly the n text
+bytes (16 B per lane): read_factor = n / FETCH bytes of that launch (2.0 as
+the guide prescribes; the local sort, which reads exactly 12 B per suffix in
+8-B and 4-B lanes, lands within 3 % of 12 with the same factor).
 WRITE_SIZE is reported as measured (exact for 16-B/lane streaming stores per
 the guide; the scatter's 8-B / 4-B run stores are uncalibrated).
 """
@@ -29,7 +30,8 @@ KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist
          ("k_onesweep<sa::SrcKeysIota", "scatter_iota"), ("k_onesweep<sa::SrcKeys,", "scatter_keys"),
          ("k_onesweep<sa::SrcBucketIota", "scatter_first"), ("k_onesweep<sa::SrcBucketKeys", "scatter_keys"),
          ("k_pack_bucket", "pack"), ("k_window_starts", "windows"), ("k_window_max", "windows"),
-         ("k_bucket_sort", "local_sort"),
+         ("k_bucket_sort_lsd", "local_sort_lsd"), ("k_bucket_sort", "local_sort"),
+         ("k_materialize", "sort_u_keys"), ("k_wscan_", "seg_write"), ("k_u_gather", "seg_write"),
          ("k_onesweep<sa::SrcU", "scatter_u"), ("k_onesweep<sa::SrcRank", "scatter_rank"),
          ("k_global_hist", "global_hist"), ("k_digit_base", "digit_base"), ("k_alphabet", "alphabet"),
          ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
@@ -92,9 +94,10 @@ def main():
                         acc[k][grid(row)].append(float(row["Counter_Value"]) * 1024.0)   # KiB -> bytes
         pmc[name] = {k: sum(v[max(v)]) / len(v[max(v)]) for k, v in acc.items() if v}
     fetch, write = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
+    # calibration: k_alphabet reads exactly n text bytes (16 B per lane)
     read_factor = None
-    if fetch.get("seg_count"):
-        read_factor = 8.0 * n / fetch["seg_count"]
+    if fetch.get("alphabet"):
+        read_factor = 1.0 * n / fetch["alphabet"]
     kernels = {}
     for k, v in per.items():
         full = v["full"][max(v["full"])]
@@ -116,7 +119,7 @@ def main():
             bench = json.loads(f.read())
     summary = {
         "tag": tag, "n": n, "kind": kind, "args": args,
-        "read_calibration": {"kernel": "seg_count (full-n launch)", "known_read_bytes": 8 * n,
+        "read_calibration": {"kernel": "alphabet (full-n launch)", "known_read_bytes": n,
                              "factor": read_factor},
         "kernels": kernels,
         # per full-size launch, keyed like bench.py's kernel kinds
