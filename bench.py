@@ -16,11 +16,12 @@ range-partitioned build of ONE n-symbol string over all ranks
 "strong"; `--mode replicas` instead builds one string per rank (weak).
 
 Output: one JSON line on rank 0 with the driver's contract keys plus
-"roofline" (dominant kernel: the single-pass radix scatter over stored keys,
-algorithmic bytes 24 B/suffix per launch, HIP-event timed in the timed
-region; N = 1) and "cpu_baseline" (the oracle's reference-identical
-single-thread restatement of src/sequential on a bounded sample, rank 0,
-N = 1 only).
+"roofline" (the dominant kernel -- most HIP-event time per build -- with its
+algorithmic bytes per launch over its mean launch duration, timed in the
+timed region; N = 1; "traffic" from the committed rocprof summary of the same
+workload), "kernels_gbs" (the same for every kernel kind) and "cpu_baseline"
+(the oracle's reference-identical single-thread restatement of src/sequential
+on a bounded sample, rank 0, N = 1 only).
 """
 from __future__ import annotations
 
