@@ -28,6 +28,7 @@
 #include "sa_kernels.h"
 #include "sa_lcp.h"
 #include "sa_onesweep.h"
+#include "sa_split.h"
 
 namespace sa {
 
@@ -107,6 +108,7 @@ struct sa_context {
     uint64_t* states = nullptr;                 // onesweep tile states [tiles][256]
     uint32_t epoch = 0;                         // onesweep state tag of the last pass
     int radix = 0;                              // 0 onesweep, 1 reduce-then-scan
+    int cus = 256;                              // compute units (persistent grids)
     uint32_t* member = nullptr;                 // bitmap of round-1 unsorted positions
     uint32_t* hist = nullptr;      // 256 * kMaxChunks
     uint32_t* totals = nullptr;    // 256
@@ -945,6 +947,8 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
     SA_HIP(hipSetDevice(device));
     sa_context* c = new sa_context();
     c->device = device;
+    if (hipDeviceGetAttribute(&c->cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || c->cus <= 0)
+        c->cus = 256;
     if (hipMalloc(&c->hist, (size_t)kRadix * kMaxChunks * 4) != hipSuccess ||
         hipMalloc(&c->totals, kRadix * 4) != hipSuccess || hipMalloc(&c->counts, 4 * kMaxChunks * 4) != hipSuccess ||
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||

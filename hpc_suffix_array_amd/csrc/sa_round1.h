@@ -59,6 +59,17 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     return false;
 }
 
+// one persistent single-pass scatter (sa_split.h): one workgroup per CU
+template <class Src, int RBITS, bool STABLE>
+static void split_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t lshift, uint32_t lmask,
+                       const uint32_t* base, uint32_t* ticket, uint64_t* out_keys, uint32_t* out_vals, hipStream_t s) {
+    const uint32_t epoch = next_epoch(c, s);
+    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
+    hipLaunchKernelGGL((k_split<Src, RBITS, STABLE>), dim3(grid), dim3(kSpBlock), 0, s, src, n, shift, lshift, lmask,
+                       base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
+}
+
 // *done: the SA and keys[0] hold the sorted first round.  *fused: the
 // round-1 segments were produced with it (few unsorted suffixes): rank[] for
 // the unsorted set only (member bitmap), the unsorted set compacted in
@@ -87,23 +98,24 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c) + kRadix, 1u << hb,
                        os_base(c) + kRadix);
     tm.end();
-    // two stable passes over the bucket: low byte, then the high bb - 8 bits
-    // (text order -> bucket order)
+    // two passes over the bucket: its low byte (any order within a digit),
+    // then its high bb - 8 bits, keeping the low byte's order (text order ->
+    // bucket order; sa_split.h)
     tm.begin(SA_K_SCATTER_FIRST);
-    onesweep_pass(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.bsh, bp.bs.cmul}, n, 0, 8, os_base(c), os_tickets(c),
-                  c->keys[0], c->vals_alt, s);
+    split_pass<SrcBucketIota, 8, false>(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.bsh, bp.bs.cmul}, n, 0, 0, 0,
+                                        os_base(c), os_tickets(c), c->keys[0], c->vals_alt, s);
     tm.end();
     add_bytes(st, SA_K_SCATTER_FIRST, 20 * n);
     tm.begin(SA_K_SCATTER_KEYS);
     {
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
+        uint32_t* tk = os_tickets(c) + 1;
         if (hb == 8)
-            onesweep_pass<SrcBucketKeys, 8>(c, sb, n, 8, 8, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+            split_pass<SrcBucketKeys, 8, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
         else if (hb == 9)
-            onesweep_pass<SrcBucketKeys, 9>(c, sb, n, 8, 9, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u, s);
+            split_pass<SrcBucketKeys, 9, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
         else
-            onesweep_pass<SrcBucketKeys, 10>(c, sb, n, 8, 10, os_base(c) + kRadix, os_tickets(c) + 1, c->keys_u, c->vals_u,
-                                             s);
+            split_pass<SrcBucketKeys, 10, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);

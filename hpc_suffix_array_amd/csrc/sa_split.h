@@ -1,0 +1,293 @@
+// sa_split.h -- the two bucket passes of the bucketed first round
+// (sa_round1.h) as persistent single-pass scatters: the counting passes of
+// radix_sort_suffixes_seq (manber_myers.c:15-34) over the bucket digits.
+//
+// Differences from k_onesweep (sa_onesweep.h), measured in
+// microbench_radix.hip (2^30 pairs, 8-bit digits: 10.3 -> 7.1 ms):
+//   * 8192-pair tiles (1024 x 8): half the look-back work and state traffic,
+//     digit runs twice as long (fewer partial-line writes);
+//   * ranks from one LDS atomic per pair instead of per-wave match-any
+//     ballots; the first pass need not be stable (the local sort orders each
+//     window by (key, suffix) completely), the second must keep the order of
+//     the first pass's digit only, which it does by ranking one previous
+//     digit value at a time (a tile of bucket-ordered input spans one or two
+//     of them), falling back to stable ballots when a tile spans more;
+//   * persistent workgroups that take tiles from the ticket in order and
+//     issue the next tile's loads right after ranking the current one, so
+//     they are in flight during the look-back, the LDS staging and the writes.
+// Tile ids still come from the ticket, so a tile waits only on tiles whose
+// workgroups already run: a workgroup's prefetched tile is always later than
+// its current one, hence the smallest unfinished tile is always being
+// processed and the look-back cannot deadlock.
+#pragma once
+#include "sa_onesweep.h"
+
+namespace sa {
+
+constexpr int kSpBlock = 1024;
+constexpr int kSpItems = 8;
+constexpr int kSpTile = kSpBlock * kSpItems;   // 8192 pairs
+constexpr int kSpWaves = kSpBlock / kWave;
+constexpr uint32_t kSpMaxRounds = 4;           // previous-digit values ranked one at a time
+
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) x = min(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, kWave));
+    return x;
+}
+
+// One pass over digit (src.digit(key, shift, RADIX - 1)).  STABLE: pairs of
+// equal digit keep the order of their previous-pass digit
+// src.digit(key, lshift, lmask) (the input is ordered by it); otherwise their
+// order is arbitrary.
+template <class Src, int RBITS, bool STABLE, bool FALLBACK = true>
+__global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_t shift, uint32_t lshift,
+                                                    uint32_t lmask, const uint32_t* __restrict__ digit_base,
+                                                    uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
+                                                    uint32_t epoch, uint64_t* __restrict__ out_keys,
+                                                    uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
+    constexpr int RADIX = 1 << RBITS;
+    constexpr int RWAVES = RADIX / kWave;
+    constexpr int WTILE = kWave * kSpItems;
+    constexpr int ITEMS = kSpItems;
+    static_assert(kSpBlock >= RADIX, "one thread per digit");
+    static_assert(kSpWaves * RADIX * 2 <= kSpTile * 8, "ballot wave counts alias the key stage");
+    __shared__ uint64_t s_keys[kSpTile];
+    __shared__ uint32_t s_vals[kSpTile];
+    __shared__ uint32_t s_cnt[RADIX];
+    __shared__ uint16_t s_start[RADIX];
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[RWAVES];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_lo[2];   // STABLE: min / max previous digit of the tile
+    uint16_t(*s_wcnt)[RADIX] = reinterpret_cast<uint16_t(*)[RADIX]>(s_keys);
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint32_t mask = RADIX - 1;
+    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
+    const uint32_t ep_now = epoch & kEpochMask;
+    if (dg == 0) {
+        s_tile[0] = atomicAdd(ticket, 1u);
+        s_lo[0] = ~0u;
+        s_lo[1] = 0u;
+    }
+    if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
+    __syncthreads();
+    uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    // clamped, unpredicated loads (pairs past the end are never ranked)
+    // (tile numbers come through LDS: readfirstlane keeps the tile base in
+    // scalar registers, so each load is a scalar base + 32-bit lane offset)
+    auto load = [&](uint64_t tt, uint64_t* kk, uint32_t* vv) {
+        const uint64_t tb = tt * kSpTile;
+        const uint32_t last = (uint32_t)min(n - 1 - tb, (uint64_t)(kSpTile - 1));
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const uint64_t e = tb + (le < last ? le : last);
+            kk[j] = src.key(e);
+            vv[j] = src.val(e);
+        }
+    };
+    if (t < tiles) load(t, k, v);
+    uint32_t par = 0;
+    while (t < tiles) {
+        const uint64_t tb = t * kSpTile;
+        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)kSpTile ? (n - tb) : (uint64_t)kSpTile);
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+        // dr[j] = digit << 16 | rank in the tile's digit run (< 2^13; digit RADIX: no pair)
+        uint32_t dr[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            dr[j] = (le < valid ? src_digit(src, k[j], shift, mask, 0) : (uint32_t)RADIX) << 16;
+        }
+        if constexpr (!STABLE) {
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j)
+                if ((dr[j] >> 16) < (uint32_t)RADIX) dr[j] |= atomicAdd(&s_cnt[dr[j] >> 16], 1u);
+            __syncthreads();
+        } else {
+            uint32_t lmin = ~0u, lmax = 0u;
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                if ((dr[j] >> 16) < (uint32_t)RADIX) {
+                    const uint32_t l = src_digit(src, k[j], lshift, lmask, 0);
+                    lmin = min(lmin, l);
+                    lmax = max(lmax, l);
+                }
+            }
+            lmin = wave_min_u32(lmin);
+            lmax = wave_max_u32(lmax);
+            if (lane == 0 && lmin <= lmax) {
+                atomicMin(&s_lo[0], lmin);
+                atomicMax(&s_lo[1], lmax);
+            }
+            __syncthreads();
+            const uint32_t l0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_lo[0]);
+            const uint32_t span = (uint32_t)__builtin_amdgcn_readfirstlane((int)(s_lo[1] - s_lo[0]));
+            if (!FALLBACK || span < kSpMaxRounds) {
+                // one previous-digit value per round: all pairs of value l
+                // take their ranks before any pair of value l + 1 (dr bits
+                // 13..15 hold l - l0 meanwhile)
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j)
+                    dr[j] |= ((src_digit(src, k[j], lshift, lmask, 0) - l0) & 7u) << 13;
+                for (uint32_t m = 0; m <= span; ++m) {
+#pragma unroll
+                    for (int j = 0; j < ITEMS; ++j) {
+                        if ((dr[j] >> 16) < (uint32_t)RADIX && ((dr[j] >> 13) & 7u) == m)
+                            dr[j] |= atomicAdd(&s_cnt[dr[j] >> 16], 1u);
+                    }
+                    __syncthreads();
+                }
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) dr[j] &= ~(7u << 13);
+            } else {
+                // stable ballots (match-any per wave), wave counts in the key stage
+                for (int i = dg; i < kSpWaves * RADIX; i += kSpBlock) (&s_wcnt[0][0])[i] = 0;
+                __syncthreads();
+                uint16_t* wc = s_wcnt[wave];
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j) {
+                    const uint32_t d = dr[j] >> 16;
+                    const bool ok = d < (uint32_t)RADIX;
+                    uint64_t peers = __ballot(ok);
+#pragma unroll
+                    for (int b = 0; b < RBITS; ++b) {
+                        const bool bit = (d >> b) & 1u;
+                        const uint64_t bal = __ballot(bit);
+                        peers &= bit ? bal : ~bal;
+                    }
+                    uint32_t cnt = 0;
+                    if (ok) cnt = wc[d];
+                    const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+                    dr[j] |= cnt + below;
+                    if (ok && below == 0) wc[d] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
+                }
+                __syncthreads();
+                if (dg < (uint32_t)RADIX) {
+                    uint32_t tot = 0;
+#pragma unroll
+                    for (int w = 0; w < kSpWaves; ++w) {
+                        const uint32_t x = s_wcnt[w][dg];
+                        s_wcnt[w][dg] = (uint16_t)tot;
+                        tot += x;
+                    }
+                    s_cnt[dg] = tot;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int j = 0; j < ITEMS; ++j)
+                    if ((dr[j] >> 16) < (uint32_t)RADIX) dr[j] += s_wcnt[wave][dr[j] >> 16];
+                __syncthreads();
+            }
+        }
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        uint64_t kn[ITEMS];
+        uint32_t vn[ITEMS];
+        if (tn < tiles) load(tn, kn, vn);
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)RADIX) {
+            tile_cnt = s_cnt[dg];
+            s_cnt[dg] = 0;   // for the next tile: its atomics come after three more barriers
+            st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+        }
+        if (STABLE && dg == 0) {
+            s_lo[0] = ~0u;
+            s_lo[1] = 0u;
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        if (dg < (uint32_t)RADIX) {
+            uint64_t excl = 0;
+            if (t > 0) {
+                constexpr int kLook = 4;
+                int64_t tp = (int64_t)t - 1;
+                uint32_t spins = 0;
+                while (tp >= 0) {
+                    uint64_t sv[kLook];
+#pragma unroll
+                    for (int i = 0; i < kLook; ++i)
+                        sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * RADIX + dg]) : 0ull;
+                    int used = 0;
+                    bool done = false;
+#pragma unroll
+                    for (int i = 0; i < kLook; ++i) {
+                        if (done || used != i) break;
+                        if (tp - i < 0) {
+                            done = true;
+                            break;
+                        }
+                        const uint64_t status = sv[i] & (3ull << 62);
+                        if (((uint32_t)(sv[i] >> 48) & kEpochMask) != ep_now || status == 0) break;
+                        excl += sv[i] & kCountMask;
+                        ++used;
+                        if (status == kStPrefix) done = true;
+                    }
+                    if (done) break;
+                    tp -= used;
+                    if (used == 0) {
+                        if (++spins > kSpinLimit) {
+                            atomicOr(err, 1u);
+                            break;
+                        }
+                        __builtin_amdgcn_s_sleep(1);
+                    }
+                }
+                st_store(&states[t * RADIX + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
+            }
+            s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t d = dr[j] >> 16;
+            if (d < (uint32_t)RADIX) {
+                const uint32_t pos = s_start[d] + (dr[j] & 0x1FFFu);
+                s_keys[pos] = k[j];
+                s_vals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * kSpBlock + dg;
+            if (q < valid) {
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = src_digit(src, key, shift, mask, 0);
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < n) {
+                    out_keys[g] = key;
+                    out_vals[g] = s_vals[q];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            k[j] = kn[j];
+            v[j] = vn[j];
+        }
+        t = tn;
+        par ^= 1u;
+    }
+}
+
+}  // namespace sa

@@ -186,7 +186,9 @@ def test_config3_1gib_minus_1_known_answer(gpu, oracle, golden):
     d_sa = torch.empty(n, dtype=torch.int32, device="cuda")
     b = DeviceBuilder(n)
     st = b.build(d_text, n, d_sa)
-    assert st["rounds"] == k["rounds"]
+    # the packed schedule (default) takes fewer, longer rounds than the
+    # reference's 5 (the h-prefix lengths per round are checked elsewhere)
+    assert st["schedule"] == "packed" and st["rounds"] <= k["rounds"]
     assert b.check(d_text, n, d_sa)
     sa = d_sa.cpu().numpy()
     assert oracle.sha256(sa) == k["sa_sha256_i32"]
