@@ -82,6 +82,9 @@ struct SrcBucketKeys {
 // coalesced store; LDS histograms of the bucket's low byte -> ghist[0..255]
 // and of its high bb - 8 bits -> ghist[256 ..].
 // ---------------------------------------------------------------------------
+// STORE false: the digit totals only (the fused first pass, sa_split.h
+// k_split_text, computes the keys itself)
+template <bool STORE = true>
 __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, Chunking ch,
                                                         BucketSpec b, uint64_t* __restrict__ keys,
@@ -136,7 +139,7 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
             const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
             const uint64_t low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
             const uint64_t key = (D << b.rb) | low;
-            kd[j] = key;
+            if constexpr (STORE) kd[j] = key;
             if (i < e1) {
                 const uint32_t bk = bucket_of(key, b.rb, b.cmul, b.bsh);
                 atomicAdd(&s_hlo[bk & 0xFFu], 1u);
@@ -144,17 +147,95 @@ __global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restric
             }
         }
         __syncthreads();
+        if constexpr (STORE) {
 #pragma unroll
-        for (int j = 0; j < kPackRun; ++j) {
-            const uint32_t q = j * kBlock + threadIdx.x;
-            const uint64_t g = tb + q;
-            if (g < e1) keys[g] = s_k[q + q / kPackRun];
+            for (int j = 0; j < kPackRun; ++j) {
+                const uint32_t q = j * kBlock + threadIdx.x;
+                const uint64_t g = tb + q;
+                if (g < e1) keys[g] = s_k[q + q / kPackRun];
+            }
+            __syncthreads();
         }
-        __syncthreads();
     }
     if (s_hlo[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], s_hlo[threadIdx.x]);
     for (uint32_t i = threadIdx.x; i < (1u << (b.bb - 8)); i += kBlock)
         if (s_hhi[i]) atomicAdd(&ghist[kRadix + i], s_hhi[i]);
+}
+
+// ---------------------------------------------------------------------------
+// Digit totals of the first bucket pass straight from the text: the bucket
+// depends on D (the first s dense digits, < sigma * 2^bb <= 2^26) only, so
+// each lane rolls D in 32 bits over 16 consecutive positions; an LDS
+// histogram of the low byte -> ghist[0..255] (the high bb - 8 bits are
+// counted by the first pass itself, k_split_text).  Grid-stride over
+// 4096-position tiles.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
+                                                        const uint16_t* __restrict__ code, BucketSpec b,
+                                                        uint32_t* __restrict__ ghist) {
+    constexpr int RUN = kTile / kBlock;   // 16
+    __shared__ uint8_t s_map[256];
+    __shared__ uint8_t s_dc[kTile + kMaxK];
+    __shared__ uint32_t s_hlo[kRadix];
+    {
+        const uint32_t cv = code[threadIdx.x];
+        s_map[threadIdx.x] = (uint8_t)(cv ? cv - 1u : 0u);
+    }
+    s_hlo[threadIdx.x] = 0;
+    const uint32_t sig = b.sigma, ps1 = (uint32_t)b.pow_s1;
+    const uint32_t shh = b.bsh;
+    __syncthreads();
+    const uint64_t tiles = (n + kTile - 1) / kTile;
+    for (uint64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
+        const uint64_t tb = tt * kTile;
+        {
+            const uint64_t i = tb + (uint64_t)threadIdx.x * RUN;
+            uint32_t w[4];
+            if (i + RUN <= n && (((uintptr_t)(text + i)) & 15) == 0) {
+                const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+                w[0] = v.x;
+                w[1] = v.y;
+                w[2] = v.z;
+                w[3] = v.w;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t o = 0;
+#pragma unroll
+                    for (int y = 0; y < 4; ++y) o |= (uint32_t)s_map[(w[q] >> (8 * y)) & 0xFFu] << (8 * y);
+                    w[q] = o;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    uint32_t o = 0;
+                    for (int y = 0; y < 4; ++y) {
+                        const uint64_t p = i + 4 * q + y;
+                        o |= (p < n ? (uint32_t)s_map[text[p]] : 0u) << (8 * y);
+                    }
+                    w[q] = o;
+                }
+            }
+            *reinterpret_cast<uint4*>(s_dc + threadIdx.x * RUN) = make_uint4(w[0], w[1], w[2], w[3]);
+            if (threadIdx.x < (uint32_t)kMaxK) {
+                const uint64_t h = tb + kTile + threadIdx.x;
+                s_dc[kTile + threadIdx.x] = (h < n) ? s_map[text[h]] : (uint8_t)0;
+            }
+        }
+        __syncthreads();
+        const uint32_t l0 = threadIdx.x * RUN;
+        uint32_t D = 0;
+        for (uint32_t q = 0; q < b.s; ++q) D = D * sig + s_dc[l0 + q];
+#pragma unroll
+        for (int j = 0; j < RUN; ++j) {
+            if (j > 0) D = (D - s_dc[l0 + j - 1] * ps1) * sig + s_dc[l0 + j - 1 + b.s];
+            if (tb + l0 + j < n) {
+                const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> shh);
+                atomicAdd(&s_hlo[bk & 0xFFu], 1u);
+            }
+        }
+        __syncthreads();
+    }
+    if (s_hlo[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], s_hlo[threadIdx.x]);
 }
 
 // ---------------------------------------------------------------------------

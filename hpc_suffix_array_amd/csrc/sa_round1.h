@@ -79,33 +79,45 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                            hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused, uint64_t seg[3]) {
     *done = false;
     *fused = false;
-    const Chunking ch = plan_chunks(n);
     int rc = onesweep_prepare(c, s);
     if (rc) return rc;
     // [0..2] D, m, G of the fused segments, [5] largest window, [6] local-sort
     // flags, [7] windows, [10] skewed windows
     SA_HIP(hipMemsetAsync(c->words, 0, 12, s));
     SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
+    // digit totals of both bucket passes (one read of the text)
     tm.begin(SA_K_PACK);
-    hipLaunchKernelGGL(k_pack_bucket, dim3(ch.chunks), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, ch,
-                       bp.bs, c->keys[1], os_ghist(c));
+    {
+        const uint64_t tiles = (n + kTile - 1) / kTile;
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4u * (uint32_t)c->cus));
+        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
+                           os_ghist(c));
+    }
     tm.end();
-    add_bytes(st, SA_K_PACK, 9 * n);
+    add_bytes(st, SA_K_PACK, n);
     const uint32_t hb = bp.bs.bb - 8;   // high-pass digit bits (8..10)
     tm.begin(SA_K_SCAN);
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c), (uint32_t)kRadix,
                        os_base(c));
-    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c) + kRadix, 1u << hb,
-                       os_base(c) + kRadix);
     tm.end();
     // two passes over the bucket: its low byte (any order within a digit),
     // then its high bb - 8 bits, keeping the low byte's order (text order ->
     // bucket order; sa_split.h)
     tm.begin(SA_K_SCATTER_FIRST);
-    split_pass<SrcBucketIota, 8, false>(c, SrcBucketIota{c->keys[1], bp.bs.rb, bp.bs.bsh, bp.bs.cmul}, n, 0, 0, 0,
-                                        os_base(c), os_tickets(c), c->keys[0], c->vals_alt, s);
+    {
+        const uint32_t epoch = next_epoch(c, s);
+        const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
+        hipLaunchKernelGGL(k_split_text, dim3(grid), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
+                           (const uint32_t*)os_base(c), c->states, os_tickets(c), epoch, c->keys[0], c->vals_alt,
+                           c->words + 4, os_ghist(c) + kRadix);
+    }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, 20 * n);
+    add_bytes(st, SA_K_SCATTER_FIRST, 13 * n);
+    tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
+    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c) + kRadix, 1u << hb,
+                       os_base(c) + kRadix);
+    tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};

@@ -20,6 +20,7 @@
 // its current one, hence the smallest unfinished tile is always being
 // processed and the look-back cannot deadlock.
 #pragma once
+#include "sa_bucket.h"
 #include "sa_onesweep.h"
 
 namespace sa {
@@ -39,6 +40,52 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) x = max(x, (uint32_t)__shfl_xor((int)x, o, kWave));
     return x;
+}
+
+// Decoupled look-back of digit dg for tile t (the tile's AGGREGATE is
+// already published): sums predecessors' counts, kLook state words per
+// step, until an INCLUSIVE prefix; publishes this tile's own prefix.
+template <int RADIX>
+__device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states, uint64_t t, uint32_t dg,
+                                                  uint32_t tile_cnt, uint64_t tag, uint32_t* __restrict__ err) {
+    uint64_t excl = 0;
+    if (t == 0) return 0;
+    constexpr int kLook = 4;
+    const uint32_t ep_now = (uint32_t)(tag >> 48) & kEpochMask;
+    int64_t tp = (int64_t)t - 1;
+    uint32_t spins = 0;
+    while (tp >= 0) {
+        uint64_t sv[kLook];
+#pragma unroll
+        for (int i = 0; i < kLook; ++i)
+            sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * RADIX + dg]) : 0ull;
+        int used = 0;
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < kLook; ++i) {
+            if (done || used != i) break;
+            if (tp - i < 0) {
+                done = true;
+                break;
+            }
+            const uint64_t status = sv[i] & (3ull << 62);
+            if (((uint32_t)(sv[i] >> 48) & kEpochMask) != ep_now || status == 0) break;
+            excl += sv[i] & kCountMask;
+            ++used;
+            if (status == kStPrefix) done = true;
+        }
+        if (done) break;
+        tp -= used;
+        if (used == 0) {
+            if (++spins > kSpinLimit) {
+                atomicOr(err, 1u);
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    st_store(&states[t * RADIX + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
+    return excl;
 }
 
 // One pass over digit (src.digit(key, shift, RADIX - 1)).  STABLE: pairs of
@@ -72,7 +119,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
     const uint32_t mask = RADIX - 1;
     const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
     const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
-    const uint32_t ep_now = epoch & kEpochMask;
     if (dg == 0) {
         s_tile[0] = atomicAdd(ticket, 1u);
         s_lo[0] = ~0u;
@@ -194,7 +240,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
-        if (tn < tiles) load(tn, kn, vn);
+        // the waves that look back issue their prefetch after it: vmcnt
+        // counts in order, so a look-back load issued behind the prefetch
+        // would wait for the whole next tile
+        if (dg >= (uint32_t)RADIX && tn < tiles) load(tn, kn, vn);
         uint32_t tile_cnt = 0;
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
@@ -216,44 +265,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
         }
         if (dg < (uint32_t)RADIX) {
-            uint64_t excl = 0;
-            if (t > 0) {
-                constexpr int kLook = 4;
-                int64_t tp = (int64_t)t - 1;
-                uint32_t spins = 0;
-                while (tp >= 0) {
-                    uint64_t sv[kLook];
-#pragma unroll
-                    for (int i = 0; i < kLook; ++i)
-                        sv[i] = (tp - i >= 0) ? st_load(&states[(uint64_t)(tp - i) * RADIX + dg]) : 0ull;
-                    int used = 0;
-                    bool done = false;
-#pragma unroll
-                    for (int i = 0; i < kLook; ++i) {
-                        if (done || used != i) break;
-                        if (tp - i < 0) {
-                            done = true;
-                            break;
-                        }
-                        const uint64_t status = sv[i] & (3ull << 62);
-                        if (((uint32_t)(sv[i] >> 48) & kEpochMask) != ep_now || status == 0) break;
-                        excl += sv[i] & kCountMask;
-                        ++used;
-                        if (status == kStPrefix) done = true;
-                    }
-                    if (done) break;
-                    tp -= used;
-                    if (used == 0) {
-                        if (++spins > kSpinLimit) {
-                            atomicOr(err, 1u);
-                            break;
-                        }
-                        __builtin_amdgcn_s_sleep(1);
-                    }
-                }
-                st_store(&states[t * RADIX + dg], kStPrefix | tag | ((excl + tile_cnt) & kCountMask));
-            }
+            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
             s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
+            if (tn < tiles) load(tn, kn, vn);
         }
         __syncthreads();
 #pragma unroll
@@ -288,6 +302,189 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         t = tn;
         par ^= 1u;
     }
+}
+
+// ---------------------------------------------------------------------------
+// The first bucket pass straight from the text (replaces k_pack_bucket +
+// k_split<SrcBucketIota>): each lane computes key1 of 8 consecutive
+// positions (Horner for the first, rolling updates of D and of the
+// remainder for the rest, as k_pack_bucket) from dense digits staged in LDS,
+// and the pair (key1, position) is scattered by the bucket's low byte.  The
+// order within a digit is arbitrary (LDS atomics), so the lane -> position
+// mapping is free.  The digit totals come from k_pack_bucket<false>.
+// The next tile's text (8 bytes per lane + the K - 1 byte halo) is loaded
+// into registers right after ranking the current one.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
+                                                         const uint16_t* __restrict__ code, BucketSpec b,
+                                                         const uint32_t* __restrict__ digit_base,
+                                                         uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
+                                                         uint32_t epoch, uint64_t* __restrict__ out_keys,
+                                                         uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err,
+                                                         uint32_t* __restrict__ ghist_hi) {
+    constexpr int RADIX = kRadix;
+    constexpr int RWAVES = RADIX / kWave;
+    constexpr int ITEMS = kSpItems;
+    constexpr int kHalo = kMaxK;   // >= K - 1 bytes past the tile
+    __shared__ uint64_t s_keys[kSpTile];
+    __shared__ uint16_t s_idx[kSpTile];
+    __shared__ uint8_t s_dig[kSpTile];
+    __shared__ uint8_t s_dc[kSpTile + kHalo];
+    __shared__ uint8_t s_map[256];
+    __shared__ uint32_t s_cnt[RADIX];
+    __shared__ uint16_t s_start[RADIX];
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[RWAVES];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (bucket >> 8)
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
+    const uint32_t K = b.s + b.R;
+    s_hhi[dg] = 0;
+    if (dg < 256u) {
+        const uint32_t cv = code[dg];
+        s_map[dg] = (uint8_t)(cv ? cv - 1u : 0u);
+        s_cnt[dg] = 0;
+    }
+    if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    // raw text: 8 bytes at tile offset 8 dg (dg < 1024), the halo at
+    // kSpTile + 8 (dg - 1024 ...) is loaded by lanes dg < kHalo / 8 as a
+    // second word; bytes at or past n are never read
+    auto load8 = [&](uint64_t pos) -> uint64_t {
+        if (pos + 8 <= n && (((uintptr_t)(text + pos)) & 7) == 0) return *reinterpret_cast<const uint64_t*>(text + pos);
+        uint64_t w = 0;
+        for (int q = 0; q < 8; ++q)
+            if (pos + q < n) w |= (uint64_t)text[pos + q] << (8 * q);
+        return w;
+    };
+    uint64_t raw = 0, rawh = 0;
+    auto load = [&](uint64_t tt) {
+        const uint64_t tb = tt * kSpTile;
+        raw = load8(tb + 8ull * dg);
+        if (dg < (uint32_t)(kHalo / 8)) rawh = load8(tb + kSpTile + 8ull * dg);
+    };
+    if (t < tiles) load(t);
+    uint32_t par = 0;
+    while (t < tiles) {
+        const uint64_t tb = t * kSpTile;
+        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)kSpTile ? (n - tb) : (uint64_t)kSpTile);
+        // dense digits (0 past the end)
+        {
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint64_t pos = tb + 8ull * dg + q;
+                const uint32_t x = pos < n ? s_map[(raw >> (8 * q)) & 0xFFu] : 0u;
+                if (q < 4) lo |= x << (8 * q);
+                else hi |= x << (8 * (q - 4));
+            }
+            *reinterpret_cast<uint2*>(s_dc + 8 * dg) = make_uint2(lo, hi);
+            if (dg < (uint32_t)(kHalo / 8)) {
+                lo = hi = 0;
+#pragma unroll
+                for (int q = 0; q < 8; ++q) {
+                    const uint64_t pos = tb + kSpTile + 8ull * dg + q;
+                    const uint32_t x = pos < n ? s_map[(rawh >> (8 * q)) & 0xFFu] : 0u;
+                    if (q < 4) lo |= x << (8 * q);
+                    else hi |= x << (8 * (q - 4));
+                }
+                *reinterpret_cast<uint2*>(s_dc + kSpTile + 8 * dg) = make_uint2(lo, hi);
+            }
+        }
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        // key1 of positions tb + 8 dg + j (D < sigma * 2^bb <= 2^26 rolls in
+        // 32 bits; the remainder in 64)
+        uint64_t k[ITEMS];
+        uint32_t dr[ITEMS];
+        {
+            const uint32_t l0 = 8 * dg;
+            uint32_t D = 0;
+            uint64_t r = 0;
+            for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
+            for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
+            const bool interior = tb + kSpTile + K <= n;   // every suffix of the tile has >= K symbols
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                if (j > 0) {
+                    const uint32_t xi = s_dc[l0 + j - 1 + b.s];
+                    D = (D - s_dc[l0 + j - 1] * (uint32_t)b.pow_s1) * b.sigma + xi;
+                    r = (r - (uint64_t)xi * b.powR1) * b.sigma + s_dc[l0 + j - 1 + K];
+                }
+                uint64_t low;
+                if (interior) {
+                    low = b.s + r * (b.R + 1) + b.R;
+                } else {
+                    const uint64_t L = n - (tb + l0 + j);   // wraps past the end: never ranked
+                    const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+                    low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
+                }
+                k[j] = ((uint64_t)D << b.rb) | low;
+                const bool ok = l0 + j < valid;
+                const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
+                const uint32_t d = ok ? (bk & 0xFFu) : (uint32_t)RADIX;
+                dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
+                if (ok) atomicAdd(&s_hhi[bk >> 8], 1u);
+            }
+        }
+        __syncthreads();
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        if (dg >= (uint32_t)RADIX && tn < tiles) load(tn);   // look-back waves: after it (see k_split)
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)RADIX) {
+            tile_cnt = s_cnt[dg];
+            s_cnt[dg] = 0;
+            st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        if (dg < (uint32_t)RADIX) {
+            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
+            s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
+            if (tn < tiles) load(tn);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t d = dr[j] >> 16;
+            if (d < (uint32_t)RADIX) {
+                const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
+                s_keys[pos] = k[j];
+                s_idx[pos] = (uint16_t)(8 * dg + j);
+                s_dig[pos] = (uint8_t)d;
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * kSpBlock + dg;
+            if (q < valid) {
+                const uint32_t dd = s_dig[q];
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < n) {
+                    out_keys[g] = s_keys[q];
+                    out_vals[g] = (uint32_t)(tb + s_idx[q]);
+                }
+            }
+        }
+        __syncthreads();
+        t = tn;
+        par ^= 1u;
+    }
+    if (s_hhi[dg]) atomicAdd(&ghist_hi[dg], s_hhi[dg]);
 }
 
 }  // namespace sa
