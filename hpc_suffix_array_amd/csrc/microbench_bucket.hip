@@ -128,6 +128,15 @@ int main(int argc, char** argv) {
                                words, ib, okeys, ovals, skew, SegOut{});
         });
     }
+    for (uint32_t g : {512u, 1024u}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "bucket_sort 512x18 + seg grid %u", g);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((k_bucket_sort<512, 18, 0>), dim3(g), dim3(512), 0, 0, (const uint64_t*)keys,
+                               (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals,
+                               skew, so);
+        });
+    }
     {   // per-phase clock64 spans of one workgroup's thread 0, per window
         CK(hipMemset(words + 32, 0, 64));
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 2>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,

@@ -40,11 +40,15 @@
 
 namespace sa {
 
-constexpr int kBsBlock = 1024;               // local sort workgroup (16 waves)
-constexpr int kBsItems = 9;                  // per thread
-constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window (72 KiB of LDS: two workgroups per CU)
+// local sort workgroup: 8 waves x 18 suffixes per lane; 72 KiB of LDS and
+// <= 128 VGPRs, so two workgroups share a CU and one's loads and stores
+// overlap the other's sorting (1024 x 9 ran one per CU: 11.1 -> 8.3 ms at
+// 2^30 in microbench_bucket)
+constexpr int kBsBlock = 512;
+constexpr int kBsItems = 18;
+constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
-constexpr uint32_t kBsGrid = 512;            // two local-sort workgroups per CU (LDS-bound)
+constexpr uint32_t kBsGrid = 1024;           // workgroups (two per CU resident, the rest queue)
 constexpr uint64_t kBucketMinN = 1ull << 20; // auto: bucketed first round from 1 Mi suffixes
 
 __device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64_t cmul, uint32_t bsh) {
@@ -671,7 +675,7 @@ constexpr int kNet = 16;   // sub-buckets up to this size are sorted in register
 // loaded window is written back in input order); 2 accumulates per-phase
 // clock64() spans of thread 0 into words[16..23] (words must hold 24 u64)
 template <int BLOCK, int ITEMS, int kVariant = 0>
-__global__ __launch_bounds__(BLOCK) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
+__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint32_t* __restrict__ vals_in,
                                                        const uint32_t* __restrict__ ws,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
