@@ -402,9 +402,9 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&states, states_n * 8));
     CK(hipMemset(states, 0, states_n * 8));
     CK(hipMalloc(&ws, 1 << 16));
-    CK(hipMalloc(&err, 4));
+    CK(hipMalloc(&err, 256));
     CK(hipMalloc(&chk, 16));
-    CK(hipMemset(err, 0, 4));
+    CK(hipMemset(err, 0, 256));
     hipLaunchKernelGGL(k_rand_keys, dim3(4096), dim3(256), 0, 0, k0, v0, n, 12345ull);
     uint32_t* ghist = ws;        // [2][1024]
     uint32_t* base = ws + 2048;  // [2][1024]
@@ -512,6 +512,37 @@ int main(int argc, char** argv) {
         std::printf("%-34s %8.3f ms %7.1f GB/s  unsorted(17 bits)=%llu sum=%016llx\n", "k_split B 9 bits stable", msb,
                     24.0 * n / msb / 1e6, h[0], h[1]);
     }
+    auto phases = [&](const char* name, auto launch) {
+        CK(hipMemset(err, 0, 256));
+        launch();
+        CK(hipDeviceSynchronize());
+        unsigned long long tp[5];
+        CK(hipMemcpy(tp, err + 2, 40, hipMemcpyDeviceToHost));
+        double tot = 0;
+        for (int q = 0; q < 5; ++q) tot += (double)tp[q];
+        const char* nm[5] = {"load+rank", "publish+scan", "lookback", "stage", "write"};
+        std::printf("%s phases:", name);
+        for (int q = 0; q < 5; ++q) std::printf("  %s %.1f%%", nm[q], 100.0 * tp[q] / tot);
+        unsigned long long ls[2];
+        CK(hipMemcpy(ls, err + 12, 16, hipMemcpyDeviceToHost));
+        const double tiles = (double)((n + kSpTile - 1) / kSpTile);
+        std::printf("  (%.0f clk per tile; look-back steps per tile-digit %.2f, empty %.2f)\n", tot / tiles,
+                    ls[0] / tiles / 256.0, ls[1] / tiles / 256.0);
+    };
+    phases("A", [&] {
+        CK(hipMemsetAsync(tick, 0, 4));
+        ++epoch;
+        hipLaunchKernelGGL((k_split<SrcKeys, 8, false, true, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
+                           SrcKeys{k0, v0}, n, shift, 0u, 0u, (const uint32_t*)base, states, tick, epoch, k1, v1, err);
+    });
+    phases("B", [&] {
+        CK(hipMemsetAsync(tick, 0, 4));
+        ++epoch;
+        hipLaunchKernelGGL((k_split<SrcKeys, 9, true, true, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
+                           SrcKeys{k1, v1}, n, 28u, shift, 255u, (const uint32_t*)(base + 1024), states, tick, epoch, k2,
+                           v2, err);
+    });
+    CK(hipMemset(err, 0, 8));
     uint32_t herr = 0;
     CK(hipMemcpy(&herr, err, 4, hipMemcpyDeviceToHost));
     std::printf("lookback_errors %u\n", herr);

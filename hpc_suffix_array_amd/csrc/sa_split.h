@@ -45,9 +45,10 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 // Decoupled look-back of digit dg for tile t (the tile's AGGREGATE is
 // already published): sums predecessors' counts, kLook state words per
 // step, until an INCLUSIVE prefix; publishes this tile's own prefix.
-template <int RADIX>
+template <int RADIX, bool PROF = false>
 __device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states, uint64_t t, uint32_t dg,
-                                                  uint32_t tile_cnt, uint64_t tag, uint32_t* __restrict__ err) {
+                                                  uint32_t tile_cnt, uint64_t tag, uint32_t* __restrict__ err,
+                                                  uint32_t* steps = nullptr) {
     uint64_t excl = 0;
     if (t == 0) return 0;
     constexpr int kLook = 4;
@@ -74,6 +75,10 @@ __device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states,
             ++used;
             if (status == kStPrefix) done = true;
         }
+        if constexpr (PROF) {
+            steps[0] += 1;
+            steps[1] += used == 0;
+        }
         if (done) break;
         tp -= used;
         if (used == 0) {
@@ -92,7 +97,7 @@ __device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states,
 // equal digit keep the order of their previous-pass digit
 // src.digit(key, lshift, lmask) (the input is ordered by it); otherwise their
 // order is arbitrary.
-template <class Src, int RBITS, bool STABLE, bool FALLBACK = true>
+template <class Src, int RBITS, bool STABLE, bool FALLBACK = true, bool PROF = false>
 __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_t shift, uint32_t lshift,
                                                     uint32_t lmask, const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
@@ -145,10 +150,20 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
     };
     if (t < tiles) load(t, k, v);
     uint32_t par = 0;
+    // PROF (microbenchmarks only): per-phase clock64 spans of thread 0
+    // accumulated into err[2..11] as u64
+    uint64_t tacc[5] = {0, 0, 0, 0, 0}, tlast = PROF ? clock64() : 0;
+    uint32_t lbsteps[2] = {0, 0};   // look-back steps, steps that found nothing ready
+    auto stamp = [&](int q) {
+        if constexpr (PROF) {
+            const uint64_t now = clock64();
+            tacc[q] += now - tlast;
+            tlast = now;
+        }
+    };
     while (t < tiles) {
         const uint64_t tb = t * kSpTile;
         const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)kSpTile ? (n - tb) : (uint64_t)kSpTile);
-        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         // dr[j] = digit << 16 | rank in the tile's digit run (< 2^13; digit RADIX: no pair)
         uint32_t dr[ITEMS];
 #pragma unroll
@@ -237,17 +252,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
                 __syncthreads();
             }
         }
-        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
-        uint64_t kn[ITEMS];
-        uint32_t vn[ITEMS];
-        // the waves that look back issue their prefetch after it: vmcnt
-        // counts in order, so a look-back load issued behind the prefetch
-        // would wait for the whole next tile
-        if (dg >= (uint32_t)RADIX && tn < tiles) load(tn, kn, vn);
+        stamp(0);
         uint32_t tile_cnt = 0;
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
-            s_cnt[dg] = 0;   // for the next tile: its atomics come after three more barriers
             st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
         }
         if (STABLE && dg == 0) {
@@ -264,12 +272,23 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
             for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
         }
+        stamp(1);
         if (dg < (uint32_t)RADIX) {
-            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
+            const uint64_t excl = tile_lookback<RADIX, PROF>(states, t, dg, tile_cnt, tag, err, lbsteps);
             s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
-            if (tn < tiles) load(tn, kn, vn);
         }
+        // the next tile: its ticket is taken only now (a tile is processed
+        // soon after its ticket, so successors seldom find it unpublished),
+        // its loads are in flight during the staging and the writes (past
+        // the last tile: the last again, unused; one program point for every
+        // wave, so nothing waits for them at a branch join)
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         __syncthreads();
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        uint64_t kn[ITEMS];
+        uint32_t vn[ITEMS];
+        load(tn < tiles ? tn : tiles - 1, kn, vn);
+        stamp(2);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
@@ -280,6 +299,8 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
             }
         }
         __syncthreads();
+        if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;   // the next tile's atomics come after the next barrier
+        stamp(3);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t q = j * kSpBlock + dg;
@@ -294,6 +315,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
             }
         }
         __syncthreads();
+        stamp(4);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             k[j] = kn[j];
@@ -301,6 +323,14 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         }
         t = tn;
         par ^= 1u;
+    }
+    if constexpr (PROF) {
+        if (dg == 0)
+            for (int q = 0; q < 5; ++q) atomicAdd(reinterpret_cast<unsigned long long*>(err + 2) + q, tacc[q]);
+        if (dg < (uint32_t)RADIX) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(err + 12), (unsigned long long)lbsteps[0]);
+            atomicAdd(reinterpret_cast<unsigned long long*>(err + 14), (unsigned long long)lbsteps[1]);
+        }
     }
 }
 
@@ -396,7 +426,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                 *reinterpret_cast<uint2*>(s_dc + kSpTile + 8 * dg) = make_uint2(lo, hi);
             }
         }
-        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         __syncthreads();
         // key1 of positions tb + 8 dg + j (D < sigma * 2^bb <= 2^26 rolls in
         // 32 bits; the remainder in 64)
@@ -433,8 +462,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
             }
         }
         __syncthreads();
-        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
-        if (dg >= (uint32_t)RADIX && tn < tiles) load(tn);   // look-back waves: after it (see k_split)
         uint32_t tile_cnt = 0;
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
@@ -454,9 +481,12 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         if (dg < (uint32_t)RADIX) {
             const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
             s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
-            if (tn < tiles) load(tn);
         }
+        // the next tile's ticket and text loads (see k_split)
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         __syncthreads();
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        load(tn < tiles ? tn : tiles - 1);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
