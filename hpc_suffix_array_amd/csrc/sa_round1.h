@@ -105,12 +105,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // bucket order; sa_split.h)
     tm.begin(SA_K_SCATTER_FIRST);
     {
-        const uint32_t epoch = next_epoch(c, s);
         const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
         hipLaunchKernelGGL(k_split_text, dim3(grid), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
-                           (const uint32_t*)os_base(c), c->states, os_tickets(c), epoch, c->keys[0], c->vals_alt,
-                           c->words + 4, os_ghist(c) + kRadix);
+                           (const uint32_t*)os_base(c), os_tickets(c), c->keys[0], c->vals_alt, os_ghist(c) + kRadix,
+                           os_ghist(c) + 5 * kRadix);
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_FIRST, 13 * n);

@@ -341,17 +341,17 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // remainder for the rest, as k_pack_bucket) from dense digits staged in LDS,
 // and the pair (key1, position) is scattered by the bucket's low byte.  The
 // order within a digit is arbitrary (LDS atomics), so the lane -> position
-// mapping is free.  The digit totals come from k_pack_bucket<false>.
-// The next tile's text (8 bytes per lane + the K - 1 byte halo) is loaded
-// into registers right after ranking the current one.
+// mapping is free, and so is the order of the tiles within a digit: each
+// tile claims its place from a per-digit cursor (no look-back).  The digit
+// totals come from k_bucket_hist.  The next tile's text (8 bytes per lane +
+// the K - 1 byte halo) is loaded while the current one is staged and written.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
-                                                         uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
-                                                         uint32_t epoch, uint64_t* __restrict__ out_keys,
-                                                         uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err,
-                                                         uint32_t* __restrict__ ghist_hi) {
+                                                         uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
+                                                         uint32_t* __restrict__ out_vals,
+                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
     constexpr int RADIX = kRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int ITEMS = kSpItems;
@@ -371,7 +371,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
-    const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
     const uint32_t K = b.s + b.R;
     s_hhi[dg] = 0;
     if (dg < 256u) {
@@ -466,7 +465,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
             s_cnt[dg] = 0;
-            st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+            // the pass need not be stable, so a tile's place in each digit
+            // is claimed from a cursor (one atomic round trip, whatever the
+            // other tiles do) instead of a look-back
+            s_gofs[dg] = digit_base[dg] + (tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u);
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
@@ -477,10 +479,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
 #pragma unroll
             for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
-        }
-        if (dg < (uint32_t)RADIX) {
-            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
-            s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
         }
         // the next tile's ticket and text loads (see k_split)
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
