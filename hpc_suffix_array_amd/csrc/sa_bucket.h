@@ -25,16 +25,22 @@
 // 16-bit bucket = (D * cmul) >> 32 (sigma^s >= 2^16) and the top bits of
 // low are near-uniform.
 //
-//   k_pack_bucket     text -> key1 in text order (+ the digit totals of the
-//                     two bucket passes)
-//   2 x k_onesweep    stable LSD passes over the bucket's two bytes
-//                     (SrcBucketIota, SrcBucketKeys)
+//   k_bucket_hist     text -> the first pass's digit totals (low kLoBits)
+//   k_split_text      first pass (sa_split.h): key1 computed per tile from
+//                     the text, scattered by the low kLoBits of the bucket
+//                     (unstable, atomic cursors; also counts the high bits)
+//   k_split           second pass: stable by the high bb - kLoBits bits
+//                     (SrcBucketKeys; look-back)
 //   k_window_starts   window j starts at the first bucket boundary >= j*W
-//   k_window_max      largest window (the host checks it against the LDS
-//                     capacity; oversize windows fall back to the full sort)
-//   k_bucket_sort     one workgroup per window: LSD radix in LDS over the
-//                     bits of key1 - min(window) (ascending idx packed below)
-//                     -> sorted key1 + SA, both written coalesced
+//   k_window_list     the non-empty windows and the largest (the host
+//                     checks it against the LDS capacity; oversize windows
+//                     fall back to the full LSD sort)
+//   k_bucket_sort     one workgroup per window: counting scatter into
+//                     sub-buckets + register sorting networks over
+//                     key1 - min(window) (idx packed below) -> sorted key1 +
+//                     SA written coalesced, and the round-1 groups
+//   k_bucket_sort_lsd windows with clustered keys: LSD passes in LDS
+//   k_wscan_* + k_u_gather  the unsorted set in SA order
 #pragma once
 #include "sa_kernels.h"
 
@@ -50,23 +56,17 @@ constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
 constexpr uint32_t kBsGrid = 1024;           // workgroups (two per CU resident, the rest queue)
 constexpr uint64_t kBucketMinN = 1ull << 20; // auto: bucketed first round from 1 Mi suffixes
+// bucket digits: the first pass (unstable, atomic cursors) takes the low
+// kLoBits, the second (stable, look-back) the remaining bb - kLoBits (9 + 8
+// at 2^30: 7.1 + 8.2 ms, 8 + 9: 6.0 + 9.0 ms)
+constexpr uint32_t kLoBits = 8;
+constexpr uint32_t kLoRadix = 1u << kLoBits;
 
 __device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64_t cmul, uint32_t bsh) {
     return (uint32_t)(((key1 >> rb) * cmul) >> bsh);
 }
 
-// radix sources of the two bucket passes (digits of bucket_of(key))
-struct SrcBucketIota {
-    const uint64_t* __restrict__ keys;
-    uint32_t rb, bsh;
-    uint64_t cmul;
-    __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
-    __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
-    __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
-        return (bucket_of(k, rb, cmul, bsh) >> shift) & mask;
-    }
-};
-
+// radix source of the second bucket pass (digits of bucket_of(key))
 struct SrcBucketKeys {
     const uint64_t* __restrict__ keys;
     const uint32_t* __restrict__ vals;
@@ -80,97 +80,10 @@ struct SrcBucketKeys {
 };
 
 // ---------------------------------------------------------------------------
-// key1 in text order.  Like k_pack_text: a tile of codes (+ K-1 halo) staged
-// in LDS, 16 consecutive keys per lane (Horner for the first, rolling
-// updates of D and of the remainder for the rest), staged again in LDS for a
-// coalesced store; LDS histograms of the bucket's low byte -> ghist[0..255]
-// and of its high bb - 8 bits -> ghist[256 ..].
-// ---------------------------------------------------------------------------
-// STORE false: the digit totals only (the fused first pass, sa_split.h
-// k_split_text, computes the keys itself)
-template <bool STORE = true>
-__global__ __launch_bounds__(kBlock) void k_pack_bucket(const uint8_t* __restrict__ text, uint64_t n,
-                                                        const uint16_t* __restrict__ code, Chunking ch,
-                                                        BucketSpec b, uint64_t* __restrict__ keys,
-                                                        uint32_t* __restrict__ ghist) {
-    __shared__ uint16_t s_code[256];
-    __shared__ uint16_t s_c[kTile + kMaxK];
-    __shared__ uint32_t s_hlo[kRadix];
-    __shared__ uint32_t s_hhi[1024];
-    __shared__ uint64_t s_k[kTile + kTile / kPackRun];
-    s_code[threadIdx.x] = code[threadIdx.x];
-    s_hlo[threadIdx.x] = 0;
-    for (int i = threadIdx.x; i < 1024; i += kBlock) s_hhi[i] = 0;
-    const uint32_t K = b.s + b.R;
-    const uint32_t c = blockIdx.x;
-    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
-    __syncthreads();
-    for (uint64_t tb = e0; tb < e1; tb += kTile) {
-        {
-            const uint64_t i = tb + (uint64_t)threadIdx.x * 16;
-            uint16_t* dst = s_c + threadIdx.x * 16;
-            if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
-                const uint4 v = *reinterpret_cast<const uint4*>(text + i);
-                const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int y = 0; y < 4; ++y) dst[4 * q + y] = s_code[(w4[q] >> (8 * y)) & 0xFFu];
-            } else {
-                for (int q = 0; q < 16; ++q) dst[q] = (i + q < n) ? s_code[text[i + q]] : (uint16_t)0;
-            }
-            if (threadIdx.x < K) {
-                const uint64_t h = tb + kTile + threadIdx.x;
-                s_c[kTile + threadIdx.x] = (h < n) ? s_code[text[h]] : (uint16_t)0;
-            }
-        }
-        __syncthreads();
-        const uint32_t l0 = threadIdx.x * kPackRun;
-        auto dc = [](uint32_t x) -> uint64_t { return x ? x - 1u : 0u; };
-        uint64_t D = 0, r = 0;
-        for (uint32_t t = 0; t < b.s; ++t) D = D * b.sigma + dc(s_c[l0 + t]);
-        for (uint32_t t = 0; t < b.R; ++t) r = r * b.sigma + dc(s_c[l0 + b.s + t]);
-        uint64_t* kd = s_k + threadIdx.x * (kPackRun + 1);
-#pragma unroll
-        for (int j = 0; j < kPackRun; ++j) {
-            if (j > 0) {
-                const uint64_t xi = dc(s_c[l0 + j - 1 + b.s]);
-                D = (D - dc(s_c[l0 + j - 1]) * b.pow_s1) * b.sigma + xi;
-                r = (r - xi * b.powR1) * b.sigma + dc(s_c[l0 + j - 1 + b.s + b.R]);
-            }
-            const uint64_t i = tb + l0 + j;
-            const uint64_t L = n - i;   // wraps past the end: never stored
-            const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
-            const uint64_t low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
-            const uint64_t key = (D << b.rb) | low;
-            if constexpr (STORE) kd[j] = key;
-            if (i < e1) {
-                const uint32_t bk = bucket_of(key, b.rb, b.cmul, b.bsh);
-                atomicAdd(&s_hlo[bk & 0xFFu], 1u);
-                atomicAdd(&s_hhi[bk >> 8], 1u);
-            }
-        }
-        __syncthreads();
-        if constexpr (STORE) {
-#pragma unroll
-            for (int j = 0; j < kPackRun; ++j) {
-                const uint32_t q = j * kBlock + threadIdx.x;
-                const uint64_t g = tb + q;
-                if (g < e1) keys[g] = s_k[q + q / kPackRun];
-            }
-            __syncthreads();
-        }
-    }
-    if (s_hlo[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], s_hlo[threadIdx.x]);
-    for (uint32_t i = threadIdx.x; i < (1u << (b.bb - 8)); i += kBlock)
-        if (s_hhi[i]) atomicAdd(&ghist[kRadix + i], s_hhi[i]);
-}
-
-// ---------------------------------------------------------------------------
 // Digit totals of the first bucket pass straight from the text: the bucket
 // depends on D (the first s dense digits, < sigma * 2^bb <= 2^26) only, so
 // each lane rolls D in 32 bits over 16 consecutive positions; an LDS
-// histogram of the low byte -> ghist[0..255] (the high bb - 8 bits are
+// histogram of the low kLoBits -> ghist[0 .. kLoRadix) (the high bits are
 // counted by the first pass itself, k_split_text).  Grid-stride over
 // 4096-position tiles.
 // ---------------------------------------------------------------------------
@@ -180,12 +93,12 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     constexpr int RUN = kTile / kBlock;   // 16
     __shared__ uint8_t s_map[256];
     __shared__ uint8_t s_dc[kTile + kMaxK];
-    __shared__ uint32_t s_hlo[kRadix];
+    __shared__ uint32_t s_hlo[kLoRadix];
     {
         const uint32_t cv = code[threadIdx.x];
         s_map[threadIdx.x] = (uint8_t)(cv ? cv - 1u : 0u);
     }
-    s_hlo[threadIdx.x] = 0;
+    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock) s_hlo[i] = 0;
     const uint32_t sig = b.sigma, ps1 = (uint32_t)b.pow_s1;
     const uint32_t shh = b.bsh;
     __syncthreads();
@@ -234,12 +147,13 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
             if (j > 0) D = (D - s_dc[l0 + j - 1] * ps1) * sig + s_dc[l0 + j - 1 + b.s];
             if (tb + l0 + j < n) {
                 const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> shh);
-                atomicAdd(&s_hlo[bk & 0xFFu], 1u);
+                atomicAdd(&s_hlo[bk & (kLoRadix - 1)], 1u);
             }
         }
         __syncthreads();
     }
-    if (s_hlo[threadIdx.x]) atomicAdd(&ghist[threadIdx.x], s_hlo[threadIdx.x]);
+    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock)
+        if (s_hlo[i]) atomicAdd(&ghist[i], s_hlo[i]);
 }
 
 // ---------------------------------------------------------------------------

@@ -95,38 +95,45 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     }
     tm.end();
     add_bytes(st, SA_K_PACK, n);
-    const uint32_t hb = bp.bs.bb - 8;   // high-pass digit bits (8..10)
+    const uint32_t hb = bp.bs.bb - kLoBits;   // second-pass digit bits (7..10)
+    // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
+    // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
+    // low, [kLoRadix, +2^hb) high
+    uint32_t* const g_lo = os_ghist(c);
+    uint32_t* const g_hi = os_ghist(c) + kLoRadix;
+    uint32_t* const cursor = os_ghist(c) + 5 * kRadix;
     tm.begin(SA_K_SCAN);
-    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c), (uint32_t)kRadix,
-                       os_base(c));
+    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_lo, kLoRadix, os_base(c));
     tm.end();
-    // two passes over the bucket: its low byte (any order within a digit),
-    // then its high bb - 8 bits, keeping the low byte's order (text order ->
-    // bucket order; sa_split.h)
+    // two passes over the bucket: its low kLoBits (any order within a
+    // digit), then its high hb bits, keeping the low digit's order (text
+    // order -> bucket order; sa_split.h)
     tm.begin(SA_K_SCATTER_FIRST);
     {
         const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
         hipLaunchKernelGGL(k_split_text, dim3(grid), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
-                           (const uint32_t*)os_base(c), os_tickets(c), c->keys[0], c->vals_alt, os_ghist(c) + kRadix,
-                           os_ghist(c) + 5 * kRadix);
+                           (const uint32_t*)os_base(c), os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_FIRST, 13 * n);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
-    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)os_ghist(c) + kRadix, 1u << hb,
-                       os_base(c) + kRadix);
+    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
+                       os_base(c) + kLoRadix);
     tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
         uint32_t* tk = os_tickets(c) + 1;
-        if (hb == 8)
-            split_pass<SrcBucketKeys, 8, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
-        else if (hb == 9)
-            split_pass<SrcBucketKeys, 9, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
-        else
-            split_pass<SrcBucketKeys, 10, true>(c, sb, n, 8, 0, 255, os_base(c) + kRadix, tk, c->keys_u, c->vals_u, s);
+        const uint32_t* hbase = os_base(c) + kLoRadix;
+        const uint32_t lm = kLoRadix - 1;
+        switch (hb) {
+            case 7: split_pass<SrcBucketKeys, 7, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            case 8: split_pass<SrcBucketKeys, 8, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            case 9: split_pass<SrcBucketKeys, 9, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            default:
+                split_pass<SrcBucketKeys, 10, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s);
+        }
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);

@@ -335,11 +335,11 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 }
 
 // ---------------------------------------------------------------------------
-// The first bucket pass straight from the text (replaces k_pack_bucket +
-// k_split<SrcBucketIota>): each lane computes key1 of 8 consecutive
-// positions (Horner for the first, rolling updates of D and of the
-// remainder for the rest, as k_pack_bucket) from dense digits staged in LDS,
-// and the pair (key1, position) is scattered by the bucket's low byte.  The
+// The first bucket pass straight from the text (no key1 round trip through
+// HBM): each lane computes key1 of 8 consecutive positions (Horner for the
+// first, rolling updates of D and of the remainder for the rest) from dense
+// digits staged in LDS,
+// and the pair (key1, position) is scattered by the bucket's low kLoBits.  The
 // order within a digit is arbitrary (LDS atomics), so the lane -> position
 // mapping is free, and so is the order of the tiles within a digit: each
 // tile claims its place from a per-digit cursor (no look-back).  The digit
@@ -352,13 +352,13 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
                                                          uint32_t* __restrict__ out_vals,
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
-    constexpr int RADIX = kRadix;
+    constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int ITEMS = kSpItems;
     constexpr int kHalo = kMaxK;   // >= K - 1 bytes past the tile
     __shared__ uint64_t s_keys[kSpTile];
     __shared__ uint16_t s_idx[kSpTile];
-    __shared__ uint8_t s_dig[kSpTile];
+    __shared__ uint16_t s_dig[kSpTile];
     __shared__ uint8_t s_dc[kSpTile + kHalo];
     __shared__ uint8_t s_map[256];
     __shared__ uint32_t s_cnt[RADIX];
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (bucket >> 8)
+    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (bucket >> kLoBits)
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -376,8 +376,8 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     if (dg < 256u) {
         const uint32_t cv = code[dg];
         s_map[dg] = (uint8_t)(cv ? cv - 1u : 0u);
-        s_cnt[dg] = 0;
     }
+    if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
     __syncthreads();
     uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
@@ -455,9 +455,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const bool ok = l0 + j < valid;
                 const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
-                const uint32_t d = ok ? (bk & 0xFFu) : (uint32_t)RADIX;
+                const uint32_t d = ok ? (bk & (RADIX - 1)) : (uint32_t)RADIX;
                 dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
-                if (ok) atomicAdd(&s_hhi[bk >> 8], 1u);
+                if (ok) atomicAdd(&s_hhi[bk >> kLoBits], 1u);
             }
         }
         __syncthreads();
@@ -492,7 +492,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
                 s_keys[pos] = k[j];
                 s_idx[pos] = (uint16_t)(8 * dg + j);
-                s_dig[pos] = (uint8_t)d;
+                s_dig[pos] = (uint16_t)d;
             }
         }
         __syncthreads();
