@@ -494,14 +494,7 @@ int main(int argc, char** argv) {
         hipLaunchKernelGGL((k_split<SrcKeys, 9, false>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0, SrcKeys{k1, v1}, n,
                            28u, shift, 255u, (const uint32_t*)(base + 1024), states, tick, epoch, k2, v2, err);
     };
-    auto passB1 = [&] {
-        CK(hipMemsetAsync(tick, 0, 4));
-        ++epoch;
-        hipLaunchKernelGGL((k_split<SrcKeys, 9, true, false>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0, SrcKeys{k1, v1}, n,
-                           28u, shift, 255u, (const uint32_t*)(base + 1024), states, tick, epoch, k2, v2, err);
-    };
     report("k_split B 9 bits unstable", timeit(passB0), 0);
-    report("k_split B 9 bits stable no fallback", timeit(passB1), 0);
     const double msb = timeit(passB);
     {
         unsigned long long h[2] = {0, 0};
@@ -512,6 +505,27 @@ int main(int argc, char** argv) {
         std::printf("%-34s %8.3f ms %7.1f GB/s  unsorted(17 bits)=%llu sum=%016llx\n", "k_split B 9 bits stable", msb,
                     24.0 * n / msb / 1e6, h[0], h[1]);
     }
+#define RUNI(RB, ST, IT)                                                                                      \
+    do {                                                                                                      \
+        auto f = [&] {                                                                                        \
+            CK(hipMemsetAsync(tick, 0, 4));                                                                   \
+            ++epoch;                                                                                          \
+            if (RB == 8)                                                                                      \
+                hipLaunchKernelGGL((k_split<SrcKeys, 8, ST, false, IT>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0, \
+                                   SrcKeys{k0, v0}, n, shift, 0u, 0u, (const uint32_t*)base, states, tick, epoch, k1, v1, err); \
+            else                                                                                              \
+                hipLaunchKernelGGL((k_split<SrcKeys, 9, ST, false, IT>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0, \
+                                   SrcKeys{k1, v1}, n, 28u, shift, 255u, (const uint32_t*)(base + 1024), states, tick, \
+                                   epoch, k2, v2, err);                                                       \
+        };                                                                                                    \
+        report("k_split bits" #RB " stable" #ST " items " #IT, timeit(f), 0);                                   \
+    } while (0)
+    RUNI(8, false, 8);
+    RUNI(8, false, 10);
+    RUNI(8, false, 12);
+    RUNI(9, true, 8);
+    RUNI(9, true, 10);
+    RUNI(9, true, 12);
     auto phases = [&](const char* name, auto launch) {
         CK(hipMemset(err, 0, 256));
         launch();
@@ -532,13 +546,13 @@ int main(int argc, char** argv) {
     phases("A", [&] {
         CK(hipMemsetAsync(tick, 0, 4));
         ++epoch;
-        hipLaunchKernelGGL((k_split<SrcKeys, 8, false, true, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
+        hipLaunchKernelGGL((k_split<SrcKeys, 8, false, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
                            SrcKeys{k0, v0}, n, shift, 0u, 0u, (const uint32_t*)base, states, tick, epoch, k1, v1, err);
     });
     phases("B", [&] {
         CK(hipMemsetAsync(tick, 0, 4));
         ++epoch;
-        hipLaunchKernelGGL((k_split<SrcKeys, 9, true, true, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
+        hipLaunchKernelGGL((k_split<SrcKeys, 9, true, true>), dim3((uint32_t)cus), dim3(kSpBlock), 0, 0,
                            SrcKeys{k1, v1}, n, 28u, shift, 255u, (const uint32_t*)(base + 1024), states, tick, epoch, k2,
                            v2, err);
     });

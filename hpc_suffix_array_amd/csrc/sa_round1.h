@@ -60,14 +60,14 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
 }
 
 // one persistent single-pass scatter (sa_split.h): one workgroup per CU
-template <class Src, int RBITS, bool STABLE>
+template <class Src, int RBITS, bool STABLE, int ITEMS = kSpItems>
 static void split_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t lshift, uint32_t lmask,
                        const uint32_t* base, uint32_t* ticket, uint64_t* out_keys, uint32_t* out_vals, hipStream_t s) {
     const uint32_t epoch = next_epoch(c, s);
-    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint64_t tiles = (n + (uint64_t)kSpBlock * ITEMS - 1) / ((uint64_t)kSpBlock * ITEMS);
     const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
-    hipLaunchKernelGGL((k_split<Src, RBITS, STABLE>), dim3(grid), dim3(kSpBlock), 0, s, src, n, shift, lshift, lmask,
-                       base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
+    hipLaunchKernelGGL((k_split<Src, RBITS, STABLE, false, ITEMS>), dim3(grid), dim3(kSpBlock), 0, s, src, n,
+                       shift, lshift, lmask, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
 }
 
 // *done: the SA and keys[0] hold the sorted first round.  *fused: the
@@ -123,16 +123,19 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
+        // 12288-pair tiles (1024 x 12): fewer look-backs and longer digit
+        // runs than 8192 (-10 % at 2^30 in microbench_radix)
+        constexpr int kSpItemsB = 12;
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
         const uint32_t lm = kLoRadix - 1;
         switch (hb) {
-            case 7: split_pass<SrcBucketKeys, 7, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
-            case 8: split_pass<SrcBucketKeys, 8, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
-            case 9: split_pass<SrcBucketKeys, 9, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            case 7: split_pass<SrcBucketKeys, 7, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            case 8: split_pass<SrcBucketKeys, 8, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
+            case 9: split_pass<SrcBucketKeys, 9, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
             default:
-                split_pass<SrcBucketKeys, 10, true>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s);
+                split_pass<SrcBucketKeys, 10, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s);
         }
     }
     tm.end();

@@ -29,7 +29,6 @@ constexpr int kSpBlock = 1024;
 constexpr int kSpItems = 8;
 constexpr int kSpTile = kSpBlock * kSpItems;   // 8192 pairs
 constexpr int kSpWaves = kSpBlock / kWave;
-constexpr uint32_t kSpMaxRounds = 4;           // previous-digit values ranked one at a time
 
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t x) {
 #pragma unroll
@@ -97,7 +96,7 @@ __device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states,
 // equal digit keep the order of their previous-pass digit
 // src.digit(key, lshift, lmask) (the input is ordered by it); otherwise their
 // order is arbitrary.
-template <class Src, int RBITS, bool STABLE, bool FALLBACK = true, bool PROF = false>
+template <class Src, int RBITS, bool STABLE, bool PROF = false, int ITEMS = kSpItems>
 __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_t shift, uint32_t lshift,
                                                     uint32_t lmask, const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
@@ -105,29 +104,27 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
                                                     uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
-    constexpr int WTILE = kWave * kSpItems;
-    constexpr int ITEMS = kSpItems;
+    constexpr int WTILE = kWave * ITEMS;
+    constexpr int TILE = kSpBlock * ITEMS;
+    static_assert(TILE <= 16384, "ranks in 14 bits, run starts in 16");
     static_assert(kSpBlock >= RADIX, "one thread per digit");
-    static_assert(kSpWaves * RADIX * 2 <= kSpTile * 8, "ballot wave counts alias the key stage");
-    __shared__ uint64_t s_keys[kSpTile];
-    __shared__ uint32_t s_vals[kSpTile];
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_vals[TILE];
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_lo[2];   // STABLE: min / max previous digit of the tile
-    uint16_t(*s_wcnt)[RADIX] = reinterpret_cast<uint16_t(*)[RADIX]>(s_keys);
+    __shared__ uint32_t s_nx[3];   // STABLE: the next previous-digit value to rank (rotating)
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint32_t mask = RADIX - 1;
-    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
     if (dg == 0) {
         s_tile[0] = atomicAdd(ticket, 1u);
-        s_lo[0] = ~0u;
-        s_lo[1] = 0u;
+        s_nx[0] = s_nx[1] = s_nx[2] = ~0u;
     }
     if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
     __syncthreads();
@@ -138,8 +135,8 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
     // (tile numbers come through LDS: readfirstlane keeps the tile base in
     // scalar registers, so each load is a scalar base + 32-bit lane offset)
     auto load = [&](uint64_t tt, uint64_t* kk, uint32_t* vv) {
-        const uint64_t tb = tt * kSpTile;
-        const uint32_t last = (uint32_t)min(n - 1 - tb, (uint64_t)(kSpTile - 1));
+        const uint64_t tb = tt * TILE;
+        const uint32_t last = (uint32_t)min(n - 1 - tb, (uint64_t)(TILE - 1));
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t le = wave * WTILE + j * kWave + lane;
@@ -162,9 +159,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         }
     };
     while (t < tiles) {
-        const uint64_t tb = t * kSpTile;
-        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)kSpTile ? (n - tb) : (uint64_t)kSpTile);
-        // dr[j] = digit << 16 | rank in the tile's digit run (< 2^13; digit RADIX: no pair)
+        const uint64_t tb = t * TILE;
+        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+        // dr[j] = digit << 16 | rank in the tile's digit run (< 2^14; digit RADIX: no pair)
         uint32_t dr[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
@@ -177,79 +174,31 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
                 if ((dr[j] >> 16) < (uint32_t)RADIX) dr[j] |= atomicAdd(&s_cnt[dr[j] >> 16], 1u);
             __syncthreads();
         } else {
-            uint32_t lmin = ~0u, lmax = 0u;
-#pragma unroll
-            for (int j = 0; j < ITEMS; ++j) {
-                if ((dr[j] >> 16) < (uint32_t)RADIX) {
-                    const uint32_t l = src_digit(src, k[j], lshift, lmask, 0);
-                    lmin = min(lmin, l);
-                    lmax = max(lmax, l);
-                }
-            }
-            lmin = wave_min_u32(lmin);
-            lmax = wave_max_u32(lmax);
-            if (lane == 0 && lmin <= lmax) {
-                atomicMin(&s_lo[0], lmin);
-                atomicMax(&s_lo[1], lmax);
-            }
-            __syncthreads();
-            const uint32_t l0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_lo[0]);
-            const uint32_t span = (uint32_t)__builtin_amdgcn_readfirstlane((int)(s_lo[1] - s_lo[0]));
-            if (!FALLBACK || span < kSpMaxRounds) {
-                // one previous-digit value per round: all pairs of value l
-                // take their ranks before any pair of value l + 1 (dr bits
-                // 13..15 hold l - l0 meanwhile)
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j)
-                    dr[j] |= ((src_digit(src, k[j], lshift, lmask, 0) - l0) & 7u) << 13;
-                for (uint32_t m = 0; m <= span; ++m) {
-#pragma unroll
-                    for (int j = 0; j < ITEMS; ++j) {
-                        if ((dr[j] >> 16) < (uint32_t)RADIX && ((dr[j] >> 13) & 7u) == m)
-                            dr[j] |= atomicAdd(&s_cnt[dr[j] >> 16], 1u);
-                    }
-                    __syncthreads();
-                }
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j) dr[j] &= ~(7u << 13);
-            } else {
-                // stable ballots (match-any per wave), wave counts in the key stage
-                for (int i = dg; i < kSpWaves * RADIX; i += kSpBlock) (&s_wcnt[0][0])[i] = 0;
-                __syncthreads();
-                uint16_t* wc = s_wcnt[wave];
+            // ranks in rounds, one previous-digit value per round, in
+            // increasing order and only the values present in the tile: all
+            // pairs of value l take their ranks before any pair of a larger
+            // value.  Round r also finds the next value (its minimum over the
+            // block lands in s_nx[r % 3]; thread 0 clears the slot round r + 1
+            // will use, last read before round r - 1's barrier).  Round 0 only
+            // finds the smallest value.  A tile of bucket-ordered input holds
+            // one or two values, so typically two or three rounds.
+            uint32_t cur = ~0u;
+            for (uint32_t r = 0;; ++r) {
+                uint32_t nx = ~0u;
 #pragma unroll
                 for (int j = 0; j < ITEMS; ++j) {
-                    const uint32_t d = dr[j] >> 16;
-                    const bool ok = d < (uint32_t)RADIX;
-                    uint64_t peers = __ballot(ok);
-#pragma unroll
-                    for (int b = 0; b < RBITS; ++b) {
-                        const bool bit = (d >> b) & 1u;
-                        const uint64_t bal = __ballot(bit);
-                        peers &= bit ? bal : ~bal;
+                    if ((dr[j] >> 16) < (uint32_t)RADIX) {
+                        const uint32_t l = src_digit(src, k[j], lshift, lmask, 0);
+                        if (l == cur) dr[j] |= atomicAdd(&s_cnt[dr[j] >> 16], 1u);
+                        else if ((cur == ~0u || l > cur) && l < nx) nx = l;
                     }
-                    uint32_t cnt = 0;
-                    if (ok) cnt = wc[d];
-                    const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
-                    dr[j] |= cnt + below;
-                    if (ok && below == 0) wc[d] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
                 }
+                nx = wave_min_u32(nx);
+                if (lane == 0 && nx != ~0u) atomicMin(&s_nx[r % 3], nx);
+                if (dg == 0) s_nx[(r + 1) % 3] = ~0u;
                 __syncthreads();
-                if (dg < (uint32_t)RADIX) {
-                    uint32_t tot = 0;
-#pragma unroll
-                    for (int w = 0; w < kSpWaves; ++w) {
-                        const uint32_t x = s_wcnt[w][dg];
-                        s_wcnt[w][dg] = (uint16_t)tot;
-                        tot += x;
-                    }
-                    s_cnt[dg] = tot;
-                }
-                __syncthreads();
-#pragma unroll
-                for (int j = 0; j < ITEMS; ++j)
-                    if ((dr[j] >> 16) < (uint32_t)RADIX) dr[j] += s_wcnt[wave][dr[j] >> 16];
-                __syncthreads();
+                cur = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_nx[r % 3]);
+                if (cur == ~0u) break;
             }
         }
         stamp(0);
@@ -257,10 +206,6 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
             st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
-        }
-        if (STABLE && dg == 0) {
-            s_lo[0] = ~0u;
-            s_lo[1] = 0u;
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
@@ -293,13 +238,14 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
-                const uint32_t pos = s_start[d] + (dr[j] & 0x1FFFu);
+                const uint32_t pos = s_start[d] + (dr[j] & 0x3FFFu);
                 s_keys[pos] = k[j];
                 s_vals[pos] = v[j];
             }
         }
         __syncthreads();
         if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;   // the next tile's atomics come after the next barrier
+        if (STABLE && dg < 3u) s_nx[dg] = ~0u;
         stamp(3);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
