@@ -282,16 +282,18 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 
 // ---------------------------------------------------------------------------
 // The first bucket pass straight from the text (no key1 round trip through
-// HBM): each lane computes key1 of 8 consecutive positions (Horner for the
-// first, rolling updates of D and of the remainder for the rest) from dense
-// digits staged in LDS,
-// and the pair (key1, position) is scattered by the bucket's low kLoBits.  The
-// order within a digit is arbitrary (LDS atomics), so the lane -> position
-// mapping is free, and so is the order of the tiles within a digit: each
-// tile claims its place from a per-digit cursor (no look-back).  The digit
-// totals come from k_bucket_hist.  The next tile's text (8 bytes per lane +
-// the K - 1 byte halo) is loaded while the current one is staged and written.
+// HBM): each lane computes key1 of ITEMS consecutive positions (Horner for
+// the first, rolling updates of D and of the remainder for the rest) from
+// dense digits staged in LDS, and the pair (key1, position) is scattered by
+// the bucket's low kLoBits.  The order within a digit is arbitrary (LDS
+// atomics), so the lane -> position mapping is free, and so is the order of
+// the tiles within a digit: each tile claims its place from a per-digit
+// cursor (no look-back).  The digit totals come from k_bucket_hist; the
+// second pass's totals are counted here.  The next tile's text (the tile +
+// a K - 1 byte halo, as 32-bit words) is loaded while the current one is
+// staged and written.
 // ---------------------------------------------------------------------------
+template <int ITEMS>
 __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -300,12 +302,14 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
-    constexpr int ITEMS = kSpItems;
-    constexpr int kHalo = kMaxK;   // >= K - 1 bytes past the tile
-    __shared__ uint64_t s_keys[kSpTile];
-    __shared__ uint16_t s_idx[kSpTile];
-    __shared__ uint16_t s_dig[kSpTile];
-    __shared__ uint8_t s_dc[kSpTile + kHalo];
+    constexpr int TILE = kSpBlock * ITEMS;
+    constexpr int kHalo = kMaxK;                        // >= K - 1 bytes past the tile
+    constexpr int NW = (TILE + kHalo) / 4;              // staged text words
+    constexpr int WPT = (NW + kSpBlock - 1) / kSpBlock; // per lane
+    static_assert(TILE % 4 == 0 && kHalo % 4 == 0 && TILE <= 65535, "word staging, 16-bit tile offsets");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint16_t s_idx[TILE];
+    __shared__ uint32_t s_dcw[NW];                      // dense digits, 4 per word (0 past the end)
     __shared__ uint8_t s_map[256];
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
@@ -313,10 +317,11 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (bucket >> kLoBits)
+    const uint8_t* s_dc = reinterpret_cast<const uint8_t*>(s_dcw);
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
-    const uint64_t tiles = (n + kSpTile - 1) / kSpTile;
+    const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t K = b.s + b.R;
     s_hhi[dg] = 0;
     if (dg < 256u) {
@@ -327,62 +332,55 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
     __syncthreads();
     uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
-    // raw text: 8 bytes at tile offset 8 dg (dg < 1024), the halo at
-    // kSpTile + 8 (dg - 1024 ...) is loaded by lanes dg < kHalo / 8 as a
-    // second word; bytes at or past n are never read
-    auto load8 = [&](uint64_t pos) -> uint64_t {
-        if (pos + 8 <= n && (((uintptr_t)(text + pos)) & 7) == 0) return *reinterpret_cast<const uint64_t*>(text + pos);
-        uint64_t w = 0;
-        for (int q = 0; q < 8; ++q)
-            if (pos + q < n) w |= (uint64_t)text[pos + q] << (8 * q);
+    // raw text words dg, dg + 1024, ... of the tile + halo; bytes at or past
+    // n are never read
+    auto load4 = [&](uint64_t pos) -> uint32_t {
+        if (pos + 4 <= n && (((uintptr_t)(text + pos)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(text + pos);
+        uint32_t w = 0;
+        for (int q = 0; q < 4; ++q)
+            if (pos + q < n) w |= (uint32_t)text[pos + q] << (8 * q);
         return w;
     };
-    uint64_t raw = 0, rawh = 0;
+    uint32_t raw[WPT];
     auto load = [&](uint64_t tt) {
-        const uint64_t tb = tt * kSpTile;
-        raw = load8(tb + 8ull * dg);
-        if (dg < (uint32_t)(kHalo / 8)) rawh = load8(tb + kSpTile + 8ull * dg);
+        const uint64_t tb = tt * TILE;
+#pragma unroll
+        for (int i = 0; i < WPT; ++i) {
+            const uint32_t w = dg + i * kSpBlock;
+            raw[i] = w < (uint32_t)NW ? load4(tb + 4ull * w) : 0u;
+        }
     };
     if (t < tiles) load(t);
     uint32_t par = 0;
     while (t < tiles) {
-        const uint64_t tb = t * kSpTile;
-        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)kSpTile ? (n - tb) : (uint64_t)kSpTile);
+        const uint64_t tb = t * TILE;
+        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
         // dense digits (0 past the end)
-        {
-            uint32_t lo = 0, hi = 0;
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint64_t pos = tb + 8ull * dg + q;
-                const uint32_t x = pos < n ? s_map[(raw >> (8 * q)) & 0xFFu] : 0u;
-                if (q < 4) lo |= x << (8 * q);
-                else hi |= x << (8 * (q - 4));
-            }
-            *reinterpret_cast<uint2*>(s_dc + 8 * dg) = make_uint2(lo, hi);
-            if (dg < (uint32_t)(kHalo / 8)) {
-                lo = hi = 0;
+        for (int i = 0; i < WPT; ++i) {
+            const uint32_t w = dg + i * kSpBlock;
+            if (w < (uint32_t)NW) {
+                uint32_t o = 0;
 #pragma unroll
-                for (int q = 0; q < 8; ++q) {
-                    const uint64_t pos = tb + kSpTile + 8ull * dg + q;
-                    const uint32_t x = pos < n ? s_map[(rawh >> (8 * q)) & 0xFFu] : 0u;
-                    if (q < 4) lo |= x << (8 * q);
-                    else hi |= x << (8 * (q - 4));
+                for (int q = 0; q < 4; ++q) {
+                    const uint64_t pos = tb + 4ull * w + q;
+                    o |= (pos < n ? (uint32_t)s_map[(raw[i] >> (8 * q)) & 0xFFu] : 0u) << (8 * q);
                 }
-                *reinterpret_cast<uint2*>(s_dc + kSpTile + 8 * dg) = make_uint2(lo, hi);
+                s_dcw[w] = o;
             }
         }
         __syncthreads();
-        // key1 of positions tb + 8 dg + j (D < sigma * 2^bb <= 2^26 rolls in
-        // 32 bits; the remainder in 64)
+        // key1 of positions tb + ITEMS dg + j (D < sigma * 2^bb <= 2^26 rolls
+        // in 32 bits; the remainder in 64)
         uint64_t k[ITEMS];
         uint32_t dr[ITEMS];
         {
-            const uint32_t l0 = 8 * dg;
+            const uint32_t l0 = ITEMS * dg;
             uint32_t D = 0;
             uint64_t r = 0;
             for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
             for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
-            const bool interior = tb + kSpTile + K <= n;   // every suffix of the tile has >= K symbols
+            const bool interior = tb + TILE + K <= n;   // every suffix of the tile has >= K symbols
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 if (j > 0) {
@@ -437,8 +435,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
                 s_keys[pos] = k[j];
-                s_idx[pos] = (uint16_t)(8 * dg + j);
-                s_dig[pos] = (uint16_t)d;
+                s_idx[pos] = (uint16_t)(ITEMS * dg + j);
             }
         }
         __syncthreads();
@@ -446,10 +443,11 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t q = j * kSpBlock + dg;
             if (q < valid) {
-                const uint32_t dd = s_dig[q];
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh) & (RADIX - 1);
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
                 if (g < n) {
-                    out_keys[g] = s_keys[q];
+                    out_keys[g] = key;
                     out_vals[g] = (uint32_t)(tb + s_idx[q]);
                 }
             }
