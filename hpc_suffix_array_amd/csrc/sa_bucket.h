@@ -79,6 +79,25 @@ struct SrcBucketKeys {
     }
 };
 
+// NW consecutive bytes of an LDS byte array (viewed as words) starting at
+// byte `off` (any alignment), as NW / 4 words: one word read per output
+// word + 1, then v_alignbyte (the per-byte ds_read_u8 of a rolling update
+// cost more than its arithmetic)
+template <int NB>
+__device__ __forceinline__ void lds_bytes(const uint32_t* __restrict__ w32, uint32_t off, uint32_t (&out)[NB / 4]) {
+    static_assert(NB % 4 == 0, "whole words");
+    const uint32_t base = off >> 2, sh = off & 3u;
+    uint32_t w[NB / 4 + 1];
+#pragma unroll
+    for (int q = 0; q <= NB / 4; ++q) w[q] = w32[base + q];
+#pragma unroll
+    for (int q = 0; q < NB / 4; ++q) out[q] = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+}
+template <int NB>
+__device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) {
+    return (v[j >> 2] >> (8 * (j & 3))) & 0xFFu;
+}
+
 // ---------------------------------------------------------------------------
 // Digit totals of the first bucket pass straight from the text: the bucket
 // depends on D (the first s dense digits, < sigma * 2^bb <= 2^26) only, so
@@ -92,7 +111,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                                                         uint32_t* __restrict__ ghist) {
     constexpr int RUN = kTile / kBlock;   // 16
     __shared__ uint8_t s_map[256];
-    __shared__ uint8_t s_dc[kTile + kMaxK];
+    __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
+    uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
     __shared__ uint32_t s_hlo[kLoRadix];
     {
         const uint32_t cv = code[threadIdx.x];
@@ -142,9 +162,13 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
         for (uint32_t q = 0; q < b.s; ++q) D = D * sig + s_dc[l0 + q];
+        // the digits leaving (positions l0 .. l0 + 15) and entering (l0 + s ..)
+        uint32_t xo[RUN / 4], xi[RUN / 4];
+        lds_bytes<RUN>(s_dcw, l0, xo);
+        lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
 #pragma unroll
         for (int j = 0; j < RUN; ++j) {
-            if (j > 0) D = (D - s_dc[l0 + j - 1] * ps1) * sig + s_dc[l0 + j - 1 + b.s];
+            if (j > 0) D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
             if (tb + l0 + j < n) {
                 const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> shh);
                 atomicAdd(&s_hlo[bk & (kLoRadix - 1)], 1u);

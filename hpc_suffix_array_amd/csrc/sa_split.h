@@ -306,10 +306,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     constexpr int kHalo = kMaxK;                        // >= K - 1 bytes past the tile
     constexpr int NW = (TILE + kHalo) / 4;              // staged text words
     constexpr int WPT = (NW + kSpBlock - 1) / kSpBlock; // per lane
-    static_assert(TILE % 4 == 0 && kHalo % 4 == 0 && TILE <= 65535, "word staging, 16-bit tile offsets");
+    static_assert(ITEMS % 4 == 0 && kHalo % 4 == 0 && TILE <= 65535, "word staging, 16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint16_t s_idx[TILE];
-    __shared__ uint32_t s_dcw[NW];                      // dense digits, 4 per word (0 past the end)
+    __shared__ uint32_t s_dcw[NW + 8];                  // dense digits, 4 per word (0 past the end; + slack)
     __shared__ uint8_t s_map[256];
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
@@ -381,12 +381,18 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
             for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
             for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
             const bool interior = tb + TILE + K <= n;   // every suffix of the tile has >= K symbols
+            // the digits leaving D (l0 ..), moving from the remainder into D
+            // (l0 + s ..) and entering the remainder (l0 + K ..)
+            uint32_t xo[ITEMS / 4], xm[ITEMS / 4], xn[ITEMS / 4];
+            lds_bytes<ITEMS>(s_dcw, l0, xo);
+            lds_bytes<ITEMS>(s_dcw, l0 + b.s, xm);
+            lds_bytes<ITEMS>(s_dcw, l0 + K, xn);
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 if (j > 0) {
-                    const uint32_t xi = s_dc[l0 + j - 1 + b.s];
-                    D = (D - s_dc[l0 + j - 1] * (uint32_t)b.pow_s1) * b.sigma + xi;
-                    r = (r - (uint64_t)xi * b.powR1) * b.sigma + s_dc[l0 + j - 1 + K];
+                    const uint32_t xi = byte_at<ITEMS>(xm, j - 1);
+                    D = (D - byte_at<ITEMS>(xo, j - 1) * (uint32_t)b.pow_s1) * b.sigma + xi;
+                    r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
                 }
                 uint64_t low;
                 if (interior) {
