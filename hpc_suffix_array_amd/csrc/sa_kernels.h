@@ -561,12 +561,14 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
 // over the wave, one atomicOr per word per wave.
 __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__ text, uint64_t n,
                                                      uint32_t* __restrict__ present) {
-    uint32_t m[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    auto add = [&](uint32_t b) {
-        const uint32_t bit = 1u << (b & 31u), w = b >> 5;
+    // a private 256-bit mask per lane in LDS, set by one atomic OR per byte
+    // (no return value; a stride of 9 words keeps 32 lanes on 32 banks) --
+    // selecting the mask word in registers cost 8 compares per byte
+    __shared__ uint32_t s_m[kBlock * 9];
+    uint32_t* m = s_m + threadIdx.x * 9;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] |= (w == (uint32_t)i) ? bit : 0u;
-    };
+    for (int i = 0; i < 8; ++i) m[i] = 0;
+    auto add = [&](uint32_t b) { atomicOr(&m[b >> 5], 1u << (b & 31u)); };
     const uint64_t stride = (uint64_t)gridDim.x * kBlock * 16;
     for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16; i < n; i += stride) {
         if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
