@@ -21,7 +21,8 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcText>", "hist_text"),
+KINDS = [("k_split_text", "scatter_first"), ("k_split<sa::SrcBucketKeys", "scatter_keys"), ("k_bucket_hist", "pack"),
+         ("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcText>", "hist_text"),
          ("k_hist<sa::SrcU", "hist_u"), ("k_hist<sa::SrcKeys>", "hist_keys"),
          ("k_scan_rows", "scan"), ("k_scatter<sa::SrcRank>", "scatter_rank"),
          ("k_scatter<sa::SrcText>", "scatter_text"), ("k_scatter<sa::SrcU", "scatter_u"),
@@ -68,9 +69,11 @@ def main():
     def grid(row):
         return int(float(row.get("Grid_Size") or row.get("Grid_Size_X") or 0))
 
-    # per kind: all launches, and the full-size ones (largest grid of the
-    # kind: the launches over all n suffixes, not the small unsorted-set ones)
-    per = defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "full": defaultdict(list)})
+    # per kind: all launches, and the full-size ones: those within 4x of the
+    # kind's longest (the launches over all n suffixes, not the small
+    # unsorted-set ones; persistent kernels have equal grids for both, so the
+    # grid size cannot tell them apart)
+    per = defaultdict(lambda: {"calls": 0, "total_ns": 0.0, "all": []})
     if trace_csv:
         with open(trace_csv) as f:
             for row in csv.DictReader(f):
@@ -79,7 +82,7 @@ def main():
                     d = float(row["End_Timestamp"]) - float(row["Start_Timestamp"])
                     per[k]["calls"] += 1
                     per[k]["total_ns"] += d
-                    per[k]["full"][grid(row)].append(d)
+                    per[k]["all"].append(d)
     pmc = {}
     for name, sub in (("FETCH_SIZE", "fetch"), ("WRITE_SIZE", "write")):
         c = find(os.path.join(out, sub), "counter_collection.csv")
@@ -91,8 +94,15 @@ def main():
                         continue
                     k = kind_of(row.get("Kernel_Name", ""))
                     if k:
-                        acc[k][grid(row)].append(float(row["Counter_Value"]) * 1024.0)   # KiB -> bytes
-        pmc[name] = {k: sum(v[max(v)]) / len(v[max(v)]) for k, v in acc.items() if v}
+                        acc[k][(row.get("Dispatch_Id") or row.get("Correlation_Id") or len(acc[k]))].append(
+                            float(row["Counter_Value"]) * 1024.0)   # KiB -> bytes, summed over the dispatch's rows
+        big = {}
+        for k, v in acc.items():
+            tot = [sum(x) for x in v.values()]
+            if tot:
+                full = [x for x in tot if x >= 0.25 * max(tot)]
+                big[k] = sum(full) / len(full)
+        pmc[name] = big
     fetch, write = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
     # calibration: k_alphabet reads exactly n text bytes (16 B per lane)
     read_factor = None
@@ -100,7 +110,7 @@ def main():
         read_factor = 1.0 * n / fetch["alphabet"]
     kernels = {}
     for k, v in per.items():
-        full = v["full"][max(v["full"])]
+        full = [d for d in v["all"] if d >= 0.25 * max(v["all"])]
         e = {"calls": v["calls"], "avg_ms": v["total_ns"] / max(v["calls"], 1) / 1e6,
              "total_ms": v["total_ns"] / 1e6, "full_size_calls": len(full),
              "full_size_avg_ms": sum(full) / len(full) / 1e6}
