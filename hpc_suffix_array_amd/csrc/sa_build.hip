@@ -105,6 +105,7 @@ struct sa_context {
     uint32_t* u_g[2] = {nullptr, nullptr};
     uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
     uint32_t* os = nullptr;                     // onesweep ghist / digit bases / tickets
+    uint32_t* segw = nullptr;                   // second bucket pass: per-segment cursors / bases / flags
     uint64_t* states = nullptr;                 // onesweep tile states [tiles][256]
     uint32_t epoch = 0;                         // onesweep state tag of the last pass
     int radix = 0;                              // 0 onesweep, 1 reduce-then-scan
@@ -954,6 +955,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
+        hipMalloc(&c->segw, segw_words(1024) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);
@@ -985,6 +987,7 @@ void sa_context_destroy(sa_context* c) {
     hipFree(c->alpha);
     hipFree(c->code);
     hipFree(c->os);
+    hipFree(c->segw);
     hipFree(c->hist);
     hipFree(c->totals);
     hipFree(c->counts);

@@ -133,19 +133,27 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
-        // 12288-pair tiles (1024 x 12): fewer look-backs and longer digit
-        // runs than 8192 (-10 % at 2^30 in microbench_radix)
-        constexpr int kSpItemsB = 12;
+        // 12288-pair units cut at the first pass's digit boundaries, places
+        // claimed per (low digit, high digit) by atomic cursors (sa_split.h)
+        constexpr int kItemsB = 12;
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
-        const uint32_t lm = kLoRadix - 1;
+        SA_HIP(hipMemsetAsync(c->segw, 0, segw_words(1u << hb) * 4, s));   // <= 3 MiB
+        const uint64_t units = (n + kSpBlock * kItemsB - 1) / (kSpBlock * kItemsB) + kSegs;
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)c->cus));
         switch (hb) {
-            case 7: split_pass<SrcBucketKeys, 7, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
-            case 8: split_pass<SrcBucketKeys, 8, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
-            case 9: split_pass<SrcBucketKeys, 9, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s); break;
-            default:
-                split_pass<SrcBucketKeys, 10, true, kSpItemsB>(c, sb, n, kLoBits, 0, lm, hbase, tk, c->keys_u, c->vals_u, s);
+#define SA_SEG_PASS(B)                                                                                        \
+    case B:                                                                                                   \
+        hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, n, kLoBits, \
+                           (const uint32_t*)os_base(c), hbase, c->segw, tk, c->keys_u, c->vals_u, c->words + 4); \
+        break;
+            SA_SEG_PASS(7)
+            SA_SEG_PASS(8)
+            SA_SEG_PASS(9)
+            SA_SEG_PASS(10)
+#undef SA_SEG_PASS
+            default: return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
         }
     }
     tm.end();

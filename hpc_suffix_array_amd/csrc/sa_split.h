@@ -465,4 +465,219 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     if (s_hhi[dg]) atomicAdd(&ghist_hi[dg], s_hhi[dg]);
 }
 
+// ---------------------------------------------------------------------------
+// The second bucket pass without a look-back.  Its input is ordered by the
+// first pass's digit l (the bucket's low kLoBits): segment l of the input is
+// [lo_base[l], lo_base[l + 1]).  The pass must keep l's order only, and
+// within a segment all pairs share l, so work units never straddle segments
+// (the tile grid is cut at segment boundaries) and a unit of segment l
+// claims its place per high digit h from a per-(l, h) atomic cursor.  Where
+// segment l starts inside digit h -- base(h, l) = base(h) + the count of h
+// in segments < l -- is published by the last unit of segment l - 1 to
+// claim (done[l - 1] counts claims) once base(h, l - 1) is known: a chain of
+// one hop per segment (256 per pass) instead of a look-back per tile.  A
+// unit waits only for base(., l); claims never wait, so the chain always
+// advances.  No fences (a device-scope release writes back the L2: 10x
+// slower): a claim's atomic has returned before its unit counts itself
+// done, and base words carry their own ready bit (bit 32).
+// segw (zeroed before the pass): cur u32[256][RADIX] | base u64[256][RADIX]
+// | done u32[256].
+// ---------------------------------------------------------------------------
+constexpr uint32_t kSegs = kLoRadix;
+constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; }
+
+template <class Src, int RBITS, int ITEMS>
+__global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uint32_t shift,
+                                                        const uint32_t* __restrict__ lo_base,
+                                                        const uint32_t* __restrict__ digit_base,
+                                                        uint32_t* __restrict__ segw, uint32_t* __restrict__ ticket,
+                                                        uint64_t* __restrict__ out_keys,
+                                                        uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
+    constexpr int RADIX = 1 << RBITS;
+    constexpr int RWAVES = RADIX / kWave;
+    constexpr int WTILE = kWave * ITEMS;
+    constexpr int TILE = kSpBlock * ITEMS;
+    static_assert(kSpBlock >= RADIX && (int)kSegs <= kSpBlock, "one thread per digit / segment");
+    static_assert(TILE <= 65535, "16-bit tile offsets");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_vals[TILE];
+    __shared__ uint32_t s_cnt[RADIX];
+    __shared__ uint16_t s_start[RADIX];
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[kSpWaves];
+    __shared__ uint32_t s_ubase[kSegs + 1];   // units before segment l (exclusive scan)
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_last;
+    __shared__ uint32_t s_claim[RADIX];
+    uint32_t* const cur = segw;
+    uint64_t* const sbase = reinterpret_cast<uint64_t*>(segw + (uint64_t)kSegs * RADIX);
+    uint32_t* const done = segw + 3ull * kSegs * RADIX;
+    constexpr uint64_t kReady = 1ull << 32;
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint32_t mask = RADIX - 1;
+    auto seg_lo = [&](uint32_t l) -> uint64_t { return lo_base[l]; };
+    auto seg_hi = [&](uint32_t l) -> uint64_t { return l + 1 < kSegs ? (uint64_t)lo_base[l + 1] : n; };
+    auto units_of = [&](uint32_t l) -> uint32_t { return (uint32_t)((seg_hi(l) - seg_lo(l) + TILE - 1) / TILE); };
+    // unit numbering: segment by segment
+    {
+        const uint32_t x = dg < kSegs ? units_of(dg) : 0u;
+        const uint32_t inc = wave_inclusive_sum(x);
+        if (lane == kWave - 1) s_tmp[wave] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+        for (uint32_t w = 0; w < wave; ++w) off += s_tmp[w];
+        if (dg < kSegs) s_ubase[dg] = off + inc - x;
+        if (dg == kSegs - 1) s_ubase[kSegs] = off + inc;
+    }
+    if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
+    if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const uint32_t units = s_ubase[kSegs];
+    // unit -> (segment, first position, size)
+    auto locate = [&](uint32_t u, uint32_t& l, uint64_t& tb, uint32_t& valid) {
+        uint32_t a = 0, b = kSegs;   // last l with s_ubase[l] <= u (units of empty segments are skipped)
+        while (b - a > 1) {
+            const uint32_t mid = (a + b) / 2;
+            if (s_ubase[mid] <= u) a = mid;
+            else b = mid;
+        }
+        l = a;
+        tb = seg_lo(a) + (uint64_t)(u - s_ubase[a]) * TILE;
+        const uint64_t e = seg_hi(a);
+        valid = (uint32_t)(e - tb < (uint64_t)TILE ? e - tb : (uint64_t)TILE);
+    };
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    auto load = [&](uint64_t tb, uint32_t valid, uint64_t* kk, uint32_t* vv) {
+        const uint32_t last = valid - 1;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const uint64_t e = tb + (le < last ? le : last);
+            kk[j] = src.key(e);
+            vv[j] = src.val(e);
+        }
+    };
+    uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint32_t l = 0, valid = 0;
+    uint64_t tb = 0;
+    if (u < units) {
+        locate(u, l, tb, valid);
+        load(tb, valid, k, v);
+    }
+    uint32_t par = 0;
+    while (u < units) {
+        // ranks within the unit (any order: one segment, one value of l)
+        uint32_t dr[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const uint32_t d = le < valid ? src_digit(src, k[j], shift, mask, 0) : (uint32_t)RADIX;
+            dr[j] = (d << 16) | (d < (uint32_t)RADIX ? atomicAdd(&s_cnt[d], 1u) : 0u);
+        }
+        __syncthreads();
+        // claim this unit's place in (l, h); count the claim for segment l
+        // (the claim's return value is stored first: it has been performed)
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)RADIX) {
+            tile_cnt = s_cnt[dg];
+            s_claim[dg] = tile_cnt ? atomicAdd(&cur[(uint64_t)l * RADIX + dg], tile_cnt) : 0u;
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        if (dg == 0) s_last = atomicAdd(&done[l], 1u) == units_of(l) - 1 ? 1u : 0u;
+        // base(h, l): digit_base when every earlier segment is empty, else
+        // published (with its ready bit) by segment l - 1's last claimer
+        if (dg < (uint32_t)RADIX) {
+            uint32_t bh;
+            if (seg_lo(l) == 0) {
+                bh = digit_base[dg];
+            } else {
+                uint64_t w;
+                uint32_t spins = 0;
+                while (((w = __hip_atomic_load(&sbase[(uint64_t)l * RADIX + dg], __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)) & kReady) == 0) {
+                    if (++spins > kSpinLimit) {
+                        atomicOr(err, 1u);
+                        break;
+                    }
+                    __builtin_amdgcn_s_sleep(1);
+                }
+                bh = (uint32_t)w;
+            }
+            s_gofs[dg] = bh + s_claim[dg];
+            s_claim[dg] = bh;
+        }
+        __syncthreads();
+        if (s_last) {
+            // every claim of segment l has been performed: publish base(., l')
+            // for the next segment and the empty ones after it
+            if (dg < (uint32_t)RADIX) {
+                const uint32_t tot = __hip_atomic_load(&cur[(uint64_t)l * RADIX + dg], __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+                for (uint32_t l2 = l + 1; l2 < kSegs; ++l2) {
+                    __hip_atomic_store(&sbase[(uint64_t)l2 * RADIX + dg], kReady | (uint64_t)(s_claim[dg] + tot),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (seg_hi(l2) > seg_lo(l2)) break;
+                }
+            }
+        }
+        // the next unit's ticket and loads (see k_split)
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint32_t un = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        uint32_t ln = l, validn = valid;
+        uint64_t tbn = tb;
+        if (un < units) locate(un, ln, tbn, validn);
+        uint64_t kn[ITEMS];
+        uint32_t vn[ITEMS];
+        load(tbn, validn, kn, vn);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t d = dr[j] >> 16;
+            if (d < (uint32_t)RADIX) {
+                const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
+                s_keys[pos] = k[j];
+                s_vals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+        if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * kSpBlock + dg;
+            if (q < valid) {
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = src_digit(src, key, shift, mask, 0);
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < n) {
+                    out_keys[g] = key;
+                    out_vals[g] = s_vals[q];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            k[j] = kn[j];
+            v[j] = vn[j];
+        }
+        u = un;
+        l = ln;
+        tb = tbn;
+        valid = validn;
+        par ^= 1u;
+    }
+}
+
 }  // namespace sa
