@@ -59,17 +59,6 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     return false;
 }
 
-// one persistent single-pass scatter (sa_split.h): one workgroup per CU
-template <class Src, int RBITS, bool STABLE, int ITEMS = kSpItems>
-static void split_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t lshift, uint32_t lmask,
-                       const uint32_t* base, uint32_t* ticket, uint64_t* out_keys, uint32_t* out_vals, hipStream_t s) {
-    const uint32_t epoch = next_epoch(c, s);
-    const uint64_t tiles = (n + (uint64_t)kSpBlock * ITEMS - 1) / ((uint64_t)kSpBlock * ITEMS);
-    const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
-    hipLaunchKernelGGL((k_split<Src, RBITS, STABLE, false, ITEMS>), dim3(grid), dim3(kSpBlock), 0, s, src, n,
-                       shift, lshift, lmask, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
-}
-
 // *done: the SA and keys[0] hold the sorted first round.  *fused: the
 // round-1 segments were produced with it (few unsorted suffixes): rank[] for
 // the unsorted set only (member bitmap), the unsorted set compacted in
