@@ -88,3 +88,26 @@ def test_cli_and_shim_on_gpu(gpu, oracle, tmp_path):
     import pandas as pd
     df = pd.read_csv(out)
     assert list(df.columns) == B.CSV_COLUMNS and len(df) == 3
+
+
+def test_scaling_harness_columns_and_commands():
+    """scripts/benchmark_scaling.py: the mpi_results.csv columns of the
+    reference's sweep (benchmark_mpi.py:180-210) from bench.py JSON lines, and
+    the torch.distributed.run launch of N > 1 on 127.0.0.1."""
+    import benchmark_scaling as S
+
+    class A:
+        steps, warmup, n, kind, no_cpu_baseline = 3, 1, 4096, "dna", False
+    one = S.command(1, A, 29500)
+    two = S.command(2, A, 29501)
+    assert one[1].endswith("bench.py") and "--no-cpu-baseline" not in one
+    assert "torch.distributed.run" in two and "--master-addr" in two and "127.0.0.1" in two
+    assert "--no-cpu-baseline" in two and two[two.index("--gpus") + 1] == "2"
+    res = [(1, {"ms_per_step": 40.0, "value": 2.5e10, "cpu_baseline": {"value": 1e7}}),
+           (2, {"ms_per_step": 25.0, "value": 4.0e10})]
+    rows = S.rows_from(res, "dna_1073741824", 1 << 30)
+    assert [r["backend"] for r in rows] == ["hip_1", "hip_2"]
+    assert set(S.COLUMNS) == set(rows[0])
+    assert rows[1]["speedup"] == pytest.approx(1.6) and rows[1]["efficiency"] == pytest.approx(0.8)
+    assert rows[0]["speedup_vs_cpu"] == pytest.approx(2500.0)
+    assert S.last_json('noise\n{"a": 1}\n') == {"a": 1}
