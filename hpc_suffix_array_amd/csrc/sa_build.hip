@@ -653,7 +653,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
     uint64_t* ukb1 = c->keys_u;
     const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K,
-                        bucketed ? 1u : 0u, bp.bs};
+                        bucketed ? 1u : 0u, bp.bs, bucketed ? c->segw + kBstartOff : nullptr};
     if (st) st->sparse_ranks = sparse ? 1 : 0;
     SA_HIP(hipEventRecord(ev.e[1], s));
     SA_HIP(hipEventSynchronize(ev.e[1]));
@@ -955,7 +955,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
-        hipMalloc(&c->segw, segw_words(1024) * 4) != hipSuccess ||
+        hipMalloc(&c->segw, (kBstartOff + kBstartWords) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);

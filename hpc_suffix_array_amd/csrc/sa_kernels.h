@@ -139,14 +139,21 @@ struct RankLookup {
     uint32_t K;
     uint32_t bucketed;                     // 1: keys1 holds key1 (BucketSpec layout)
     BucketSpec bs;
+    const uint32_t* __restrict__ bstart;   // bucketed: bucket start positions (2^bb + 1), or null
     __device__ __forceinline__ uint32_t sparse(uint64_t j) const {
         if ((member[j >> 5] >> (j & 31)) & 1u) return rank[j];
         uint64_t x = 0;
-        if (bucketed)
+        uint64_t lo = 0, len = n;      // lower_bound(keys1, x), inside x's bucket when known
+        if (bucketed) {
             x = key1_at(text, code, n, bs, j);
-        else
+            if (bstart) {
+                const uint32_t b = (uint32_t)(((x >> bs.rb) * bs.cmul) >> bs.bsh);
+                lo = bstart[b];
+                len = bstart[b + 1] - lo;
+            }
+        } else {
             for (uint32_t t = 0; t < K; ++t) x = x * base + ((j + t < n) ? code[text[j + t]] : 0u);
-        uint64_t lo = 0, len = n;      // lower_bound(keys1, x)
+        }
         while (len > 0) {
             const uint64_t half = len >> 1;
             if (keys1[lo + half] < x) {

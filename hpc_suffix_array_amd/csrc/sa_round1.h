@@ -144,6 +144,15 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_SEG_PASS
             default: return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
         }
+        // bucket starts (sparse rank look-ups search one bucket)
+        const uint32_t gb = (uint32_t)std::min<uint64_t>(((1ull << bp.bs.bb) + kBlock) / kBlock, 1024);
+        uint32_t* bstart = c->segw + kBstartOff;
+        switch (hb) {
+            case 7: hipLaunchKernelGGL(k_bucket_starts<128>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
+            case 8: hipLaunchKernelGGL(k_bucket_starts<256>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
+            case 9: hipLaunchKernelGGL(k_bucket_starts<512>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
+            default: hipLaunchKernelGGL(k_bucket_starts<1024>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
+        }
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);

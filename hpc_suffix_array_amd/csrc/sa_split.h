@@ -485,6 +485,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegs = kLoRadix;
 constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; }
+// the bucket starts live after the widest pass's segment words
+constexpr uint64_t kBstartOff = segw_words(1024);
+constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 
 template <class Src, int RBITS, int ITEMS>
 __global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uint32_t shift,
@@ -677,6 +680,27 @@ __global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uin
         tb = tbn;
         valid = validn;
         par ^= 1u;
+    }
+}
+
+// bucket b = (h << kLoBits) | l starts at base(h, l) in the second pass's
+// output (= SA order of round 1): digit_base[h] while every segment before
+// l is empty, else the value k_split_seg published.  bstart[2^bb] = n.  The
+// sparse rank look-ups of later rounds search key1 only inside the bucket.
+template <int RADIX>
+__global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __restrict__ lo_base,
+                                                          const uint32_t* __restrict__ digit_base,
+                                                          const uint32_t* __restrict__ segw, uint64_t n,
+                                                          uint32_t* __restrict__ bstart) {
+    const uint64_t* sbase = reinterpret_cast<const uint64_t*>(segw + (uint64_t)kSegs * RADIX);
+    const uint32_t nb = (uint32_t)RADIX << kLoBits;
+    for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b <= nb; b += gridDim.x * kBlock) {
+        if (b == nb) {
+            bstart[b] = (uint32_t)n;
+            continue;
+        }
+        const uint32_t h = b >> kLoBits, l = b & (kSegs - 1);
+        bstart[b] = lo_base[l] == 0 ? digit_base[h] : (uint32_t)sbase[(uint64_t)l * RADIX + h];
     }
 }
 
