@@ -181,6 +181,33 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
 }
 
 // ---------------------------------------------------------------------------
+// The same window starts from the bucket start table (bstart[0 .. nb],
+// non-decreasing, bstart[nb] = n): ws[j] = the first bucket start >= j*W,
+// a binary search in a 512 KiB table instead of a gallop over the keys.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kBlock) void k_window_starts_tab(const uint32_t* __restrict__ bstart, uint32_t nb,
+                                                              uint64_t n, uint64_t nw, uint32_t* __restrict__ ws) {
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j <= nw; j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t x = j * kWinStride;
+        if (x >= n) {
+            ws[j] = (uint32_t)n;
+            continue;
+        }
+        uint32_t lo = 0, len = nb + 1;   // lower_bound(bstart, x)
+        while (len > 0) {
+            const uint32_t half = len >> 1;
+            if (bstart[lo + half] < x) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        ws[j] = bstart[lo];
+    }
+}
+
+// ---------------------------------------------------------------------------
 // window starts over the bucket-sorted keys: ws[j] = first g >= j*W with
 // g == 0, g == n or bucket(g) != bucket(g-1) (gallop, then bisect); j <= nw.
 // ---------------------------------------------------------------------------

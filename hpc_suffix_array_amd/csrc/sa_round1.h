@@ -164,8 +164,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_WINDOWS);
     {
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nw + kBlock) / kBlock, 8192);
-        hipLaunchKernelGGL(k_window_starts, dim3(g1), dim3(kBlock), 0, s, (const uint64_t*)c->keys_u, n, nw, bp.bs.rb,
-                           bp.bs.cmul, bp.bs.bsh, ws);
+        hipLaunchKernelGGL(k_window_starts_tab, dim3(g1), dim3(kBlock), 0, s, (const uint32_t*)(c->segw + kBstartOff),
+                           1u << bp.bs.bb, n, nw, ws);
         const uint32_t g2 = (uint32_t)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(k_window_list, dim3(g2), dim3(kBlock), 0, s, (const uint32_t*)ws, nw, list, c->words);
     }
