@@ -293,8 +293,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // a K - 1 byte halo, as 32-bit words) is loaded while the current one is
 // staged and written.
 // ---------------------------------------------------------------------------
-template <int ITEMS>
-__global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
+// (BLOCK 512, two workgroups per CU, measured slower: 5.5 -> 6.3 ms)
+template <int ITEMS, int BLOCK = kSpBlock>
+__global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
@@ -302,10 +303,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
-    constexpr int TILE = kSpBlock * ITEMS;
+    constexpr int TILE = BLOCK * ITEMS;
     constexpr int kHalo = kMaxK;                        // >= K - 1 bytes past the tile
     constexpr int NW = (TILE + kHalo) / 4;              // staged text words
-    constexpr int WPT = (NW + kSpBlock - 1) / kSpBlock; // per lane
+    constexpr int WPT = (NW + BLOCK - 1) / BLOCK; // per lane
     static_assert(ITEMS % 4 == 0 && kHalo % 4 == 0 && TILE <= 65535, "word staging, 16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint16_t s_idx[TILE];
@@ -323,7 +324,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
     const uint32_t dg = threadIdx.x;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t K = b.s + b.R;
-    s_hhi[dg] = 0;
+    for (uint32_t i = dg; i < 1024u; i += BLOCK) s_hhi[i] = 0;
     if (dg < 256u) {
         const uint32_t cv = code[dg];
         s_map[dg] = (uint8_t)(cv ? cv - 1u : 0u);
@@ -346,7 +347,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         const uint64_t tb = tt * TILE;
 #pragma unroll
         for (int i = 0; i < WPT; ++i) {
-            const uint32_t w = dg + i * kSpBlock;
+            const uint32_t w = dg + i * BLOCK;
             raw[i] = w < (uint32_t)NW ? load4(tb + 4ull * w) : 0u;
         }
     };
@@ -358,7 +359,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         // dense digits (0 past the end)
 #pragma unroll
         for (int i = 0; i < WPT; ++i) {
-            const uint32_t w = dg + i * kSpBlock;
+            const uint32_t w = dg + i * BLOCK;
             if (w < (uint32_t)NW) {
                 uint32_t o = 0;
 #pragma unroll
@@ -447,7 +448,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            const uint32_t q = j * kSpBlock + dg;
+            const uint32_t q = j * BLOCK + dg;
             if (q < valid) {
                 const uint64_t key = s_keys[q];
                 const uint32_t dd = (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh) & (RADIX - 1);
@@ -462,7 +463,8 @@ __global__ __launch_bounds__(kSpBlock) void k_split_text(const uint8_t* __restri
         t = tn;
         par ^= 1u;
     }
-    if (s_hhi[dg]) atomicAdd(&ghist_hi[dg], s_hhi[dg]);
+    for (uint32_t i = dg; i < 1024u; i += BLOCK)
+        if (s_hhi[i]) atomicAdd(&ghist_hi[i], s_hhi[i]);
 }
 
 // ---------------------------------------------------------------------------
@@ -489,8 +491,9 @@ constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; 
 constexpr uint64_t kBstartOff = segw_words(1024);
 constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 
-template <class Src, int RBITS, int ITEMS>
-__global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uint32_t shift,
+// (BLOCK 512 x 10 items, two workgroups per CU, measured slower: 7.2 -> 9.1 ms)
+template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock>
+__global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint64_t n, uint32_t shift,
                                                         const uint32_t* __restrict__ lo_base,
                                                         const uint32_t* __restrict__ digit_base,
                                                         uint32_t* __restrict__ segw, uint32_t* __restrict__ ticket,
@@ -499,15 +502,15 @@ __global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uin
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
-    constexpr int TILE = kSpBlock * ITEMS;
-    static_assert(kSpBlock >= RADIX && (int)kSegs <= kSpBlock, "one thread per digit / segment");
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(BLOCK >= RADIX && (int)kSegs <= BLOCK, "one thread per digit / segment");
     static_assert(TILE <= 65535, "16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint32_t s_vals[TILE];
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
     __shared__ uint32_t s_gofs[RADIX];
-    __shared__ uint32_t s_tmp[kSpWaves];
+    __shared__ uint32_t s_tmp[(BLOCK / kWave)];
     __shared__ uint32_t s_ubase[kSegs + 1];   // units before segment l (exclusive scan)
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_last;
@@ -658,7 +661,7 @@ __global__ __launch_bounds__(kSpBlock) void k_split_seg(Src src, uint64_t n, uin
         if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            const uint32_t q = j * kSpBlock + dg;
+            const uint32_t q = j * BLOCK + dg;
             if (q < valid) {
                 const uint64_t key = s_keys[q];
                 const uint32_t dd = src_digit(src, key, shift, mask, 0);
