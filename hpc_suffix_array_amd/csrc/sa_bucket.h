@@ -100,7 +100,7 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) 
 
 // ---------------------------------------------------------------------------
 // Digit totals of the first bucket pass straight from the text: the bucket
-// depends on D (the first s dense digits, < sigma * 2^bb <= 2^26) only, so
+// depends on D (the first s dense digits, < 2^32: plan_bucketed) only, so
 // each lane rolls D in 32 bits over 16 consecutive positions; an LDS
 // histogram of the low kLoBits -> ghist[0 .. kLoRadix) (the high bits are
 // counted by the first pass itself, k_split_text).  Grid-stride over

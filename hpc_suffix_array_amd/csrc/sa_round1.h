@@ -28,6 +28,15 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
         ps *= sigma;
         ++s;
     }
+    // sigma^s a multiple of 2^bb (sigma a power of two): every bucket is an
+    // equal range of D values.  Otherwise buckets hold floor or ceil of
+    // sigma^s / 2^bb values -- up to 2x apart when the ratio is ~1 (alnum:
+    // 9472-suffix windows at 2^30, over the LDS tile) -- so s grows until the
+    // ratio is >= 64 (sizes within 1/64), which keeps D < 64 sigma 2^bb <= 2^32
+    while (ps % (1ull << bb) != 0 && ps < (64ull << bb) && s + 1 < K) {
+        ps *= sigma;
+        ++s;
+    }
     if (K <= s || K > (uint32_t)kMaxK) return false;
     const uint32_t ib = bit_width(n - 1);
     const uint32_t bd = bit_width(ps - 1);

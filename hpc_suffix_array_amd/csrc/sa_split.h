@@ -371,7 +371,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             }
         }
         __syncthreads();
-        // key1 of positions tb + ITEMS dg + j (D < sigma * 2^bb <= 2^26 rolls
+        // key1 of positions tb + ITEMS dg + j (D < 64 sigma 2^bb <= 2^32 rolls
         // in 32 bits; the remainder in 64)
         uint64_t k[ITEMS];
         uint32_t dr[ITEMS];

@@ -19,7 +19,7 @@ for f in glob.glob(out + "/**/*counter_collection.csv", recursive=True):
         k = r["Kernel_Name"].split("(")[0][:60]
         acc[k][r["Counter_Name"]] += float(r["Counter_Value"])
 for k, v in acc.items():
-    if any(s in k for s in ("bucket_sort", "onesweep", "pack_bucket", "seg_")):
+    if any(s in k for s in ("bucket_sort", "onesweep", "k_split", "bucket_hist", "seg_")):
         print(k)
         for c, x in sorted(v.items()):
             print(f"   {c:24s} {x:.4g}")
