@@ -66,6 +66,15 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t key1, uint32_t rb, uint64
     return (uint32_t)(((key1 >> rb) * cmul) >> bsh);
 }
 
+// smallest D of bucket b (D * cmul >> bsh is monotone: d0 = floor(b 2^bsh /
+// cmul) has bucket <= b and d0 + 1 bucket >= b).  Bucket-relative items
+// (second pass output) are w = (key1 - (Dmin(b) << rb)) << ib | idx, which
+// fits 64 bits by plan_bucketed's span + rb + ib <= 64.
+__device__ __forceinline__ uint32_t bucket_dmin(uint32_t b, uint64_t cmul, uint32_t bsh) {
+    const uint64_t d0 = ((uint64_t)b << bsh) / cmul;
+    return (uint32_t)((((d0 * cmul) >> bsh) == b) ? d0 : d0 + 1);
+}
+
 // radix source of the second bucket pass (digits of bucket_of(key))
 struct SrcBucketKeys {
     const uint64_t* __restrict__ keys;
@@ -183,14 +192,17 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
 // ---------------------------------------------------------------------------
 // The same window starts from the bucket start table (bstart[0 .. nb],
 // non-decreasing, bstart[nb] = n): ws[j] = the first bucket start >= j*W,
-// a binary search in a 512 KiB table instead of a gallop over the keys.
+// a binary search in a 512 KiB table instead of a gallop over the keys;
+// wb[j] = that bucket.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(kBlock) void k_window_starts_tab(const uint32_t* __restrict__ bstart, uint32_t nb,
-                                                              uint64_t n, uint64_t nw, uint32_t* __restrict__ ws) {
+                                                              uint64_t n, uint64_t nw, uint32_t* __restrict__ ws,
+                                                              uint32_t* __restrict__ wb) {
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j <= nw; j += (uint64_t)gridDim.x * kBlock) {
         const uint64_t x = j * kWinStride;
         if (x >= n) {
             ws[j] = (uint32_t)n;
+            wb[j] = nb;
             continue;
         }
         uint32_t lo = 0, len = nb + 1;   // lower_bound(bstart, x)
@@ -204,6 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_window_starts_tab(const uint32_t* __
             }
         }
         ws[j] = bstart[lo];
+        wb[j] = lo;   // the window's first bucket (its buckets: [wb[j], wb[j + 1]))
     }
 }
 
@@ -311,16 +324,61 @@ constexpr int kSubBits = 11;
 constexpr int kSubBuckets = 1 << kSubBits;
 constexpr uint32_t kMaxSub = 64;
 
-// window j's keys -> registers as w = (key1 - min) << ib | idx; false (and the
-// error flag) when the key span does not fit beside the index bits
+// where the second pass's bucket-relative items (k_split_seg) sit: window j
+// holds buckets [wb[j], wb[j + 1]); bucket b starts at bstart[b] and its
+// smallest D is bdmin[b]
+struct BucketRel {
+    const uint32_t* __restrict__ wb;
+    const uint32_t* __restrict__ bstart;
+    const uint32_t* __restrict__ bdmin;
+    uint32_t rb;
+};
+
+// window j's items -> registers as w = (key1 - min) << ib | idx, with key1 =
+// (Dmin(bucket) << rb) + (item >> ib); false (and the error flag) when the
+// key span does not fit beside the index bits.  s_bk: 2 x 32 words of LDS
+// (the bucket starts and Dmin of a window of up to 32 buckets).
 template <int BLOCK, int ITEMS>
-__device__ __forceinline__ bool load_window(const uint64_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in,
+__device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, const BucketRel& br, uint32_t j,
                                             uint64_t a, uint32_t m, uint32_t ib, uint64_t (&w)[ITEMS], uint64_t& mn,
                                             uint32_t& bits, uint64_t (*s_red)[BLOCK / kWave],
-                                            uint32_t* __restrict__ err) {
+                                            uint32_t (*s_bk)[32], uint32_t* __restrict__ err) {
     constexpr int WAVES = BLOCK / kWave;
     constexpr int WT = kWave * ITEMS;
     const uint32_t wave = wave_id(), lane = lane_id();
+    const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
+    const uint32_t b0 = br.wb[j], nbk = br.wb[j + 1] - b0;   // uniform
+    uint32_t dmin0 = 0;
+    if (nbk == 1) {
+        dmin0 = br.bdmin[b0];
+    } else if (nbk <= 32) {
+        if (threadIdx.x < nbk) {
+            s_bk[0][threadIdx.x] = br.bstart[b0 + threadIdx.x];
+            s_bk[1][threadIdx.x] = br.bdmin[b0 + threadIdx.x];
+        }
+        __syncthreads();
+    }
+    // bucket of position p: the last of the window's buckets starting <= p
+    auto dmin_of = [&](uint64_t p) -> uint32_t {
+        if (nbk == 1) return dmin0;
+        if (nbk <= 32) {
+            uint32_t lo = 0;
+            for (uint32_t step = 16; step; step >>= 1)
+                if (lo + step < nbk && s_bk[0][lo + step] <= p) lo += step;
+            return s_bk[1][lo];
+        }
+        uint32_t lo = b0, len = nbk;   // last b in [b0, b0 + nbk) with bstart[b] <= p
+        while (len > 1) {
+            const uint32_t half = len >> 1;
+            if (br.bstart[lo + half] <= p) {
+                lo += half;
+                len -= half;
+            } else {
+                len = half;
+            }
+        }
+        return br.bdmin[lo];
+    };
     uint32_t v[ITEMS];
     uint64_t mx = 0;
     mn = ~0ull;
@@ -332,8 +390,9 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ keys_in
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t le = l0 + i * kWave;
         const uint64_t e = a + (le < m ? le : m - 1);
-        w[i] = keys_in[e];
-        v[i] = vals_in[e];
+        const uint64_t x = w_in[e];
+        v[i] = (uint32_t)(x & imask);
+        w[i] = ((uint64_t)dmin_of(e) << br.rb) + (x >> ib);
         mn = w[i] < mn ? w[i] : mn;
         mx = w[i] > mx ? w[i] : mx;
     }
@@ -640,8 +699,7 @@ constexpr int kNet = 16;   // sub-buckets up to this size are sorted in register
 // loaded window is written back in input order); 2 accumulates per-phase
 // clock64() spans of thread 0 into words[16..23] (words must hold 24 u64)
 template <int BLOCK, int ITEMS, int kVariant = 0>
-__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
-                                                       const uint32_t* __restrict__ vals_in,
+__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in, BucketRel br,
                                                        const uint32_t* __restrict__ ws,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
                                                        uint32_t ib, uint64_t* __restrict__ keys_out,
@@ -654,6 +712,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
     __shared__ uint32_t s_tmp[WAVES];
     __shared__ uint64_t s_red[2][WAVES];
+    __shared__ uint32_t s_bk[2][32];
     constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
     static_assert(WPT >= 1 && WPT * 2 * BLOCK == kSubBuckets, "whole counter words per thread");
 
@@ -685,7 +744,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         uint64_t w[ITEMS];
         uint64_t mn;
         uint32_t bits;
-        if (!load_window<BLOCK, ITEMS>(keys_in, vals_in, a, m, ib, w, mn, bits, s_red, err)) {
+        if (!load_window<BLOCK, ITEMS>(keys_in, br, j, a, m, ib, w, mn, bits, s_red, s_bk, err)) {
             __syncthreads();
             continue;
         }
@@ -905,8 +964,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
 // in-wave ranking (match-any from 8 ballots, wave-major input order), per-
 // digit wave prefixes, digit offsets, scatter into LDS, read back in order.
 template <int BLOCK, int ITEMS>
-__global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __restrict__ keys_in,
-                                                           const uint32_t* __restrict__ vals_in,
+__global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __restrict__ keys_in, BucketRel br,
                                                            const uint32_t* __restrict__ ws,
                                                            const uint32_t* __restrict__ skew,
                                                            uint32_t* __restrict__ words, uint32_t ib,
@@ -922,6 +980,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
     __shared__ uint16_t s_start[kRadix];
     __shared__ uint32_t s_tmp[kWaves];
     __shared__ uint64_t s_red[2][WAVES];
+    __shared__ uint32_t s_bk[2][32];
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -936,7 +995,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
         uint64_t w[ITEMS];
         uint64_t mn;
         uint32_t bits;
-        if (!load_window<BLOCK, ITEMS>(keys_in, vals_in, a, m, ib, w, mn, bits, s_red, err)) {
+        if (!load_window<BLOCK, ITEMS>(keys_in, br, j, a, m, ib, w, mn, bits, s_red, s_bk, err)) {
             __syncthreads();
             continue;
         }

@@ -955,7 +955,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
-        hipMalloc(&c->segw, (kBstartOff + kBstartWords) * 4) != hipSuccess ||
+        hipMalloc(&c->segw, (kBstartOff + 2 * kBstartWords) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);

@@ -144,7 +144,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
         hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, n, kLoBits, \
-                           (const uint32_t*)os_base(c), hbase, c->segw, tk, c->keys_u, c->vals_u, c->words + 4); \
+                           (const uint32_t*)os_base(c), hbase, c->segw, tk, bp.ib, c->keys_u, c->words + 4);    \
         break;
             SA_SEG_PASS(7)
             SA_SEG_PASS(8)
@@ -153,18 +153,24 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_SEG_PASS
             default: return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
         }
-        // bucket starts (sparse rank look-ups search one bucket)
+        // bucket starts and smallest D values (the local sort rebuilds key1
+        // from them; sparse rank look-ups search one bucket)
         const uint32_t gb = (uint32_t)std::min<uint64_t>(((1ull << bp.bs.bb) + kBlock) / kBlock, 1024);
         uint32_t* bstart = c->segw + kBstartOff;
+        uint32_t* bdmin = bstart + kBstartWords;
+#define SA_BSTARTS(R)                                                                                         \
+    hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase,     \
+                       (const uint32_t*)c->segw, n, bp.bs.cmul, bp.bs.bsh, bstart, bdmin)
         switch (hb) {
-            case 7: hipLaunchKernelGGL(k_bucket_starts<128>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
-            case 8: hipLaunchKernelGGL(k_bucket_starts<256>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
-            case 9: hipLaunchKernelGGL(k_bucket_starts<512>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
-            default: hipLaunchKernelGGL(k_bucket_starts<1024>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase, (const uint32_t*)c->segw, n, bstart); break;
+            case 7: SA_BSTARTS(128); break;
+            case 8: SA_BSTARTS(256); break;
+            case 9: SA_BSTARTS(512); break;
+            default: SA_BSTARTS(1024); break;
         }
+#undef SA_BSTARTS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_KEYS, 24 * n);
+    add_bytes(st, SA_K_SCATTER_KEYS, 20 * n);
     SA_HIP(hipGetLastError());
     // windows of whole buckets; ws lives in vals_alt (free again; nw + 1 <= n)
     const uint64_t nw = (n + kWinStride - 1) / kWinStride;
@@ -174,7 +180,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nw + kBlock) / kBlock, 8192);
         hipLaunchKernelGGL(k_window_starts_tab, dim3(g1), dim3(kBlock), 0, s, (const uint32_t*)(c->segw + kBstartOff),
-                           1u << bp.bs.bb, n, nw, ws);
+                           1u << bp.bs.bb, n, nw, ws, list + 4 * nw + 2);   // wb: see br below
         const uint32_t g2 = (uint32_t)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(k_window_list, dim3(g2), dim3(kBlock), 0, s, (const uint32_t*)ws, nw, list, c->words);
     }
@@ -190,10 +196,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         return SA_OK;
     }
     // windows with clustered keys, then per-window U / U-group counts (scanned
-    // in place: nw + 1 each); 5 nw + 3 <= capacity
+    // in place: nw + 1 each), then each window's first bucket (nw + 1,
+    // written by k_window_starts_tab); 6 nw + 4 <= capacity
     uint32_t* skew = list + nw;
     uint32_t* cnt_u = skew + nw;
     uint32_t* cnt_g = cnt_u + nw + 1;
+    const BucketRel br{cnt_g + nw + 1, c->segw + kBstartOff, c->segw + kBstartOff + kBstartWords, bp.bs.rb};
     SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
     SA_HIP(hipMemsetAsync(c->member, 0, (n + 31) / 32 * 4, s));
     const SegOut so{c->rank, c->member, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g};
@@ -201,14 +209,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
-                           (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
-                           (const uint32_t*)list, c->words, bp.ib, c->keys[0], d_sa, skew, so);
+                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
+                           c->keys[0], d_sa, skew, so);
         hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
-                           (const uint64_t*)c->keys_u, (const uint32_t*)c->vals_u, (const uint32_t*)ws,
-                           (const uint32_t*)skew, c->words, bp.ib, c->keys[0], d_sa, so);
+                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)skew, c->words, bp.ib,
+                           c->keys[0], d_sa, so);
     }
     tm.end();
-    add_bytes(st, SA_K_LOCAL_SORT, 24 * n);
+    add_bytes(st, SA_K_LOCAL_SORT, 20 * n);
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));

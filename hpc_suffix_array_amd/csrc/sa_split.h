@@ -483,7 +483,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
 // slower): a claim's atomic has returned before its unit counts itself
 // done, and base words carry their own ready bit (bit 32).
 // segw (zeroed before the pass): cur u32[256][RADIX] | base u64[256][RADIX]
-// | done u32[256].
+// | done u32[256].  Output: one 64-bit word per pair, bucket-relative
+// (bucket_dmin, sa_bucket.h): w = (key1 - (Dmin(b) << rb)) << ib | idx --
+// 8 B written (and read by the local sort) instead of 12.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegs = kLoRadix;
 constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; }
@@ -497,16 +499,17 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                                                         const uint32_t* __restrict__ lo_base,
                                                         const uint32_t* __restrict__ digit_base,
                                                         uint32_t* __restrict__ segw, uint32_t* __restrict__ ticket,
-                                                        uint64_t* __restrict__ out_keys,
-                                                        uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
+                                                        uint32_t ib, uint64_t* __restrict__ out_w,
+                                                        uint32_t* __restrict__ err) {
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(BLOCK >= RADIX && (int)kSegs <= BLOCK, "one thread per digit / segment");
     static_assert(TILE <= 65535, "16-bit tile offsets");
-    __shared__ uint64_t s_keys[TILE];
-    __shared__ uint32_t s_vals[TILE];
+    __shared__ uint64_t s_keys[TILE];   // bucket-relative items, digit-sorted
+    __shared__ uint16_t s_dig[TILE];
+    __shared__ uint32_t s_dmin[RADIX];  // Dmin of bucket (h, l)
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
     __shared__ uint32_t s_gofs[RADIX];
@@ -623,6 +626,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
             s_gofs[dg] = bh + s_claim[dg];
             s_claim[dg] = bh;
+            s_dmin[dg] = bucket_dmin((dg << kLoBits) | l, src.cmul, src.bsh);
         }
         __syncthreads();
         if (s_last) {
@@ -653,8 +657,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                s_keys[pos] = k[j];
-                s_vals[pos] = v[j];
+                s_keys[pos] = ((k[j] - ((uint64_t)s_dmin[d] << src.rb)) << ib) | v[j];
+                s_dig[pos] = (uint16_t)d;
             }
         }
         __syncthreads();
@@ -663,13 +667,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t q = j * BLOCK + dg;
             if (q < valid) {
-                const uint64_t key = s_keys[q];
-                const uint32_t dd = src_digit(src, key, shift, mask, 0);
+                const uint32_t dd = s_dig[q];
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                if (g < n) {
-                    out_keys[g] = key;
-                    out_vals[g] = s_vals[q];
-                }
+                if (g < n) out_w[g] = s_keys[q];
             }
         }
         __syncthreads();
@@ -688,13 +688,16 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
 
 // bucket b = (h << kLoBits) | l starts at base(h, l) in the second pass's
 // output (= SA order of round 1): digit_base[h] while every segment before
-// l is empty, else the value k_split_seg published.  bstart[2^bb] = n.  The
-// sparse rank look-ups of later rounds search key1 only inside the bucket.
+// l is empty, else the value k_split_seg published.  bstart[2^bb] = n; the
+// bucket's smallest D is bdmin[b].  The local sort rebuilds key1 from the
+// bucket-relative items with them; the sparse rank look-ups of later rounds
+// search key1 only inside the bucket.
 template <int RADIX>
 __global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __restrict__ lo_base,
                                                           const uint32_t* __restrict__ digit_base,
                                                           const uint32_t* __restrict__ segw, uint64_t n,
-                                                          uint32_t* __restrict__ bstart) {
+                                                          uint64_t cmul, uint32_t bsh, uint32_t* __restrict__ bstart,
+                                                          uint32_t* __restrict__ bdmin) {
     const uint64_t* sbase = reinterpret_cast<const uint64_t*>(segw + (uint64_t)kSegs * RADIX);
     const uint32_t nb = (uint32_t)RADIX << kLoBits;
     for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b <= nb; b += gridDim.x * kBlock) {
@@ -704,6 +707,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __rest
         }
         const uint32_t h = b >> kLoBits, l = b & (kSegs - 1);
         bstart[b] = lo_base[l] == 0 ? digit_base[h] : (uint32_t)sbase[(uint64_t)l * RADIX + h];
+        bdmin[b] = bucket_dmin(b, cmul, bsh);
     }
 }
 
