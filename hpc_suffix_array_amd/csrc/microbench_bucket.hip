@@ -27,18 +27,28 @@ using namespace sa;
 
 // key = bucket << rb | random rbits bits, bucket = (i << 17) / n (rb = 28;
 // fewer random bits make equal keys: unsorted groups for the segments)
-__global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t n, uint32_t rb, uint32_t rbits) {
+// key1 = bucket << rb | random rbits bits, bucket = (i << 17) / n; as the
+// second bucket pass writes them: bucket-relative items (key1 - (Dmin(b) <<
+// rb)) << ib | idx with Dmin(b) = b (cmul = 1, bsh = 0); keys[] keeps key1
+// for the copy baseline and the check
+__global__ void k_keys(uint64_t* keys, uint32_t* vals, uint64_t* items, uint64_t n, uint32_t rb, uint32_t rbits,
+                       uint32_t ib) {
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
         uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
         z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
         z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
         z ^= z >> 31;
-        if (rbits == 0) {   // DNA-like: low = 20 + 13 E, E uniform in [0, 4^12) (s = 8, R = 12)
-            keys[i] = ((i << 17) / n << rb) | (20 + 13 * (z % (1ull << 24)));
-        } else {
-            keys[i] = ((i << 17) / n << rb) | ((z & ((1ull << rbits) - 1)) << (rb - rbits));
-        }
-        vals[i] = (uint32_t)(z >> 32);
+        const uint64_t low = (z & ((1ull << rbits) - 1)) << (rb - rbits);
+        keys[i] = ((i << 17) / n << rb) | low;
+        vals[i] = (uint32_t)(z >> 32) & ((1u << ib) - 1u);
+        items[i] = (low << ib) | vals[i];
+    }
+}
+
+__global__ void k_tables(uint64_t n, uint32_t* bstart, uint32_t* bdmin) {
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b <= (1u << 17); b += gridDim.x * blockDim.x) {
+        bstart[b] = b == (1u << 17) ? (uint32_t)n : (uint32_t)(((uint64_t)b * n + (1u << 17) - 1) >> 17);
+        bdmin[b] = b;
     }
 }
 
@@ -57,17 +67,25 @@ int main(int argc, char** argv) {
     const uint64_t n = 1ull << lg;
     const uint32_t rb = 28, ib = lg;
     uint64_t *keys, *okeys;
-    uint32_t *vals, *ovals, *ws, *words;
+    uint32_t *vals, *ovals, *ws, *words, *tab;
+    uint64_t* items;
     CK(hipMalloc(&keys, n * 8));
+    CK(hipMalloc(&items, n * 8));
+    CK(hipMalloc(&tab, ((1u << 17) + 1) * 8));
     CK(hipMalloc(&okeys, n * 8));
     CK(hipMalloc(&vals, n * 4));
     CK(hipMalloc(&ovals, n * 4));
     const uint64_t nw = (n + kWinStride - 1) / kWinStride;
-    CK(hipMalloc(&ws, (3 * nw + 2) * 4));
+    CK(hipMalloc(&ws, (4 * nw + 3) * 4));
     CK(hipMalloc(&words, 256));
     uint32_t* list = ws + nw + 1;
     uint32_t* skew = list + nw;
-    hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, n, rb, rbits);
+    uint32_t* wbk = skew + nw;   // each window's first bucket
+    uint32_t* bstart = tab;
+    uint32_t* bdmin = tab + (1u << 17) + 1;
+    hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, items, n, rb, rbits, ib);
+    hipLaunchKernelGGL(k_tables, dim3(512), dim3(256), 0, 0, n, bstart, bdmin);
+    const BucketRel br{wbk, bstart, bdmin, rb};
     // segments outputs (as round1_bucketed lays them out)
     uint32_t *rank, *member, *tmp;
     CK(hipMalloc(&rank, n * 4));
@@ -78,8 +96,9 @@ int main(int argc, char** argv) {
     const SegOut so{rank, member, tmp, tmp + n, tmp + 2 * n, cnt, cnt + nw + 1};
     CK(hipMemset(words, 0, 256));
     const uint64_t cmul = 1;   // bucket = D = key >> rb (17 bits), bsh = 0
-    hipLaunchKernelGGL(k_window_starts, dim3((uint32_t)std::min<uint64_t>((nw + 256) / 256, 8192)), dim3(256), 0, 0,
-                       (const uint64_t*)keys, n, nw, rb, cmul, 0u, ws);
+    (void)cmul;
+    hipLaunchKernelGGL(k_window_starts_tab, dim3((uint32_t)std::min<uint64_t>((nw + 256) / 256, 8192)), dim3(256), 0, 0,
+                       (const uint32_t*)bstart, 1u << 17, n, nw, ws, wbk);
     hipLaunchKernelGGL(k_window_list, dim3((uint32_t)std::min<uint64_t>((nw + 255) / 256, 1024)), dim3(256), 0, 0,
                        (const uint32_t*)ws, nw, list, words);
     CK(hipDeviceSynchronize());
@@ -104,7 +123,7 @@ int main(int argc, char** argv) {
         }
         std::printf("%-40s %8.3f ms  %7.1f GB/s (24 B/suffix)\n", name, best, 24.0 * n / best / 1e6);
     };
-    timeit("copy 12 B in + out", [&] {
+    timeit("copy 12 B in + out (old item size)", [&] {
         hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
     });
     for (uint32_t g : {512u}) {
@@ -112,19 +131,19 @@ int main(int argc, char** argv) {
         std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
         timeit(nm, [&] {
             hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
-                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, SegOut{});
         });
         std::snprintf(nm, sizeof nm, "bucket_sort + segments grid %u", g);
         timeit(nm, [&] {
             hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
-                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, so);
         });
         std::snprintf(nm, sizeof nm, "bucket_sort no-sort grid %u", g);
         timeit(nm, [&] {
             hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 1>), dim3(g), dim3(kBsBlock), 0, 0,
-                               (const uint64_t*)keys, (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list,
+                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, SegOut{});
         });
     }
@@ -132,15 +151,14 @@ int main(int argc, char** argv) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "bucket_sort 512x18 + seg grid %u", g);
         timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<512, 18, 0>), dim3(g), dim3(512), 0, 0, (const uint64_t*)keys,
-                               (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals,
-                               skew, so);
+            hipLaunchKernelGGL((k_bucket_sort<512, 18, 0>), dim3(g), dim3(512), 0, 0, (const uint64_t*)items, br,
+                               (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
         });
     }
     {   // per-phase clock64 spans of one workgroup's thread 0, per window
         CK(hipMemset(words + 32, 0, 64));
-        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 2>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
-                           (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
+        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 2>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
+                           br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
         CK(hipDeviceSynchronize());
         unsigned long long t[7];
         CK(hipMemcpy(t, words + 32, 56, hipMemcpyDeviceToHost));
@@ -154,8 +172,8 @@ int main(int argc, char** argv) {
     std::printf("flags=%u skewed=%u heads=%u unsorted=%u groups=%u (accumulated over runs)\n", hw[6], hw[10], hw[0], hw[1], hw[2]);
     // check: output sorted within each window, keys monotone overall
     std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
-    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)keys,
-                       (const uint32_t*)vals, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
+                       br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
     CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (size_t i = 1; i < h.size(); ++i) bad += h[i] < h[i - 1];
