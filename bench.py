@@ -29,6 +29,7 @@ import argparse
 import glob
 import json
 import os
+import re
 import statistics
 import sys
 import time
@@ -112,7 +113,10 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
 def pmc_summary() -> dict | None:
     """The latest committed rocprofv3 summary (profiles/<tag>_summary.json,
     written by profiles/collect.sh + summarize.py), or None."""
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")))
+    def version(path):   # r01_v21_summary.json -> (1, 21): numeric, not lexical, order
+        nums = re.findall(r"\d+", os.path.basename(path))
+        return tuple(int(x) for x in nums)
+    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=version)
     if not paths:
         return None
     try:

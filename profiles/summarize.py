@@ -21,7 +21,8 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_split_text", "scatter_first"), ("k_split<sa::SrcBucketKeys", "scatter_keys"), ("k_bucket_hist", "pack"),
+KINDS = [("k_split_text", "scatter_first"), ("k_split_seg", "scatter_keys"), ("k_split<sa::SrcBucketKeys", "scatter_keys"),
+         ("k_bucket_hist", "pack"), ("k_bucket_starts", "bucket_starts"),
          ("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcText>", "hist_text"),
          ("k_hist<sa::SrcU", "hist_u"), ("k_hist<sa::SrcKeys>", "hist_keys"),
          ("k_scan_rows", "scan"), ("k_scatter<sa::SrcRank>", "scatter_rank"),
