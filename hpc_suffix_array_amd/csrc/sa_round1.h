@@ -108,20 +108,19 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // order -> bucket order; sa_split.h)
     tm.begin(SA_K_SCATTER_FIRST);
     {
-        // tile size (tuning knob SA_TUNE_ITEMS_A = 8 | 12, default 12)
-        static const int items_a = [] {
-            const char* e = std::getenv("SA_TUNE_ITEMS_A");
-            return (e && std::atoi(e) == 8) ? 8 : 12;
-        }();
-        const uint64_t tile = (uint64_t)kSpBlock * items_a;
+        // 12288-position tiles (8192: 5.7 ms, measured on the same box)
+        constexpr int kItemsA = 12;
+        const uint64_t tile = (uint64_t)kSpBlock * kItemsA;
         const uint64_t tiles = (n + tile - 1) / tile;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
-        if (items_a == 8)
-            hipLaunchKernelGGL(k_split_text<8>, dim3(grid), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code,
-                               bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
-        else
-            hipLaunchKernelGGL(k_split_text<12>, dim3(grid), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code,
-                               bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
+        const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
+#define SA_TEXT_PASS(P)                                                                                       \
+    hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,       \
+                       (const uint16_t*)c->code, bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0],    \
+                       c->vals_alt, g_hi, cursor)
+        if (pow2) SA_TEXT_PASS(true);
+        else SA_TEXT_PASS(false);
+#undef SA_TEXT_PASS
     }
     tm.end();
     add_bytes(st, SA_K_SCATTER_FIRST, 13 * n);

@@ -294,7 +294,9 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // staged and written.
 // ---------------------------------------------------------------------------
 // (BLOCK 512, two workgroups per CU, measured slower: 5.5 -> 6.3 ms)
-template <int ITEMS, int BLOCK = kSpBlock>
+// POW2: sigma a power of two -- D and the remainder roll by shifts and masks
+// and the bucket is a bit field of D (no multiplications)
+template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -379,8 +381,18 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t l0 = ITEMS * dg;
             uint32_t D = 0;
             uint64_t r = 0;
-            for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
-            for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
+            // POW2: lg = log2 sigma; D < 2^(lg s) <= 2^32, r < 2^(lg R)
+            const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(b.sigma) : 0u;
+            const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
+            const uint64_t rmask = POW2 ? ((1ull << (lg * b.R)) - 1ull) : 0ull;
+            const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;   // bucket = D >> (lg s - bb)
+            if constexpr (POW2) {
+                for (uint32_t q = 0; q < b.s; ++q) D = (D << lg) | s_dc[l0 + q];
+                for (uint32_t q = 0; q < b.R; ++q) r = (r << lg) | s_dc[l0 + b.s + q];
+            } else {
+                for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
+                for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
+            }
             const bool interior = tb + TILE + K <= n;   // every suffix of the tile has >= K symbols
             // the digits leaving D (l0 ..), moving from the remainder into D
             // (l0 + s ..) and entering the remainder (l0 + K ..)
@@ -392,8 +404,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             for (int j = 0; j < ITEMS; ++j) {
                 if (j > 0) {
                     const uint32_t xi = byte_at<ITEMS>(xm, j - 1);
-                    D = (D - byte_at<ITEMS>(xo, j - 1) * (uint32_t)b.pow_s1) * b.sigma + xi;
-                    r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
+                    if constexpr (POW2) {
+                        D = ((D << lg) | xi) & dmask;
+                        r = ((r << lg) | byte_at<ITEMS>(xn, j - 1)) & rmask;
+                    } else {
+                        D = (D - byte_at<ITEMS>(xo, j - 1) * (uint32_t)b.pow_s1) * b.sigma + xi;
+                        r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
+                    }
                 }
                 uint64_t low;
                 if (interior) {
@@ -405,7 +422,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 }
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const bool ok = l0 + j < valid;
-                const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
+                const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 const uint32_t d = ok ? (bk & (RADIX - 1)) : (uint32_t)RADIX;
                 dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
                 if (ok) atomicAdd(&s_hhi[bk >> kLoBits], 1u);
