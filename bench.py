@@ -77,8 +77,9 @@ def parse():
     ap.add_argument("--init-chars", type=int, default=0)
     ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
     ap.add_argument("--round1", default="auto", choices=["auto", "lsd", "bucketed"])
-    ap.add_argument("--mode", default="distributed", choices=["distributed", "replicas"],
-                    help="N > 1: one string over all ranks, or one string per rank")
+    ap.add_argument("--mode", default=None, choices=["distributed", "replicas"],
+                    help="distributed: one string range-partitioned over all ranks (strong scaling; also runs the "
+                         "distributed driver at N = 1); replicas (default): one 1 GiB string per rank (weak scaling)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -261,8 +262,12 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    use_pg = world > 1 or a.mode == "distributed"
+    if use_pg:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29533")
+        os.environ.setdefault("RANK", "0")
+        os.environ.setdefault("WORLD_SIZE", "1")
         dist.init_process_group("nccl", device_id=dev)
 
     def barrier():
@@ -271,7 +276,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    distributed = world > 1 and a.mode == "distributed"
+    distributed = a.mode == "distributed"
     runner = run_distributed if distributed else run_single
     elapsed, extra = runner(a, torch, dev, world, rank, barrier)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -309,7 +314,7 @@ def main():
         if a.json_out:
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

@@ -115,6 +115,8 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) 
 // counted by the first pass itself, k_split_text).  Grid-stride over
 // 4096-position tiles.
 // ---------------------------------------------------------------------------
+// POW2: sigma a power of two (shifts and masks, the bucket a bit field of D)
+template <bool POW2 = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
                                                         uint32_t* __restrict__ ghist) {
@@ -170,16 +172,22 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         __syncthreads();
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
-        for (uint32_t q = 0; q < b.s; ++q) D = D * sig + s_dc[l0 + q];
+        const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(sig) : 0u;
+        const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
+        const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;
+        for (uint32_t q = 0; q < b.s; ++q) D = POW2 ? ((D << lg) | s_dc[l0 + q]) : D * sig + s_dc[l0 + q];
         // the digits leaving (positions l0 .. l0 + 15) and entering (l0 + s ..)
         uint32_t xo[RUN / 4], xi[RUN / 4];
         lds_bytes<RUN>(s_dcw, l0, xo);
         lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
 #pragma unroll
         for (int j = 0; j < RUN; ++j) {
-            if (j > 0) D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
+            if (j > 0) {
+                if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
+                else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
+            }
             if (tb + l0 + j < n) {
-                const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> shh);
+                const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
                 atomicAdd(&s_hlo[bk & (kLoRadix - 1)], 1u);
             }
         }

@@ -88,8 +88,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4u * (uint32_t)c->cus));
-        hipLaunchKernelGGL(k_bucket_hist, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
-                           os_ghist(c));
+        if ((bp.bs.sigma & (bp.bs.sigma - 1)) == 0)
+            hipLaunchKernelGGL(k_bucket_hist<true>, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code,
+                               bp.bs, os_ghist(c));
+        else
+            hipLaunchKernelGGL(k_bucket_hist<false>, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code,
+                               bp.bs, os_ghist(c));
     }
     tm.end();
     add_bytes(st, SA_K_PACK, n);
