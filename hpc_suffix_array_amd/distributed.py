@@ -104,6 +104,14 @@ class HipOps:
                                             ko.data_ptr(), vo.data_ptr(), self._stream()), "sa_sort_pairs_device")
         return ko, vo.to(I64)
 
+    def scatter(self, dst: torch.Tensor, idx: torch.Tensor, base: int, src: torch.Tensor) -> None:
+        """dst[idx - base] = src (int64) by a HIP kernel: torch's index_put
+        faulted on the GPU for 2^30-element int64 targets (1 GiB, world 1)."""
+        assert dst.dtype == I64 and idx.dtype == I64 and src.dtype == I64 and idx.numel() == src.numel()
+        idx, src = idx.contiguous(), src.contiguous()
+        N.check(self.L.sa_scatter_u64_device(dst.data_ptr(), dst.numel(), idx.data_ptr(), base, src.data_ptr(),
+                                             idx.numel(), self._stream()), "sa_scatter_u64_device")
+
 
 class DistributedSA:
     """Distributed builder over an initialised process group."""
@@ -140,8 +148,16 @@ class DistributedSA:
         return outs, recv
 
     def _route(self, dest: torch.Tensor, tensors: List[torch.Tensor]):
-        order = torch.argsort(dest, stable=True)
-        send = torch.bincount(dest, minlength=self.G).tolist()
+        # destination order by the local HIP radix sort (stable), counts by
+        # searching the sorted destinations: torch.bincount over 2^30
+        # elements raised SIGFPE on ROCm (1 GiB, world size 1)
+        if self.G == 1:
+            order = torch.arange(dest.numel(), dtype=I64, device=dest.device)
+            send = [dest.numel()]
+        else:
+            sd, order = self.ops.argsort(dest.to(I64), bit_width(self.G - 1))
+            q = torch.arange(self.G + 1, dtype=I64, device=dest.device)
+            send = torch.diff(torch.searchsorted(sd, q)).tolist()
         outs, recv = self._alltoallv([t[order] for t in tensors], send)
         return outs, recv, order, send
 
@@ -286,7 +302,7 @@ class DistributedSA:
         hpos = self._carry_start(head, gpos, dev)
         rank_local = torch.zeros(hi - lo, dtype=I64, device=dev)
         (ri, rv), _, _, _ = self._route(owner(idx), [idx, hpos + 1])
-        rank_local[ri - lo] = rv
+        self.ops.scatter(rank_local, ri, lo, rv)
         fin_pos, fin_idx = [gpos[single]], [idx[single]]
         keep = ~single
         upos, uidx, uhead = gpos[keep], idx[keep], hpos[keep]
@@ -310,8 +326,8 @@ class DistributedSA:
             (rq,), recv, order, send = self._route(owner(qv), [qv])
             (ans,), _ = self._alltoallv([rank_local[rq - lo]], recv)
             tmp = torch.empty_like(qv)
-            tmp[order] = ans
-            r1[valid] = tmp
+            self.ops.scatter(tmp, order, 0, ans)
+            self.ops.scatter(r1, valid.nonzero().squeeze(1), 0, tmp)
             # dense group id (groups are contiguous in SA order across ranks)
             ghead, _ = self._run_flags([uhead], dev)
             gcount = int(ghead.sum().item())
@@ -334,7 +350,7 @@ class DistributedSA:
             pos = uhead + (uindex - gstart)
             newhead = uhead + (rstart - gstart)
             (ri, rv), _, _, _ = self._route(owner(uidx), [uidx, newhead + 1])
-            rank_local[ri - lo] = rv
+            self.ops.scatter(rank_local, ri, lo, rv)
             fin_pos.append(pos[rsingle])
             fin_idx.append(uidx[rsingle])
             keep = ~rsingle
@@ -347,7 +363,7 @@ class DistributedSA:
         fi = torch.cat(fin_idx)
         (sp, si), _, _, _ = self._route(owner(fp), [fp, fi])
         sa = torch.full((hi - lo,), -1, dtype=I64, device=dev)
-        sa[sp - lo] = si
+        self.ops.scatter(sa, sp, lo, si)
         return sa
 
 

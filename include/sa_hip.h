@@ -155,6 +155,13 @@ int sa_pack_keys_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint
 int sa_sort_pairs_device(sa_context* ctx, const uint64_t* d_keys_in, const uint32_t* d_vals_in, uint64_t m,
                          uint32_t bits, uint64_t* d_keys_out, uint32_t* d_vals_out, void* stream);
 
+/* dst[idx[i] - base] = src[i] for i < m (8-byte values, int64 indices):
+ * the owner-side scatters of the exchange steps (new ranks, SA slices).
+ * Indices outside [base, base + dst_n) are skipped and reported as
+ * SA_E_INVALID; synchronous on `stream`. */
+int sa_scatter_u64_device(uint64_t* d_dst, uint64_t dst_n, const int64_t* d_idx, int64_t base,
+                          const uint64_t* d_src, uint64_t m, void* stream);
+
 /* Seeded synthetic text in device memory: the splitmix64 generator of
  * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
  * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */

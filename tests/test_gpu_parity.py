@@ -217,6 +217,16 @@ def test_distributed_hip_single_rank(gpu, oracle):
             d = DistributedSA(ops)
             sa = gather_sa(d.build(text, len(t)), len(t)).cpu().numpy()
             assert (sa == oracle.sa_c(t).astype(np.int64)).all()
+        # owner-side scatter: in-range writes land, out-of-range ones are refused
+        dst = torch.full((8,), -1, dtype=torch.int64, device="cuda")
+        ops.scatter(dst, torch.tensor([12, 10], dtype=torch.int64, device="cuda"), 10,
+                    torch.tensor([5, 7], dtype=torch.int64, device="cuda"))
+        assert dst.tolist() == [7, -1, 5, -1, -1, -1, -1, -1]
+        from hpc_suffix_array_amd._native import SAError
+        with pytest.raises(SAError):
+            ops.scatter(dst, torch.tensor([9, 18], dtype=torch.int64, device="cuda"), 10,
+                        torch.tensor([1, 2], dtype=torch.int64, device="cuda"))
+        assert dst.tolist() == [7, -1, 5, -1, -1, -1, -1, -1]
     finally:
         dist.destroy_process_group()
 
