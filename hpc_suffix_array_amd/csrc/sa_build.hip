@@ -1177,6 +1177,41 @@ int sa_scatter_u64_device(uint64_t* d_dst, uint64_t dst_n, const int64_t* d_idx,
     return SA_OK;
 }
 
+// dst[i] = src[idx[i] - base]; out-of-range indices write 0 and are counted.
+__global__ __launch_bounds__(256) void k_gather_u64(uint64_t* __restrict__ dst, const uint64_t* __restrict__ src,
+                                                    uint64_t src_n, const int64_t* __restrict__ idx, int64_t base,
+                                                    uint64_t m, unsigned long long* __restrict__ bad) {
+    uint32_t nbad = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t j = (uint64_t)(idx[i] - base);
+        uint64_t v = 0;
+        if (j < src_n) v = src[j];
+        else ++nbad;
+        dst[i] = v;
+    }
+    if (nbad) atomicAdd(bad, (unsigned long long)nbad);
+}
+
+int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n, const int64_t* d_idx, int64_t base,
+                         uint64_t m, void* stream) {
+    if (m == 0) return SA_OK;
+    if (!d_dst || !d_idx || !d_src) return set_err(SA_E_INVALID, "NULL device pointer");
+    hipStream_t s = (hipStream_t)stream;
+    unsigned long long* d_bad = nullptr;
+    unsigned long long bad = 0;
+    SA_HIP(hipMallocAsync((void**)&d_bad, 8, s));
+    SA_HIP(hipMemsetAsync(d_bad, 0, 8, s));
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((m + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_gather_u64, dim3(grid), dim3(256), 0, s, d_dst, d_src, src_n, d_idx, base, m, d_bad);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipFreeAsync(d_bad, s));
+    SA_HIP(hipStreamSynchronize(s));
+    if (bad) return set_err(SA_E_INVALID, "%llu gather indices outside [%lld, %lld)", bad, (long long)base,
+                            (long long)(base + (int64_t)src_n));
+    return SA_OK;
+}
+
 int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8], void* stream) {
     if (!present_out) return set_err(SA_E_INVALID, "present_out is NULL");
     std::memset(present_out, 0, 32);

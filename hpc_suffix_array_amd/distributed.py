@@ -43,6 +43,30 @@ from . import _native as N
 
 I64 = torch.int64
 SAMPLES = 64
+# torch's index / scan kernels are used on slices of at most CHUNK elements:
+# on 2^30-element tensors (1 GiB, world size 1) torch.bincount raised SIGFPE
+# and an index_put faulted on ROCm; permutations go through HIP kernels
+CHUNK = 1 << 26
+
+
+def mask_positions(mask: torch.Tensor) -> torch.Tensor:
+    """int64 positions of the set elements of a bool vector (torch.nonzero
+    over CHUNK-element slices)."""
+    parts = [mask[a: a + CHUNK].nonzero().squeeze(1) + a for a in range(0, mask.numel(), CHUNK)]
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=I64, device=mask.device)
+
+
+def running_max(v: torch.Tensor) -> torch.Tensor:
+    """Inclusive running max of an int64 vector, CHUNK elements per cummax."""
+    out = torch.empty_like(v)
+    carry = None
+    for a in range(0, v.numel(), CHUNK):
+        c, _ = torch.cummax(v[a: a + CHUNK], dim=0)
+        if carry is not None:
+            c = torch.maximum(c, carry)
+        out[a: a + c.numel()] = c
+        carry = c[-1]
+    return out
 
 
 def bit_width(x: int) -> int:
@@ -104,6 +128,16 @@ class HipOps:
                                             ko.data_ptr(), vo.data_ptr(), self._stream()), "sa_sort_pairs_device")
         return ko, vo.to(I64)
 
+    def gather(self, src: torch.Tensor, idx: torch.Tensor, base: int = 0) -> torch.Tensor:
+        """src[idx - base] (int64) by a HIP kernel (torch's index kernels are
+        avoided on 2^30-element tensors, see scatter)."""
+        assert src.dtype == I64 and idx.dtype == I64
+        src, idx = src.contiguous(), idx.contiguous()
+        out = torch.empty(idx.numel(), dtype=I64, device=idx.device)
+        N.check(self.L.sa_gather_u64_device(out.data_ptr(), src.data_ptr(), src.numel(), idx.data_ptr(), base,
+                                            idx.numel(), self._stream()), "sa_gather_u64_device")
+        return out
+
     def scatter(self, dst: torch.Tensor, idx: torch.Tensor, base: int, src: torch.Tensor) -> None:
         """dst[idx - base] = src (int64) by a HIP kernel: torch's index_put
         faulted on the GPU for 2^30-element int64 targets (1 GiB, world 1)."""
@@ -151,14 +185,14 @@ class DistributedSA:
         # destination order by the local HIP radix sort (stable), counts by
         # searching the sorted destinations: torch.bincount over 2^30
         # elements raised SIGFPE on ROCm (1 GiB, world size 1)
-        if self.G == 1:
+        if self.G == 1:   # everything stays: no permutation, no exchange
             order = torch.arange(dest.numel(), dtype=I64, device=dest.device)
-            send = [dest.numel()]
+            return list(tensors), [dest.numel()], order, [dest.numel()]
         else:
             sd, order = self.ops.argsort(dest.to(I64), bit_width(self.G - 1))
             q = torch.arange(self.G + 1, dtype=I64, device=dest.device)
             send = torch.diff(torch.searchsorted(sd, q)).tolist()
-        outs, recv = self._alltoallv([t[order] for t in tensors], send)
+        outs, recv = self._alltoallv([self.ops.gather(t, order) for t in tensors], send)
         return outs, recv, order, send
 
     # -- sorting ---------------------------------------------------------------
@@ -168,7 +202,7 @@ class DistributedSA:
         segment and the segment's global offset."""
         dev = keys.device
         keys, perm = self.ops.argsort(keys, bits)
-        payloads = [p[perm] for p in payloads]
+        payloads = [self.ops.gather(p, perm) for p in payloads]
         m = keys.numel()
         # samples (key, rank, position, valid)
         s = min(SAMPLES, m)
@@ -204,7 +238,7 @@ class DistributedSA:
         outs, _ = self._alltoallv([keys] + payloads, send)
         keys, payloads = outs[0], outs[1:]
         keys, perm = self.ops.argsort(keys, bits)
-        payloads = [p[perm] for p in payloads]
+        payloads = [self.ops.gather(p, perm) for p in payloads]
         sizes = self._gather(torch.tensor([keys.numel()], dtype=I64, device=dev)).reshape(-1).tolist()
         off = sum(sizes[: self.r])
         return keys, payloads, off, sizes
@@ -254,13 +288,13 @@ class DistributedSA:
         """For each element the value of idx at the last head at or before it
         (scanning across ranks)."""
         m = head.numel()
-        local_last = int(idx[head].max().item()) if m and bool(head.any()) else -1
+        local_last = int(torch.where(head, idx, torch.full_like(idx, -1)).max().item()) if m else -1
         lasts = self._gather(torch.tensor([local_last], dtype=I64, device=dev)).reshape(-1).tolist()
         carry = max([-1] + lasts[: self.r])
         if m == 0:
             return idx
         v = torch.where(head, idx, torch.full_like(idx, -1))
-        v, _ = torch.cummax(v, dim=0)
+        v = running_max(v)
         return torch.where(v < 0, torch.full_like(v, carry), v)
 
     # -- the build ----------------------------------------------------------------
@@ -303,9 +337,11 @@ class DistributedSA:
         rank_local = torch.zeros(hi - lo, dtype=I64, device=dev)
         (ri, rv), _, _, _ = self._route(owner(idx), [idx, hpos + 1])
         self.ops.scatter(rank_local, ri, lo, rv)
-        fin_pos, fin_idx = [gpos[single]], [idx[single]]
+        sel = mask_positions(single)
+        fin_pos, fin_idx = [self.ops.gather(gpos, sel)], [self.ops.gather(idx, sel)]
         keep = ~single
-        upos, uidx, uhead = gpos[keep], idx[keep], hpos[keep]
+        sel = mask_positions(keep)
+        upos, uidx, uhead = (self.ops.gather(t, sel) for t in (gpos, idx, hpos))
         D = self._sum(int(head.sum().item()), dev)
         self.stats["rounds"] = 1
         self.stats["distinct"].append(D)
@@ -322,12 +358,13 @@ class DistributedSA:
             q = uidx + h
             valid = q < n
             r1 = torch.zeros_like(uidx)
-            qv = q[valid]
+            vsel = mask_positions(valid)
+            qv = self.ops.gather(q, vsel)
             (rq,), recv, order, send = self._route(owner(qv), [qv])
-            (ans,), _ = self._alltoallv([rank_local[rq - lo]], recv)
+            (ans,), _ = self._alltoallv([self.ops.gather(rank_local, rq, lo)], recv)
             tmp = torch.empty_like(qv)
             self.ops.scatter(tmp, order, 0, ans)
-            self.ops.scatter(r1, valid.nonzero().squeeze(1), 0, tmp)
+            self.ops.scatter(r1, vsel, 0, tmp)
             # dense group id (groups are contiguous in SA order across ranks)
             ghead, _ = self._run_flags([uhead], dev)
             gcount = int(ghead.sum().item())
@@ -351,13 +388,15 @@ class DistributedSA:
             newhead = uhead + (rstart - gstart)
             (ri, rv), _, _, _ = self._route(owner(uidx), [uidx, newhead + 1])
             self.ops.scatter(rank_local, ri, lo, rv)
-            fin_pos.append(pos[rsingle])
-            fin_idx.append(uidx[rsingle])
+            sel = mask_positions(rsingle)
+            fin_pos.append(self.ops.gather(pos, sel))
+            fin_idx.append(self.ops.gather(uidx, sel))
             keep = ~rsingle
             D = (n - total_u) + self._sum(int(rhead.sum().item()), dev)
             self.stats["rounds"] += 1
             self.stats["distinct"].append(D)
-            upos, uidx, uhead = pos[keep], uidx[keep], newhead[keep]
+            sel = mask_positions(keep)
+            upos, uidx, uhead = (self.ops.gather(t, sel) for t in (pos, uidx, newhead))
             h *= 2
         fp = torch.cat(fin_pos)
         fi = torch.cat(fin_idx)

@@ -162,6 +162,12 @@ int sa_sort_pairs_device(sa_context* ctx, const uint64_t* d_keys_in, const uint3
 int sa_scatter_u64_device(uint64_t* d_dst, uint64_t dst_n, const int64_t* d_idx, int64_t base,
                           const uint64_t* d_src, uint64_t m, void* stream);
 
+/* dst[i] = src[idx[i] - base] for i < m (8-byte values, int64 indices):
+ * the permutations of the exchange steps.  Indices outside
+ * [base, base + src_n) read 0 and are reported as SA_E_INVALID. */
+int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n, const int64_t* d_idx, int64_t base,
+                         uint64_t m, void* stream);
+
 /* Seeded synthetic text in device memory: the splitmix64 generator of
  * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
  * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */

@@ -2,7 +2,7 @@
 driver (hpc_suffix_array_amd/distributed.py) run under gloo on CPU so its
 exchange logic is tested without a GPU.  Mirrors the three local operations
 of libsa_hip the driver calls: sa_alphabet_device, sa_pack_keys_device,
-sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device."""
+sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device, sa_gather_u64_device."""
 import torch
 
 I64 = torch.int64
@@ -36,3 +36,8 @@ class CpuOps:
         j = idx - base
         assert bool(((j >= 0) & (j < dst.numel())).all())
         dst[j] = src
+
+    def gather(self, src, idx, base=0):
+        j = idx - base
+        assert bool(((j >= 0) & (j < src.numel())).all())
+        return src[j]
