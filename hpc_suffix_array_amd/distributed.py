@@ -47,6 +47,8 @@ SAMPLES = 64
 # on 2^30-element tensors (1 GiB, world size 1) torch.bincount raised SIGFPE
 # and an index_put faulted on ROCm; permutations go through HIP kernels
 CHUNK = 1 << 26
+# elements per peer pair in one all_to_all_single (see _alltoallv)
+XCHUNK = 1 << 25
 
 
 def mask_positions(mask: torch.Tensor) -> torch.Tensor:
@@ -169,15 +171,42 @@ class DistributedSA:
         return int(t.item())
 
     def _alltoallv(self, tensors: List[torch.Tensor], send: List[int]) -> Tuple[List[torch.Tensor], List[int]]:
+        """all_to_all_v of each tensor (send[j] elements to rank j, in rank
+        order).  Each collective moves at most XCHUNK elements per peer pair:
+        one all_to_all_single of 2^28 int64 (2 GiB) returned half garbage on
+        RCCL (a 32-bit byte count), so larger exchanges run in slices, the
+        slice count agreed by a MAX all_reduce."""
         dev = tensors[0].device
+        if self.G == 1:
+            return list(tensors), list(send)
         sc = torch.tensor(send, dtype=I64, device=dev)
         rc = torch.empty_like(sc)
         dist.all_to_all_single(rc, sc, group=self.group)
         recv = rc.tolist()
+        C = XCHUNK
+        t_loc = torch.tensor([max([0] + [(x + C - 1) // C for x in send + recv])], dtype=I64, device=dev)
+        dist.all_reduce(t_loc, op=dist.ReduceOp.MAX, group=self.group)
+        T = int(t_loc.item())
+        so = [sum(send[:j]) for j in range(self.G)]
+        ro = [sum(recv[:j]) for j in range(self.G)]
         outs = []
         for t in tensors:
+            t = t.contiguous()
             o = torch.empty(sum(recv), dtype=t.dtype, device=dev)
-            dist.all_to_all_single(o, t.contiguous(), recv, list(send), group=self.group)
+            if T <= 1:
+                dist.all_to_all_single(o, t, recv, list(send), group=self.group)
+                outs.append(o)
+                continue
+            for k in range(T):
+                sl = [min(C, max(0, x - k * C)) for x in send]
+                rl = [min(C, max(0, x - k * C)) for x in recv]
+                inp = torch.cat([t[so[j] + k * C: so[j] + k * C + sl[j]] for j in range(self.G)])
+                got = torch.empty(sum(rl), dtype=t.dtype, device=dev)
+                dist.all_to_all_single(got, inp, rl, sl, group=self.group)
+                a = 0
+                for j in range(self.G):
+                    o[ro[j] + k * C: ro[j] + k * C + rl[j]] = got[a: a + rl[j]]
+                    a += rl[j]
             outs.append(o)
         return outs, recv
 
@@ -407,12 +436,20 @@ class DistributedSA:
 
 
 def gather_sa(sa_local: torch.Tensor, n: int, group=None) -> torch.Tensor:
-    """Concatenate the SA slices of all ranks (every rank gets the full SA)."""
+    """Concatenate the SA slices of all ranks (every rank gets the full SA);
+    all_gathers of at most CHUNK elements per rank (see _alltoallv)."""
     G = dist.get_world_size(group)
     sizes = [n * (q + 1) // G - n * q // G for q in range(G)]
+    if G == 1:
+        return sa_local[: sizes[0]]
     m = max(sizes)
     buf = torch.full((m,), -1, dtype=I64, device=sa_local.device)
     buf[: sa_local.numel()] = sa_local
-    out = [torch.empty_like(buf) for _ in range(G)]
-    dist.all_gather(out, buf, group=group)
-    return torch.cat([o[: sizes[q]] for q, o in enumerate(out)])
+    full = torch.empty(G * m, dtype=I64, device=sa_local.device)
+    for a in range(0, m, CHUNK):
+        b = min(m, a + CHUNK)
+        out = [torch.empty(b - a, dtype=I64, device=buf.device) for _ in range(G)]
+        dist.all_gather(out, buf[a:b].contiguous(), group=group)
+        for q in range(G):
+            full[q * m + a: q * m + b] = out[q]
+    return torch.cat([full[q * m: q * m + sizes[q]] for q in range(G)])

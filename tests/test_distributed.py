@@ -36,7 +36,7 @@ def _texts():
     }
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, chunks=None):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -44,7 +44,10 @@ def _worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
     from dist_cpu_ops import CpuOps
+    from hpc_suffix_array_amd import distributed as D
     from hpc_suffix_array_amd.distributed import DistributedSA, gather_sa
+    if chunks:
+        D.XCHUNK, D.CHUNK = chunks
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = {}
@@ -60,12 +63,11 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_distributed_gloo(oracle, world):
+def _run(oracle, world, chunks=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -77,6 +79,11 @@ def test_distributed_gloo(oracle, world):
         want = oracle.sa_c(t)
         assert (sa == want.astype(np.int64)).all(), (name, world)
         assert st["distinct"][-1] == len(t), name
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_gloo(oracle, world):
+    _run(oracle, world)
 
 
 def test_choose_chars_keeps_int64_keys():
@@ -99,3 +106,8 @@ def test_chunked_helpers(monkeypatch):
         v = torch.randint(-5, 100, (n,), generator=g)
         if n:
             assert torch.equal(D.running_max(v), torch.cummax(v, 0)[0])
+
+
+def test_distributed_gloo_sliced_exchange(oracle):
+    """The sliced all_to_all_v / all_gather paths (XCHUNK, CHUNK tiny)."""
+    _run(oracle, 3, chunks=(97, 1000))
