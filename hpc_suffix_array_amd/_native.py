@@ -32,7 +32,7 @@ DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_a
 EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", "sa_build_device",
                "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
-               "sa_gather_u64_device",
+               "sa_gather_u64_device", "sa_running_max_i64_device",
                "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
 
 
@@ -146,6 +146,8 @@ def lib() -> ctypes.CDLL:
     L.sa_scatter_u64_device.restype = i32
     L.sa_gather_u64_device.argtypes = [vp, vp, u64, vp, ctypes.c_int64, u64, vp]
     L.sa_gather_u64_device.restype = i32
+    L.sa_running_max_i64_device.argtypes = [vp, u64, vp]
+    L.sa_running_max_i64_device.restype = i32
     L.sa_generate_text_device.argtypes = [vp, u64, u64, ctypes.c_char_p, ctypes.c_uint32, vp]
     L.sa_generate_text_device.restype = i32
     L.sa_last_error.argtypes = []

@@ -1212,6 +1212,96 @@ int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n,
     return SA_OK;
 }
 
+// Inclusive running max of m int64 values, in place: per-tile maxima
+// (256 lanes x 16 contiguous values), one workgroup scans the tile maxima,
+// each tile then scans itself from its carry.
+constexpr int kRmBlock = 256, kRmItems = 16, kRmTile = kRmBlock * kRmItems;
+
+__device__ inline int64_t rm_block_incl(int64_t v, int64_t* s_w) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(v, o, 64);
+        if (lane >= o && y > v) v = y;
+    }
+    if (lane == 63) s_w[w] = v;
+    __syncthreads();
+    for (int q = 0; q < w; ++q) v = s_w[q] > v ? s_w[q] : v;
+    return v;
+}
+
+// exclusive block max: the inclusive max of the previous lane
+__device__ inline int64_t rm_block_excl(int64_t v, int64_t* s_w) {
+    const int64_t incl = rm_block_incl(v, s_w);
+    int64_t c = __shfl_up(incl, 1, 64);
+    if ((threadIdx.x & 63) == 0) {
+        c = INT64_MIN;
+        for (int q = 0; q < (int)(threadIdx.x >> 6); ++q) c = s_w[q] > c ? s_w[q] : c;
+    }
+    return c;
+}
+
+__global__ __launch_bounds__(kRmBlock) void k_rmax_tiles(const int64_t* __restrict__ v, uint64_t m,
+                                                         int64_t* __restrict__ tmax) {
+    __shared__ int64_t s_w[kRmBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
+    int64_t x = INT64_MIN;
+    for (int j = 0; j < kRmItems; ++j)
+        if (b0 + j < m) x = v[b0 + j] > x ? v[b0 + j] : x;
+    x = rm_block_incl(x, s_w);
+    if (threadIdx.x == kRmBlock - 1) tmax[blockIdx.x] = x;
+}
+
+// exclusive running max of the tile maxima (one workgroup of kRmBlock lanes)
+__global__ __launch_bounds__(kRmBlock) void k_rmax_carry(int64_t* __restrict__ tmax, uint64_t tiles) {
+    __shared__ int64_t s_w[kRmBlock / 64];
+    const uint64_t per = (tiles + kRmBlock - 1) / kRmBlock;
+    const uint64_t a = (uint64_t)threadIdx.x * per, e = a + per < tiles ? a + per : tiles;
+    int64_t x = INT64_MIN;
+    for (uint64_t i = a; i < e; ++i) x = tmax[i] > x ? tmax[i] : x;
+    int64_t c = rm_block_excl(x, s_w);
+    for (uint64_t i = a; i < e; ++i) {
+        const int64_t y = tmax[i];
+        tmax[i] = c;
+        c = y > c ? y : c;
+    }
+}
+
+__global__ __launch_bounds__(kRmBlock) void k_rmax_apply(int64_t* __restrict__ v, uint64_t m,
+                                                         const int64_t* __restrict__ tcarry) {
+    __shared__ int64_t s_w[kRmBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
+    int64_t r[kRmItems];
+    int64_t x = INT64_MIN;
+    for (int j = 0; j < kRmItems; ++j) {
+        r[j] = b0 + j < m ? v[b0 + j] : INT64_MIN;
+        x = r[j] > x ? r[j] : x;
+    }
+    int64_t c = rm_block_excl(x, s_w);
+    const int64_t tc = tcarry[blockIdx.x];
+    c = tc > c ? tc : c;
+    for (int j = 0; j < kRmItems; ++j) {
+        c = r[j] > c ? r[j] : c;
+        if (b0 + j < m) v[b0 + j] = c;
+    }
+}
+
+int sa_running_max_i64_device(int64_t* d_v, uint64_t m, void* stream) {
+    if (m == 0) return SA_OK;
+    if (!d_v) return set_err(SA_E_INVALID, "NULL device pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const uint64_t tiles = (m + kRmTile - 1) / kRmTile;
+    if (tiles > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "m too large");
+    int64_t* d_t = nullptr;
+    SA_HIP(hipMallocAsync((void**)&d_t, tiles * 8, s));
+    hipLaunchKernelGGL(k_rmax_tiles, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
+    hipLaunchKernelGGL(k_rmax_carry, dim3(1), dim3(kRmBlock), 0, s, d_t, tiles);
+    hipLaunchKernelGGL(k_rmax_apply, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipFreeAsync(d_t, s));
+    return SA_OK;
+}
+
 int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8], void* stream) {
     if (!present_out) return set_err(SA_E_INVALID, "present_out is NULL");
     std::memset(present_out, 0, 32);

@@ -168,6 +168,10 @@ int sa_scatter_u64_device(uint64_t* d_dst, uint64_t dst_n, const int64_t* d_idx,
 int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n, const int64_t* d_idx, int64_t base,
                          uint64_t m, void* stream);
 
+/* In-place inclusive running max of m int64 values (the group-start
+ * carries of the distributed re-rank); asynchronous on `stream`. */
+int sa_running_max_i64_device(int64_t* d_v, uint64_t m, void* stream);
+
 /* Seeded synthetic text in device memory: the splitmix64 generator of
  * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
  * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */

@@ -2,7 +2,7 @@
 driver (hpc_suffix_array_amd/distributed.py) run under gloo on CPU so its
 exchange logic is tested without a GPU.  Mirrors the three local operations
 of libsa_hip the driver calls: sa_alphabet_device, sa_pack_keys_device,
-sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device, sa_gather_u64_device."""
+sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device, sa_gather_u64_device, sa_running_max_i64_device."""
 import torch
 
 I64 = torch.int64
@@ -41,3 +41,6 @@ class CpuOps:
         j = idx - base
         assert bool(((j >= 0) & (j < src.numel())).all())
         return src[j]
+
+    def running_max(self, v):
+        return torch.cummax(v, 0)[0] if v.numel() else v.clone()

@@ -95,7 +95,7 @@ def test_choose_chars_keeps_int64_keys():
 
 
 def test_chunked_helpers(monkeypatch):
-    """mask_positions / running_max agree with torch when split into slices."""
+    """mask_positions agrees with torch.nonzero when split into slices."""
     import torch
     from hpc_suffix_array_amd import distributed as D
     monkeypatch.setattr(D, "CHUNK", 7)
@@ -103,9 +103,6 @@ def test_chunked_helpers(monkeypatch):
     for n in (0, 1, 6, 7, 8, 50):
         mask = torch.rand(n, generator=g) < 0.4
         assert torch.equal(D.mask_positions(mask), mask.nonzero().squeeze(1))
-        v = torch.randint(-5, 100, (n,), generator=g)
-        if n:
-            assert torch.equal(D.running_max(v), torch.cummax(v, 0)[0])
 
 
 def test_distributed_gloo_sliced_exchange(oracle):

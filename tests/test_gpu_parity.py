@@ -217,6 +217,13 @@ def test_distributed_hip_single_rank(gpu, oracle):
             d = DistributedSA(ops)
             sa = gather_sa(d.build(text, len(t)), len(t)).cpu().numpy()
             assert (sa == oracle.sa_c(t).astype(np.int64)).all()
+        # running max across tile boundaries (4096 values per tile)
+        g = torch.Generator().manual_seed(5)
+        for m in (1, 63, 4096, 4097, 300_001):
+            v = torch.randint(-1, 1 << 40, (m,), generator=g, dtype=torch.int64)
+            v[torch.rand(m, generator=g) < 0.7] = -1
+            got = ops.running_max(v.cuda()).cpu()
+            assert torch.equal(got, torch.cummax(v, 0)[0]), m
         # owner-side scatter: in-range writes land, out-of-range ones are refused
         dst = torch.full((8,), -1, dtype=torch.int64, device="cuda")
         ops.scatter(dst, torch.tensor([12, 10], dtype=torch.int64, device="cuda"), 10,
