@@ -521,6 +521,11 @@ static uint32_t choose_chars(uint32_t sigma, uint64_t n, int32_t req) {
     return K;
 }
 
+// unsorted-set rounds try the per-group register sort when the average
+// group holds at most kUsAvg suffixes; its oversize flag lives in words[12]
+constexpr uint64_t kUsAvg = 4;
+constexpr int kUsFlagWord = 12;
+
 template <class Pos>
 static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
                     bool sparse_ok, bool* sparse_out,
@@ -673,8 +678,36 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         const Chunking cu = plan_chunks(m);
         const int ui = uo;
         uo ^= 1;
-        uint64_t* sorted;
-        if (c->radix == 0) {
+        uint64_t* sorted = nullptr;
+        if (c->radix == 0 && G > 0 && m <= kUsAvg * G) {
+            // small groups on average: sort each group in registers, unless
+            // one of them is larger than kUsLimit (then the radix sort below)
+            SA_HIP(hipMemsetAsync(c->words + kUsFlagWord, 0, 4, s));
+            const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
+            tm.begin(SA_K_SORT_U);
+            if (sparse)
+                hipLaunchKernelGGL(k_usort_small<SrcU<true>>, dim3(grid), dim3(kBlock), 0, s,
+                                   SrcU<true>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, c->u_g[ui], m, ukb0, c->vals_u,
+                                   c->words + kUsFlagWord);
+            else
+                hipLaunchKernelGGL(k_usort_small<SrcU<false>>, dim3(grid), dim3(kBlock), 0, s,
+                                   SrcU<false>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, c->u_g[ui], m, ukb0, c->vals_u,
+                                   c->words + kUsFlagWord);
+            tm.end();
+            SA_HIP(hipGetLastError());
+            SA_HIP(hipMemcpyAsync(c->host_words + kUsFlagWord, c->words + kUsFlagWord, 4, hipMemcpyDeviceToHost, s));
+            SA_HIP(hipStreamSynchronize(s));
+            add_bytes(st, SA_K_SORT_U, 28 * m);
+            if (c->host_words[kUsFlagWord] == 0) {
+                sorted = ukb0;
+                P = 1;
+            }
+            SA_TRACE("  round h=%llu: per-group register sort %s", (unsigned long long)h,
+                     sorted ? "done" : "found a large group");
+        }
+        if (sorted) {
+            rc = SA_OK;
+        } else if (c->radix == 0) {
             // keys (g, rank[i + h]) once into ukb1 -- the first pass reads them
             // from there and the second overwrites them -- with the digit totals
             rc = onesweep_prepare(c, s);

@@ -183,6 +183,71 @@ struct SrcU {
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
 };
 
+// An unsorted-set round whose groups are all small (most are pairs on
+// random text): each group -- a run of equal u_g, contiguous in SA order --
+// is sorted by its keys (g, rank[i + h]) in registers by the lane at its
+// first member, instead of a full LSD radix sort of the set.  Groups larger
+// than kUsLimit set *flag and are left unwritten (the caller then runs the
+// radix sort).  Equal keys may come out in any order: the round only needs
+// the classes of equal keys and their order, later rounds re-sort ties.
+constexpr int kUsLimit = 8;
+
+__device__ __forceinline__ void us_cx(uint64_t& ka, uint32_t& va, uint64_t& kb, uint32_t& vb) {
+    if (kb < ka) {
+        const uint64_t tk = ka;
+        ka = kb;
+        kb = tk;
+        const uint32_t tv = va;
+        va = vb;
+        vb = tv;
+    }
+}
+
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_usort_small(Src src, const uint32_t* __restrict__ u_g, uint64_t m,
+                                                        uint64_t* __restrict__ out_keys,
+                                                        uint32_t* __restrict__ out_vals, uint32_t* __restrict__ flag) {
+    for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < m; s += (uint64_t)gridDim.x * kBlock) {
+        const uint32_t g = u_g[s];
+        if (s > 0 && u_g[s - 1] == g) continue;
+        uint32_t len = 1;
+        while (len <= kUsLimit && s + len < m && u_g[s + len] == g) ++len;
+        if (len > kUsLimit) {
+            atomicOr(flag, 1u);
+            continue;
+        }
+        uint64_t k[kUsLimit];
+        uint32_t v[kUsLimit];
+#pragma unroll
+        for (int j = 0; j < kUsLimit; ++j) {
+            k[j] = ~0ull;
+            v[j] = 0;
+            if ((uint32_t)j < len) {
+                k[j] = src.key(s + j);
+                v[j] = src.val(s + j);
+            }
+        }
+        // Batcher odd-even merge sort of 8 (19 compare-exchanges)
+        us_cx(k[0], v[0], k[1], v[1]); us_cx(k[2], v[2], k[3], v[3]);
+        us_cx(k[4], v[4], k[5], v[5]); us_cx(k[6], v[6], k[7], v[7]);
+        us_cx(k[0], v[0], k[2], v[2]); us_cx(k[1], v[1], k[3], v[3]);
+        us_cx(k[4], v[4], k[6], v[6]); us_cx(k[5], v[5], k[7], v[7]);
+        us_cx(k[1], v[1], k[2], v[2]); us_cx(k[5], v[5], k[6], v[6]);
+        us_cx(k[0], v[0], k[4], v[4]); us_cx(k[1], v[1], k[5], v[5]);
+        us_cx(k[2], v[2], k[6], v[6]); us_cx(k[3], v[3], k[7], v[7]);
+        us_cx(k[2], v[2], k[4], v[4]); us_cx(k[3], v[3], k[5], v[5]);
+        us_cx(k[1], v[1], k[2], v[2]); us_cx(k[3], v[3], k[4], v[4]);
+        us_cx(k[5], v[5], k[6], v[6]);
+#pragma unroll
+        for (int j = 0; j < kUsLimit; ++j) {
+            if ((uint32_t)j < len) {
+                out_keys[s + j] = k[j];
+                out_vals[s + j] = v[j];
+            }
+        }
+    }
+}
+
 // Later passes: the previous pass's output.
 struct SrcKeys {
     const uint64_t* __restrict__ keys;
