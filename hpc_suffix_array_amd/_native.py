@@ -13,6 +13,8 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG_DIR, "lib", "libsa_hip.so")
+# A/B runs of build variants point SA_LIB_PATH at another in-tree build
+LIB_PATH = os.environ.get("SA_LIB_PATH", LIB_PATH)
 CSRC = os.path.join(PKG_DIR, "csrc")
 
 SA_MAX_ROUNDS = 64

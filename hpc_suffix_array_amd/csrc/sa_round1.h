@@ -9,6 +9,15 @@
 // the full LSD sort of the packed K-symbol key instead.
 #pragma once
 
+// positions / pairs per lane of the two bucket passes (tile = 1024 x items);
+// overridable at build time for A/B runs
+#ifndef SA_ITEMS_A
+#define SA_ITEMS_A 12
+#endif
+#ifndef SA_ITEMS_B
+#define SA_ITEMS_B 10
+#endif
+
 struct BucketPlan {
     BucketSpec bs{};
     uint32_t ib = 0;   // bit width of n - 1 (index bits packed under the key in the local sort)
@@ -113,7 +122,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_SCATTER_FIRST);
     {
         // 12288-position tiles (8192: 5.7 ms, measured on the same box)
-        constexpr int kItemsA = 12;
+        constexpr int kItemsA = SA_ITEMS_A;
         const uint64_t tile = (uint64_t)kSpBlock * kItemsA;
         const uint64_t tiles = (n + tile - 1) / tile;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
@@ -136,7 +145,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         // 12288-pair units cut at the first pass's digit boundaries, places
         // claimed per (low digit, high digit) by atomic cursors (sa_split.h)
-        constexpr int kItemsB = 12;
+        constexpr int kItemsB = SA_ITEMS_B;
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
