@@ -54,7 +54,13 @@ constexpr int kBsBlock = 512;
 constexpr int kBsItems = 18;
 constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
-constexpr uint32_t kBsGrid = 1024;           // workgroups (two per CU resident, the rest queue)
+#ifndef SA_BS_GRID
+#define SA_BS_GRID (1u << 22)
+#endif
+// one workgroup per window: the dispatcher balances the windows (a grid
+// of 1024 workgroups looping over them: 7.90 ms at 2^30, 8192: 7.58,
+// one per window: 7.40; interleaved A/B on one box)
+constexpr uint32_t kBsGrid = SA_BS_GRID;
 constexpr uint64_t kBucketMinN = 1ull << 20; // auto: bucketed first round from 1 Mi suffixes
 // bucket digits: the first pass (unstable, atomic cursors) takes the low
 // kLoBits, the second (stable, look-back) the remaining bb - kLoBits (9 + 8
