@@ -24,6 +24,12 @@
 #include <vector>
 
 #include "../../include/sa_hip.h"
+
+// alphabet kernel workgroups (overridable for A/B runs)
+#ifndef SA_ALPHA_GRID
+#define SA_ALPHA_GRID 2048
+#endif
+
 #include "sa_bucket.h"
 #include "sa_kernels.h"
 #include "sa_lcp.h"
@@ -582,7 +588,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     SA_HIP(hipMemsetAsync(c->alpha, 0, 8 * 4, s));
     tm.begin(SA_K_ALPHABET);
     {
-        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 2048);
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), SA_ALPHA_GRID);
         hipLaunchKernelGGL(k_alphabet, dim3(grid), dim3(kBlock), 0, s, d_text, n, c->alpha);
     }
     tm.end();

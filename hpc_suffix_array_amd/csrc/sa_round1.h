@@ -9,8 +9,13 @@
 // the full LSD sort of the packed K-symbol key instead.
 #pragma once
 
-// positions / pairs per lane of the two bucket passes (tile = 1024 x items);
-// overridable at build time for A/B runs
+// Launch shapes, overridable at build time for A/B runs
+// (scripts/ab_build_variants.sh).  Bucket histogram workgroups per CU: 4 ->
+// 64 took it from 0.62 to 0.47 ms at 2^30 (more waves in flight per CU).
+#ifndef SA_HIST_WPC
+#define SA_HIST_WPC 64
+#endif
+// positions / pairs per lane of the two bucket passes (tile = 1024 x items)
 #ifndef SA_ITEMS_A
 #define SA_ITEMS_A 12
 #endif
@@ -96,7 +101,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_PACK);
     {
         const uint64_t tiles = (n + kTile - 1) / kTile;
-        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 4u * (uint32_t)c->cus));
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
         if ((bp.bs.sigma & (bp.bs.sigma - 1)) == 0)
             hipLaunchKernelGGL(k_bucket_hist<true>, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code,
                                bp.bs, os_ghist(c));

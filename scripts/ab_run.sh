@@ -9,6 +9,6 @@ for v in default "$@" default "$@"; do
 import json,sys
 d=json.loads([l for l in open(sys.argv[2]) if l.startswith('{')][0])
 k=d['kernels_ms_per_step']
-print(sys.argv[1], d['ms_per_step'], d['verified'], 'first', k['scatter_first'], 'second', k['scatter_keys'], 'local', k['local_sort'])
+print(sys.argv[1], d['ms_per_step'], d['verified'], 'alpha', k['alphabet'], 'hist', k['pack'], 'first', k['scatter_first'], 'second', k['scatter_keys'], 'local', k['local_sort'], 'u', k['sort_u'])
 PY
 done
