@@ -51,7 +51,10 @@ namespace sa {
 // overlap the other's sorting (1024 x 9 ran one per CU: 11.1 -> 8.3 ms at
 // 2^30 in microbench_bucket)
 constexpr int kBsBlock = 512;
-constexpr int kBsItems = 18;
+#ifndef SA_BS_ITEMS
+#define SA_BS_ITEMS 18
+#endif
+constexpr int kBsItems = SA_BS_ITEMS;
 constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
 #ifndef SA_BS_GRID
