@@ -228,7 +228,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
                            c->keys[0], d_sa, skew, so);
-        hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
+        // skewed windows are rare: a small grid loops over them (one
+        // workgroup per listed window spent 0.1 ms on empty workgroups)
+        const uint32_t gl = std::min<uint32_t>(g, 1024);
+        hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(gl), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)skew, c->words, bp.ib,
                            c->keys[0], d_sa, so);
     }
