@@ -38,7 +38,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-METRIC = "suffixes sorted/sec + ms/doubling-round, 1 GiB input"
+METRIC = "suffixes sorted/sec + ms/doubling-round, 1 GiB input at 1/2/4/8 MI355X"   # BASELINE.json metric
 
 ALPHABETS = {
     "dna": b"ACGT",
