@@ -72,7 +72,10 @@ static bool trace_on() {
 
 // chunks of the chunked (tile-sequential) kernels: 4096 workgroups keep 16
 // per CU in flight on the 256 CUs
-constexpr uint32_t kMaxChunks = 4096;
+#ifndef SA_MAX_CHUNKS
+#define SA_MAX_CHUNKS 4096
+#endif
+constexpr uint32_t kMaxChunks = SA_MAX_CHUNKS;
 // sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
 constexpr uint64_t kSparseDiv = 8;
 constexpr int kEvPool = 256;

@@ -40,6 +40,26 @@ __device__ __forceinline__ void st_store(uint64_t* p, uint64_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Adds one wave's keys (one per active lane, the active lanes a prefix of
+// the wave) to the LDS digit histograms: per pass, only the first lane of
+// each run of equal digits across neighbouring lanes adds the run's length.
+// Random digits cost one atomic per lane as before; sorted-like keys (the
+// high digits of a degenerate text's unsorted-set rounds) one per run instead
+// of 64 colliding atomics on one bin (k_materialize 13.1 ms per 2^30 keys).
+__device__ __forceinline__ void hist_add_runs(uint32_t (*s_h)[kRadix], uint64_t k, uint32_t passes) {
+    const uint32_t lane = lane_id();
+    const uint32_t nact = (uint32_t)__popcll(__ballot(1));
+    const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    for (uint32_t p = 0; p < passes; ++p) {
+        const uint32_t d = (uint32_t)(k >> (8 * p)) & 0xFFu;
+        const uint32_t dl = __shfl_up(d, 1, 64);
+        const bool head = lane == 0 || dl != d;
+        const uint64_t hm = __ballot(head) & above;
+        const uint32_t next = hm ? (uint32_t)__ffsll((long long)hm) - 1u : nact;
+        if (head) atomicAdd(&s_h[p][d], next - lane);
+    }
+}
+
 // digit histograms of all `passes` 8-bit digits of the source keys
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_global_hist(Src src, uint64_t n, uint32_t passes,
@@ -48,8 +68,7 @@ __global__ __launch_bounds__(kBlock) void k_global_hist(Src src, uint64_t n, uin
     for (int i = threadIdx.x; i < (int)(kMaxPasses * kRadix); i += kBlock) (&s_h[0][0])[i] = 0;
     __syncthreads();
     for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t k = src.key(e);
-        for (uint32_t p = 0; p < passes; ++p) atomicAdd(&s_h[p][(k >> (8 * p)) & 0xFFu], 1u);
+        hist_add_runs(s_h, src.key(e), passes);
     }
     __syncthreads();
     for (uint32_t p = 0; p < passes; ++p) {
@@ -70,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void k_materialize(Src src, uint64_t n, uin
     for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = src.key(e);
         keys[e] = k;
-        for (uint32_t p = 0; p < passes; ++p) atomicAdd(&s_h[p][(k >> (8 * p)) & 0xFFu], 1u);
+        hist_add_runs(s_h, k, passes);
     }
     __syncthreads();
     for (uint32_t p = 0; p < passes; ++p) {
