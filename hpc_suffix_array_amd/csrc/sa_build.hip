@@ -73,7 +73,7 @@ static bool trace_on() {
 // chunks of the chunked (tile-sequential) kernels: 4096 workgroups keep 16
 // per CU in flight on the 256 CUs
 #ifndef SA_MAX_CHUNKS
-#define SA_MAX_CHUNKS 4096
+#define SA_MAX_CHUNKS 4096   // 16384 cut degenerate k_seg_write 317 -> 298 ms but k_scan_chunk_max (sa_lcp.h) scans at most kBlock * 16 = 4096 chunks
 #endif
 constexpr uint32_t kMaxChunks = SA_MAX_CHUNKS;
 // sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
