@@ -86,16 +86,26 @@ def parse():
 
 def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
     """Reference-identical CPU restatement (oracle/mm_oracle.c = the two-pass
-    counting sort of manber_myers.c:15-133), one thread, SA_TIME semantics
-    (build only; create is a memcpy), median of `reps`."""
+    counting sort of manber_myers.c:15-133), one thread pinned to one core
+    (`taskset -c 0`; here sched_setaffinity of this process
+    around the timing), SA_TIME semantics (build only; create is a memcpy),
+    median of `reps`."""
     from oracle import oracle as O
     O.build_oracle()
     t = O.gen_text(kind if kind != "degenerate" else "degenerate", n_sample, seed=seed)
     times, rounds = [], 0
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        _, rounds, _, _ = O.sa_c(t, stats=True)
-        times.append(time.perf_counter() - t0)
+    old = os.sched_getaffinity(0) if hasattr(os, "sched_getaffinity") else None
+    core = min(old) if old else None
+    try:
+        if core is not None:
+            os.sched_setaffinity(0, {core})
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            _, rounds, _, _ = O.sa_c(t, stats=True)
+            times.append(time.perf_counter() - t0)
+    finally:
+        if old is not None:
+            os.sched_setaffinity(0, old)
     med = statistics.median(times)
     model = ""
     try:
@@ -107,8 +117,9 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
     except OSError:
         pass
     return {"value": n_sample / med, "unit": "suffixes/s", "cores": 1, "kind": "port",
-            "sample": f"{kind} n={n_sample} seed={seed}, oracle/mm_oracle.c single thread, "
-                      f"median of {reps} ({med:.2f} s, {rounds} rounds), cpu '{model}'"}
+            "sample": f"{kind} n={n_sample} seed={seed}, oracle/mm_oracle.c single thread pinned to core {core}, "
+                      f"median of {reps} ({med:.2f} s, {rounds} rounds), cpu '{model}', "
+                      f"host cpus {os.cpu_count()}"}
 
 
 def pmc_summary() -> dict | None:
@@ -316,6 +327,10 @@ def main():
                 f.write(line + "\n")
     if use_pg:
         dist.destroy_process_group()
+    # a build that fails the O(n) check must not pass for a measurement
+    if out.get("verified") is False:
+        print("bench.py: the suffix array failed the O(n) check", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

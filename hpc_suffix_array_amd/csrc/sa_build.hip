@@ -15,12 +15,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sa_hip.h"
@@ -73,9 +75,12 @@ static bool trace_on() {
 // chunks of the chunked (tile-sequential) kernels: 4096 workgroups keep 16
 // per CU in flight on the 256 CUs
 #ifndef SA_MAX_CHUNKS
-#define SA_MAX_CHUNKS 4096   // 16384 cut degenerate k_seg_write 317 -> 298 ms but k_scan_chunk_max (sa_lcp.h) scans at most kBlock * 16 = 4096 chunks
+#define SA_MAX_CHUNKS 4096   // 16384 cut degenerate k_seg_write 317 -> 298 ms
 #endif
 constexpr uint32_t kMaxChunks = SA_MAX_CHUNKS;
+// the one-workgroup chunk scans (k_seg_scan, k_scan_heads, k_scan_chunk_max)
+// loop over blocks with a carry; the scratch arrays are sized by kMaxChunks
+static_assert(kMaxChunks >= 1 && kMaxChunks <= (1u << 20), "chunk scratch sized for at most 2^20 chunks");
 // sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
 constexpr uint64_t kSparseDiv = 8;
 constexpr int kEvPool = 256;
@@ -947,6 +952,127 @@ __global__ __launch_bounds__(kBlock) void k_gen_text(uint8_t* __restrict__ out, 
     }
 }
 
+// ---------------------------------------------------------------------------
+// Host <-> HBM copies of the host-pointer entry points (the reference's
+// read_file / create path, utils.c:6-48, hands over pageable malloc memory).
+// Pageable copies are staged by the HIP runtime one piece at a time; here a
+// ring of pinned chunks is filled by several host threads while the DMA
+// engine drains the previous chunk, so the PCIe link stays busy.  Memory the
+// caller already pinned (hipHostMalloc / hipHostRegister) is copied directly.
+// ---------------------------------------------------------------------------
+constexpr size_t kStageChunk = 32ull << 20;
+constexpr int kStageBufs = 3;
+
+static bool host_is_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// memcpy of a large block by up to 8 threads (one core moves ~10 GB/s, the
+// link ~50 GB/s)
+static void par_memcpy(void* dst, const void* src, size_t bytes) {
+    const size_t kPiece = 4ull << 20;
+    const int th = (int)std::min<size_t>(8, (bytes + kPiece - 1) / kPiece);
+    if (th <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::vector<std::thread> pool;
+    const size_t per = (bytes + th - 1) / th;
+    for (int t = 0; t < th; ++t) {
+        const size_t a = (size_t)t * per, e = std::min(bytes, a + per);
+        if (a >= e) break;
+        pool.emplace_back([=] { std::memcpy((char*)dst + a, (const char*)src + a, e - a); });
+    }
+    for (auto& x : pool) x.join();
+}
+
+struct Staging {
+    void* buf[kStageBufs] = {nullptr, nullptr, nullptr};
+    hipEvent_t ev[kStageBufs] = {nullptr, nullptr, nullptr};
+    int make() {
+        for (int i = 0; i < kStageBufs; ++i) {
+            if (hipHostMalloc(&buf[i], kStageChunk, hipHostMallocDefault) != hipSuccess ||
+                hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) {
+                (void)hipGetLastError();
+                return set_err(SA_E_NOMEM, "pinned staging allocation failed");
+            }
+        }
+        return SA_OK;
+    }
+    ~Staging() {
+        for (int i = 0; i < kStageBufs; ++i) {
+            if (buf[i]) hipHostFree(buf[i]);
+            if (ev[i]) hipEventDestroy(ev[i]);
+        }
+    }
+};
+
+static int copy_h2d(void* d_dst, const void* h_src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return SA_OK;
+    if (bytes <= kStageChunk || host_is_pinned(h_src)) {
+        SA_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, s));
+        return SA_OK;
+    }
+    Staging st;
+    int rc = st.make();
+    if (rc) return rc;
+    size_t off = 0;
+    for (int k = 0; off < bytes; ++k, off += kStageChunk) {
+        const int b = k % kStageBufs;
+        const size_t len = std::min(kStageChunk, bytes - off);
+        if (k >= kStageBufs) SA_HIP(hipEventSynchronize(st.ev[b]));   // its previous DMA is done
+        par_memcpy(st.buf[b], (const char*)h_src + off, len);
+        SA_HIP(hipMemcpyAsync((char*)d_dst + off, st.buf[b], len, hipMemcpyHostToDevice, s));
+        SA_HIP(hipEventRecord(st.ev[b], s));
+    }
+    SA_HIP(hipStreamSynchronize(s));
+    return SA_OK;
+}
+
+// conv: 4 = raw u32 copy, 8 = widen u32 -> int64 into the host array
+static int copy_d2h(void* h_dst, const uint32_t* d_src, uint64_t count, int width, hipStream_t s) {
+    const size_t bytes = count * 4;
+    if (count == 0) return SA_OK;
+    if (width == 4 && (bytes <= kStageChunk || host_is_pinned(h_dst))) {
+        SA_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipStreamSynchronize(s));
+        return SA_OK;
+    }
+    Staging st;
+    int rc = st.make();
+    if (rc) return rc;
+    const uint64_t per = kStageChunk / 4;
+    const uint64_t chunks = (count + per - 1) / per;
+    auto issue = [&](uint64_t k) -> int {
+        const int b = (int)(k % kStageBufs);
+        const uint64_t a = k * per, len = std::min(per, count - a);
+        SA_HIP(hipMemcpyAsync(st.buf[b], d_src + a, len * 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipEventRecord(st.ev[b], s));
+        return SA_OK;
+    };
+    for (uint64_t k = 0; k < chunks && k + 1 < (uint64_t)kStageBufs; ++k)
+        if ((rc = issue(k))) return rc;
+    for (uint64_t k = 0; k < chunks; ++k) {
+        const int b = (int)(k % kStageBufs);
+        SA_HIP(hipEventSynchronize(st.ev[b]));
+        if (k + kStageBufs - 1 < chunks && (rc = issue(k + kStageBufs - 1))) return rc;
+        const uint64_t a = k * per, len = std::min(per, count - a);
+        if (width == 4) {
+            par_memcpy((uint32_t*)h_dst + a, st.buf[b], len * 4);
+        } else {
+            const uint32_t* src = (const uint32_t*)st.buf[b];
+            int64_t* o = (int64_t*)h_dst + a;
+            for (uint64_t i = 0; i < len; ++i) o[i] = src[i];
+        }
+    }
+    return SA_OK;
+}
+
 // process-wide context for the host-pointer entry points (lazy, locked)
 static std::mutex g_mu;
 static sa_context* g_ctx = nullptr;
@@ -1089,9 +1215,9 @@ int sa_lcp(const uint8_t* text, uint64_t n, const void* sa, int sa_width, void* 
         (void)hipGetLastError();
         return set_err(SA_E_NOMEM, "device allocation failed");
     }
-    if (hipMemcpy(d_text, text, n, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_sa, src, n * 4, hipMemcpyHostToDevice) != hipSuccess)
-        rc = set_err(SA_E_HIP, "H2D copy failed");
+    if (copy_h2d(d_text, text, n, nullptr) != SA_OK || copy_h2d(d_sa, src, n * 4, nullptr) != SA_OK ||
+        hipStreamSynchronize(nullptr) != hipSuccess)
+        rc = set_err(SA_E_HIP, "H2D copy failed: %s", g_err.c_str());
     // the checker rejects a non-permutation before PHI would scatter through it
     if (rc == SA_OK) {
         rc = check_device(c, d_text, n, d_sa, nullptr);
@@ -1100,18 +1226,7 @@ int sa_lcp(const uint8_t* text, uint64_t n, const void* sa, int sa_width, void* 
     }
     if (rc == SA_OK) rc = lcp_device(c, d_text, n, d_sa, d_lcp, lrs_len, lrs_pos, nullptr);
     if (rc == SA_OK) {
-        if (sa_width == 4) {
-            if (hipMemcpy(lcp_out, d_lcp, n * 4, hipMemcpyDeviceToHost) != hipSuccess)
-                rc = set_err(SA_E_HIP, "D2H copy failed");
-        } else {
-            std::vector<uint32_t> tmp(n);
-            if (hipMemcpy(tmp.data(), d_lcp, n * 4, hipMemcpyDeviceToHost) != hipSuccess) {
-                rc = set_err(SA_E_HIP, "D2H copy failed");
-            } else {
-                int64_t* o = (int64_t*)lcp_out;
-                for (uint64_t i = 0; i < n; ++i) o[i] = tmp[i];
-            }
-        }
+        rc = copy_d2h(lcp_out, d_lcp, n, sa_width, nullptr);
     }
     hipFree(d_text);
     hipFree(d_sa);
@@ -1142,43 +1257,24 @@ int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, con
     }
     SA_TRACE("text/sa allocated");
     hipStream_t s = nullptr;
-    hipEvent_t e0, e1;
-    hipEventCreate(&e0);
-    hipEventCreate(&e1);
-    hipEventRecord(e0, s);
-    hipError_t e = hipMemcpyAsync(d_text, text, n, hipMemcpyHostToDevice, s);
-    hipEventRecord(e1, s);
-    if (e == hipSuccess) e = hipEventSynchronize(e1);
-    float h2d = 0.f;
-    hipEventElapsedTime(&h2d, e0, e1);
-    if (e == hipSuccess) {
-        rc = build_device(c, d_text, n, d_sa, s, opts, stats);
-    } else {
-        rc = set_err(SA_E_HIP, "H2D copy failed: %s", hipGetErrorString(e));
-    }
-    float d2h = 0.f;
+    // PCIe legs timed on the host clock (pinned staging overlaps host copies
+    // with the DMA; sa_stats reports them apart from total_ms)
+    auto t0 = std::chrono::steady_clock::now();
+    rc = copy_h2d(d_text, text, n, s);
+    if (rc == SA_OK) SA_HIP(hipStreamSynchronize(s));
+    auto t1 = std::chrono::steady_clock::now();
+    const double h2d = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (rc == SA_OK) rc = build_device(c, d_text, n, d_sa, s, opts, stats);
+    double d2h = 0.0;
     if (rc == SA_OK) {
-        hipEventRecord(e0, s);
-        if (sa_width == 4) {
-            e = hipMemcpyAsync(sa_out, d_sa, n * 4, hipMemcpyDeviceToHost, s);
-        } else {
-            std::vector<uint32_t> tmp(n);
-            e = hipMemcpyAsync(tmp.data(), d_sa, n * 4, hipMemcpyDeviceToHost, s);
-            if (e == hipSuccess) e = hipStreamSynchronize(s);
-            int64_t* o = (int64_t*)sa_out;
-            for (uint64_t i = 0; i < n; ++i) o[i] = tmp[i];
-        }
-        hipEventRecord(e1, s);
-        if (e == hipSuccess) e = hipEventSynchronize(e1);
-        hipEventElapsedTime(&d2h, e0, e1);
-        if (e != hipSuccess) rc = set_err(SA_E_HIP, "D2H copy failed: %s", hipGetErrorString(e));
+        t0 = std::chrono::steady_clock::now();
+        rc = copy_d2h(sa_out, d_sa, n, sa_width, s);
+        d2h = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     }
     if (stats) {
         stats->h2d_ms = h2d;
         stats->d2h_ms = d2h;
     }
-    hipEventDestroy(e0);
-    hipEventDestroy(e1);
     hipFree(d_text);
     hipFree(d_sa);
     return rc;
@@ -1364,15 +1460,22 @@ int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8
 
 int sa_pack_keys_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint64_t lo, uint64_t hi,
                         const uint16_t code[256], uint64_t base, uint32_t K, uint64_t* d_keys_out, void* stream) {
-    if (!ctx || !d_text || !d_keys_out || !code) return set_err(SA_E_INVALID, "NULL argument");
     if (lo > hi || hi > n) return set_err(SA_E_INVALID, "bad range [%llu, %llu) of %llu", (unsigned long long)lo,
                                           (unsigned long long)hi, (unsigned long long)n);
     if (K == 0 || K >= (uint32_t)kMaxK || base < 2 || key_bits(base, K) > 64)
         return set_err(SA_E_INVALID, "bad packing K=%u base=%llu", K, (unsigned long long)base);
+    // an empty slice (n < world size) writes nothing: a zero-element tensor's
+    // data pointer may be NULL
     if (hi == lo) return SA_OK;
+    if (!ctx || !d_text || !d_keys_out || !code) return set_err(SA_E_INVALID, "NULL argument");
     hipStream_t s = (hipStream_t)stream;
     SA_HIP(hipSetDevice(ctx->device));
-    SA_HIP(hipMemcpyAsync(ctx->code, code, 512, hipMemcpyHostToDevice, s));
+    // the caller's code[] may be a temporary: stage it in the context's pinned
+    // words and wait for the copy before returning
+    uint16_t* h_code = reinterpret_cast<uint16_t*>(ctx->host_words + 320);
+    std::memcpy(h_code, code, 512);
+    SA_HIP(hipMemcpyAsync(ctx->code, h_code, 512, hipMemcpyHostToDevice, s));
+    SA_HIP(hipStreamSynchronize(s));
     uint64_t top = 1;
     for (uint32_t t = 1; t < K; ++t) top *= base;
     const Chunking ch = plan_chunks(hi - lo);
@@ -1453,9 +1556,9 @@ int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width) {
         return set_err(SA_E_NOMEM, "device allocation failed");
     }
     rc = SA_OK;
-    if (hipMemcpy(d_text, text, n, hipMemcpyHostToDevice) != hipSuccess ||
-        hipMemcpy(d_sa, src, n * 4, hipMemcpyHostToDevice) != hipSuccess)
-        rc = set_err(SA_E_HIP, "H2D copy failed");
+    if (copy_h2d(d_text, text, n, nullptr) != SA_OK || copy_h2d(d_sa, src, n * 4, nullptr) != SA_OK ||
+        hipStreamSynchronize(nullptr) != hipSuccess)
+        rc = set_err(SA_E_HIP, "H2D copy failed: %s", g_err.c_str());
     if (rc == SA_OK) rc = check_device(c, d_text, n, d_sa, nullptr);
     hipFree(d_text);
     hipFree(d_sa);

@@ -164,29 +164,39 @@ __global__ __launch_bounds__(kBlock) void k_chunk_max(const uint32_t* __restrict
     }
 }
 
-// exclusive max-scan of the chunk maxima (chunks <= kBlock * 16)
+// exclusive max-scan of the chunk maxima (one workgroup; blocks of kBlock * 16
+// chunks with a carry, so any chunk count is scanned -- SA_MAX_CHUNKS is a
+// build-time override)
 __global__ __launch_bounds__(kBlock) void k_scan_chunk_max(uint32_t* __restrict__ cmax, uint32_t chunks) {
     __shared__ uint32_t s[kWaves];
-    uint32_t x[16], m = 0;
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < chunks; base += kBlock * 16) {
+        uint32_t x[16], m = 0;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t i = threadIdx.x * 16 + j;
-        x[j] = i < chunks ? cmax[i] : 0u;
-        m = m > x[j] ? m : x[j];
-    }
-    const uint32_t inc = wave_inclusive_max(m);
-    if (lane_id() == kWave - 1) s[wave_id()] = inc;
-    __syncthreads();
-    uint32_t run = 0;
-    for (int w = 0; w < (int)wave_id(); ++w) run = run > s[w] ? run : s[w];
-    uint32_t ex = __shfl_up(inc, 1, kWave);
-    if (lane_id() == 0) ex = 0;
-    run = run > ex ? run : ex;
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = base + threadIdx.x * 16 + j;
+            x[j] = i < chunks ? cmax[i] : 0u;
+            m = m > x[j] ? m : x[j];
+        }
+        const uint32_t inc = wave_inclusive_max(m);
+        if (lane_id() == kWave - 1) s[wave_id()] = inc;
+        __syncthreads();
+        uint32_t run = carry, blk = carry;
+        for (int w = 0; w < kWaves; ++w) {
+            if (w < (int)wave_id()) run = run > s[w] ? run : s[w];
+            blk = blk > s[w] ? blk : s[w];
+        }
+        uint32_t ex = __shfl_up(inc, 1, kWave);
+        if (lane_id() == 0) ex = 0;
+        run = run > ex ? run : ex;
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        const uint32_t i = threadIdx.x * 16 + j;
-        if (i < chunks) cmax[i] = run;
-        run = run > x[j] ? run : x[j];
+        for (int j = 0; j < 16; ++j) {
+            const uint32_t i = base + threadIdx.x * 16 + j;
+            if (i < chunks) cmax[i] = run;
+            run = run > x[j] ? run : x[j];
+        }
+        carry = blk;
+        __syncthreads();   // s[] is rewritten by the next block
     }
 }
 

@@ -101,6 +101,8 @@ class HipOps:
     def pack_keys(self, text: torch.Tensor, n: int, lo: int, hi: int, codes: Sequence[int], base: int,
                   K: int) -> torch.Tensor:
         keys = torch.empty(hi - lo, dtype=I64, device=self.dev)
+        if hi == lo:   # an empty slice (n < world size)
+            return keys
         code = (ctypes.c_uint16 * 256)(*codes)
         N.check(self.L.sa_pack_keys_device(self.b.ctx, text.data_ptr(), n, lo, hi, code, base, K, keys.data_ptr(),
                                            self._stream()), "sa_pack_keys_device")

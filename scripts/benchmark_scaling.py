@@ -107,6 +107,9 @@ def main(argv=None):
             print(f"FAILED (exit {p.returncode}): {p.stderr.strip().splitlines()[-1:]}")
             continue
         r = last_json(p.stdout)
+        if r.get("verified") is not True:
+            print(f"REJECTED (suffix array not verified: {r.get('verified')})")
+            continue
         results.append((N, r))
         print(f"OK ({r['ms_per_step']:.2f} ms, {r['value'] / 1e9:.2f} G suffixes/s)")
     if args.dry_run or not results:

@@ -96,3 +96,32 @@ def test_invalid_arguments(sa_lib):
     assert L.sa_build_ex(None, 4, None, 4, None, None) < 0
     assert L.sa_build_ex(ctypes.c_char_p(b"abcd"), 4, None, 3, None, None) < 0
     assert L.sa_context_create(0, 0, None) < 0
+
+
+def test_reference_cli_links_unchanged(sa_lib, tmp_path):
+    """The reference's own caller (src/sequential/main_sequential.c:100-120
+    with src/common/utils.c), compiled from its sources where they lie and
+    linked unchanged against libsa_hip.so (oracle/Makefile ref_cli): every
+    symbol it needs resolves, and without a GPU build_suffix_array aborts with
+    the library's reason instead of falling back to the CPU.  Build container
+    only (the reference tree is absent on the GPU box)."""
+    import os
+    import subprocess
+    ref_src = "/root/reference/src/sequential/main_sequential.c"
+    if not os.path.exists(ref_src):
+        pytest.skip("reference sources absent (GPU box)")
+    if sa_lib.device_count() > 0:
+        pytest.skip("a GPU is visible: the no-device abort is not reachable")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "ref_cli"], check=True)
+    exe = os.path.join(root, "oracle", "_ref", "main_sequential_hip")
+    nm = subprocess.run(["nm", "-u", exe], capture_output=True, text=True, check=True).stdout
+    for sym in sa_lib.DROPIN_SYMBOLS:
+        if sym in ("build_lcp_array", "find_longest_repeated_substring", "is_valid_suffix_array",
+                   "create_suffix_array", "destroy_suffix_array", "build_suffix_array"):
+            assert sym in nm, sym   # resolved from libsa_hip.so, not from the reference
+    f = tmp_path / "banana.txt"
+    f.write_bytes(b"banana")
+    p = subprocess.run([exe, str(f)], capture_output=True, text=True, timeout=60)
+    assert p.returncode != 0
+    assert "libsa_hip: build_suffix_array failed: no HIP device" in p.stderr

@@ -195,6 +195,35 @@ def test_config3_1gib_minus_1_known_answer(gpu, oracle, golden):
     b.close()
 
 
+@pytest.mark.slow
+def test_config5_degenerate_1gib(gpu):
+    """configs[4]: 1 GiB degenerate input ('a' x 2^30) on one MI355X.  The SA
+    is analytic (n-1, ..., 0); the packed schedule takes 26 rounds (first key
+    63 symbols, then h = 63 * 2^j up to 2^31 > 2^30: prefix lengths beyond
+    2^31 are handled in 64 bits; the reference needs 30 rounds,
+    manber_myers.c:97, and cannot run n = 2^30 at all)."""
+    import hashlib
+
+    import torch
+    from hpc_suffix_array_amd import DeviceBuilder
+    n = 1 << 30
+    d_text = torch.full((n,), ord("a"), dtype=torch.uint8, device="cuda")
+    d_sa = torch.empty(n, dtype=torch.int32, device="cuda")
+    b = DeviceBuilder(n)
+    st = b.build(d_text, n, d_sa)
+    assert st["rounds"] == 26, st["rounds"]
+    assert st["prefix_len"][-1] == 63 << 25 and st["distinct"][-1] == n
+    assert st["distinct"][:3] == [63, 126, 252]
+    want = torch.arange(n - 1, -1, -1, dtype=torch.int32, device="cuda")
+    assert torch.equal(d_sa, want)
+    del want
+    assert b.check(d_text, n, d_sa)
+    # the same answer as a hash of the host copy (numpy's reversed arange)
+    got = hashlib.sha256(d_sa.cpu().numpy().tobytes()).hexdigest()
+    assert got == hashlib.sha256(np.arange(n - 1, -1, -1, dtype=np.int32).tobytes()).hexdigest()
+    b.close()
+
+
 def test_distributed_hip_single_rank(gpu, oracle):
     """The multi-GPU driver with the HIP local operations and RCCL
     collectives, at world size 1 (the box has one GPU; world sizes 2-3 run
