@@ -9,9 +9,10 @@ re-rank, read-backs) from text resident in HBM to SA resident in HBM.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--n N] [--kind dna]
 
-N = 1: the single-GPU builder (libsa_hip sa_build_device).
-N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): the
-range-partitioned build of ONE n-symbol string over all ranks
+N = 1: the single-GPU builder (libsa_hip sa_build_device); "scaling":
+"strong" (the 1-GPU point of the strong-scaling curve).
+N > 1 (launched by torch.distributed.run, one process per GPU, RCCL): by
+default the range-partitioned build of ONE n-symbol string over all ranks
 (hpc_suffix_array_amd/distributed.py) -- total work fixed, "scaling":
 "strong"; `--mode replicas` instead builds one string per rank (weak).
 
@@ -78,8 +79,9 @@ def parse():
     ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
     ap.add_argument("--round1", default="auto", choices=["auto", "lsd", "bucketed"])
     ap.add_argument("--mode", default=None, choices=["distributed", "replicas"],
-                    help="distributed: one string range-partitioned over all ranks (strong scaling; also runs the "
-                         "distributed driver at N = 1); replicas (default): one 1 GiB string per rank (weak scaling)")
+                    help="distributed (default for N > 1): one string range-partitioned over all ranks (strong "
+                         "scaling; --mode distributed also runs the distributed driver at N = 1); replicas: one "
+                         "string per rank (weak scaling, opt-in)")
     ap.add_argument("--json-out", default=None)
     return ap.parse_args()
 
@@ -229,15 +231,32 @@ def run_single(a, torch, dev, world, rank, barrier):
 
 
 def run_distributed(a, torch, dev, world, rank, barrier):
-    """One string over all ranks (range-partitioned build, RCCL exchange)."""
+    """One string over all ranks: the range-partitioned build
+    (hpc_suffix_array_amd/distributed.py; every rank holds the text, each
+    sorts the suffixes of its bucket range, rank look-ups cross xGMI by RCCL
+    all_to_all).  Per-phase times are HIP-event spans on the build stream."""
     import torch.distributed as dist
-    from hpc_suffix_array_amd.builder import DeviceBuilder
-    from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, gather_sa
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa
     n = a.n
-    ops = HipOps(max(1, 2 * n // world), dev.index)
+    ops = HipRangeOps(n, dev.index)
     sptr = torch.cuda.current_stream(dev).cuda_stream
-    d_text = make_text(ops.b, n, a.kind, a.seed, dev, sptr)   # same text on every rank
+    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
+    if a.kind == "degenerate":
+        d_text.fill_(ord("a"))
+    else:
+        ops.b.generate_text(d_text, n, ALPHABETS[a.kind], seed=a.seed, stream=sptr)   # same text on every rank
     torch.cuda.synchronize(dev)
+    # the text replicated to every rank, as an RCCL broadcast from rank 0 would
+    # do it (reported, not part of the build: inputs are resident in HBM)
+    bcast_ms = None
+    if world > 1:
+        tmp = d_text.clone()
+        barrier()
+        t0 = time.perf_counter()
+        dist.broadcast(tmp, 0)
+        torch.cuda.synchronize(dev)
+        bcast_ms = 1e3 * (time.perf_counter() - t0)
+        del tmp
     holder = {}
 
     def step():
@@ -247,19 +266,27 @@ def run_distributed(a, torch, dev, world, rank, barrier):
         return d.stats
 
     elapsed, stats = timed(a.steps, a.warmup, step, barrier)
+    sa_local, sa_off = holder["sa"]
+    # verification: the full SA gathered to every rank, O(n) check on rank 0
     verified = None
-    if n < (1 << 31):
-        sa = gather_sa(holder["sa"], n)
+    if n <= 0xFFFFFFFF:
+        sa = gather_sa(sa_local, sa_off, n)
         if rank == 0:
-            chk = DeviceBuilder(n, device=dev.index)
-            verified = chk.check(d_text, n, sa.to(torch.int32))
-            chk.close()
+            verified = ops.b.check(d_text, n, sa.to(torch.int32))
         del sa
-    dist.barrier()
+    if world > 1:
+        v = torch.tensor([1 if verified in (True, None) else 0], dtype=torch.int64, device=dev)
+        dist.broadcast(v, 0)
+        verified = bool(v.item()) if n <= 0xFFFFFFFF else None
     st = stats[-1]
-    extra = {"rounds": st["rounds"], "distinct_per_round": st["distinct"], "unsorted_per_round": st["unsorted"],
-             "init_chars": st["K"], "sigma": st["sigma"], "verified": verified, "roofline": None,
-             "note": "range-partitioned build: local HIP radix sorts, RCCL all_to_all bucket and rank exchange"}
+    m_max = st.get("m_max")
+    extra = {"rounds": st["rounds"], "unsorted_per_round": st.get("unsorted"),
+             "requests_per_round": st.get("requests"), "init_chars": st.get("K"), "sigma": st.get("sigma"),
+             "bucket_bits": st.get("bucket_bits"), "path": st.get("path"), "largest_rank_share": (
+                 round(m_max / (n / world), 4) if m_max else None),
+             "text_broadcast_ms": round(bcast_ms, 3) if bcast_ms else None, "verified": verified, "roofline": None,
+             "note": "range-partitioned build: each rank sorts the suffixes of its bucket range from its text "
+                     "copy; rank requests/answers by RCCL all_to_all between doubling rounds"}
     return elapsed, extra
 
 
@@ -287,7 +314,9 @@ def main():
             dist.barrier()
         torch.cuda.synchronize(dev)
 
-    distributed = a.mode == "distributed"
+    # N > 1 measures the range-partitioned build of ONE string (strong
+    # scaling, BASELINE.json metric at 1/2/4/8 GPUs); replicas are opt-in
+    distributed = a.mode == "distributed" or (a.mode is None and world > 1)
     runner = run_distributed if distributed else run_single
     elapsed, extra = runner(a, torch, dev, world, rank, barrier)
     t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -304,7 +333,7 @@ def main():
         "warmup": a.warmup,
         "ms_per_step": round(ms_per_step, 3),
         "higher_is_better": True,
-        "scaling": "strong" if distributed else "weak",
+        "scaling": "weak" if (world > 1 and not distributed) else "strong",
         "vs_baseline": None,
         "dtype": "u32",
         "data": f"synthetic: seeded splitmix64 {a.kind} text generated in HBM (SURVEY.md 8(d)), seed {a.seed}"

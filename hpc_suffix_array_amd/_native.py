@@ -35,6 +35,8 @@ EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", 
                "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
                "sa_gather_u64_device", "sa_running_max_i64_device",
+               "sa_dist_begin", "sa_dist_cuts", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
+               "sa_dist_answer", "sa_dist_refine",
                "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
 
 
@@ -95,6 +97,20 @@ class SaStats(ctypes.Structure):
         }
 
 
+DIST_OK = 0
+DIST_UNSUPPORTED = 1
+DIST_UNBALANCED = 2
+
+
+class SaDistInfo(ctypes.Structure):
+    """sa_dist_info of include/sa_hip.h (range-partitioned build, per rank)."""
+    _fields_ = [("status", ctypes.c_int32), ("sigma", ctypes.c_int32), ("K", ctypes.c_int32),
+                ("bucket_bits", ctypes.c_int32), ("m", ctypes.c_uint64), ("sa_off", ctypes.c_uint64),
+                ("m_max", ctypes.c_uint64), ("bucket_lo", ctypes.c_uint32), ("bucket_hi", ctypes.c_uint32),
+                ("round1_ok", ctypes.c_int32), ("reserved", ctypes.c_int32), ("heads", ctypes.c_uint64),
+                ("unsorted", ctypes.c_uint64), ("groups", ctypes.c_uint64)]
+
+
 class SuffixArrayStruct(ctypes.Structure):
     """SuffixArray of suffix_array.h:16-21 (32 bytes: str@0 n@8 sa@16 lcp@24)."""
     _fields_ = [("str", ctypes.c_void_p), ("n", ctypes.c_int),
@@ -150,6 +166,17 @@ def lib() -> ctypes.CDLL:
     L.sa_gather_u64_device.restype = i32
     L.sa_running_max_i64_device.argtypes = [vp, u64, vp]
     L.sa_running_max_i64_device.restype = i32
+    DI = ctypes.POINTER(SaDistInfo)
+    L.sa_dist_begin.argtypes = [vp, vp, u64, i32, i32, ctypes.POINTER(ctypes.c_uint32), vp, vp, DI]
+    L.sa_dist_cuts.argtypes = [vp, ctypes.POINTER(u64), DI]
+    L.sa_dist_round1.argtypes = [vp, vp, vp, DI, ctypes.POINTER(SaStats)]
+    L.sa_dist_req_count.argtypes = [vp, u64, ctypes.POINTER(u64), vp, DI]
+    L.sa_dist_req_fill.argtypes = [vp, u64, vp, vp]
+    L.sa_dist_answer.argtypes = [vp, vp, u64, vp, vp]
+    L.sa_dist_refine.argtypes = [vp, u64, vp, vp, vp, DI]
+    for f in (L.sa_dist_begin, L.sa_dist_cuts, L.sa_dist_round1, L.sa_dist_req_count, L.sa_dist_req_fill,
+              L.sa_dist_answer, L.sa_dist_refine):
+        f.restype = i32
     L.sa_generate_text_device.argtypes = [vp, u64, u64, ctypes.c_char_p, ctypes.c_uint32, vp]
     L.sa_generate_text_device.restype = i32
     L.sa_last_error.argtypes = []

@@ -93,7 +93,7 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&tmp, n * 12));
     uint32_t* cnt;
     CK(hipMalloc(&cnt, (2 * nw + 2) * 4));
-    const SegOut so{rank, member, tmp, tmp + n, tmp + 2 * n, cnt, cnt + nw + 1};
+    const SegOut so{rank, member, 0, tmp, tmp + n, tmp + 2 * n, cnt, cnt + nw + 1};
     CK(hipMemset(words, 0, 256));
     const uint64_t cmul = 1;   // bucket = D = key >> rb (17 bits), bsh = 0
     (void)cmul;

@@ -85,15 +85,18 @@ __device__ __forceinline__ uint32_t bucket_dmin(uint32_t b, uint64_t cmul, uint3
 }
 
 // radix source of the second bucket pass (digits of bucket_of(key))
+// (digits of the LOCAL bucket, bucket_of(key) - bofs: bofs = the first bucket
+// of this rank's range in the range-partitioned build, 0 on one GPU)
 struct SrcBucketKeys {
     const uint64_t* __restrict__ keys;
     const uint32_t* __restrict__ vals;
     uint32_t rb, bsh;
     uint64_t cmul;
+    uint32_t bofs;
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return vals[e]; }
     __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
-        return (bucket_of(k, rb, cmul, bsh) >> shift) & mask;
+        return ((bucket_of(k, rb, cmul, bsh) - bofs) >> shift) & mask;
     }
 };
 
@@ -125,26 +128,39 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) 
 // 4096-position tiles.
 // ---------------------------------------------------------------------------
 // POW2: sigma a power of two (shifts and masks, the bucket a bit field of D)
-template <bool POW2 = false>
+// Bucket range (the range-partitioned build, sa_dist.h): only positions in
+// [p0, p1) whose bucket lies in [blo, bhi) are counted, by their LOCAL bucket
+// bk - blo; the single-GPU build passes [0, n) and [0, 2^bb).
+// COARSE: the histogram is of (bucket >> cshift) over kCoarse 64-bit bins
+// (ghist then points at uint64 words) instead of the low kLoBits of the local
+// bucket (the cut plan of sa_dist.h).
+constexpr uint32_t kCoarseBits = 12;
+constexpr uint32_t kCoarse = 1u << kCoarseBits;
+
+template <bool POW2 = false, bool COARSE = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
-                                                        uint32_t* __restrict__ ghist) {
+                                                        uint32_t* __restrict__ ghist, uint64_t p0, uint64_t p1,
+                                                        uint32_t blo, uint32_t bhi) {
     constexpr int RUN = kTile / kBlock;   // 16
+    constexpr uint32_t NB = COARSE ? kCoarse : kLoRadix;
     __shared__ uint8_t s_map[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
     uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
-    __shared__ uint32_t s_hlo[kLoRadix];
+    __shared__ uint32_t s_hlo[NB];
     {
         const uint32_t cv = code[threadIdx.x];
         s_map[threadIdx.x] = (uint8_t)(cv ? cv - 1u : 0u);
     }
-    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock) s_hlo[i] = 0;
+    for (uint32_t i = threadIdx.x; i < NB; i += kBlock) s_hlo[i] = 0;
     const uint32_t sig = b.sigma, ps1 = (uint32_t)b.pow_s1;
     const uint32_t shh = b.bsh;
+    const uint32_t cshift = b.bb > kCoarseBits ? b.bb - kCoarseBits : 0u;
+    const uint32_t bspan = bhi - blo;
     __syncthreads();
-    const uint64_t tiles = (n + kTile - 1) / kTile;
+    const uint64_t tiles = (p1 - p0 + kTile - 1) / kTile;
     for (uint64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
-        const uint64_t tb = tt * kTile;
+        const uint64_t tb = p0 + tt * kTile;
         {
             const uint64_t i = tb + (uint64_t)threadIdx.x * RUN;
             uint32_t w[4];
@@ -195,15 +211,25 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
                 else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
             }
-            if (tb + l0 + j < n) {
+            if (tb + l0 + j < p1) {
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
-                atomicAdd(&s_hlo[bk & (kLoRadix - 1)], 1u);
+                if constexpr (COARSE) {
+                    atomicAdd(&s_hlo[bk >> cshift], 1u);
+                } else {
+                    const uint32_t lb = bk - blo;
+                    if (lb < bspan) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
+                }
             }
         }
         __syncthreads();
     }
-    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock)
-        if (s_hlo[i]) atomicAdd(&ghist[i], s_hlo[i]);
+    for (uint32_t i = threadIdx.x; i < NB; i += kBlock) {
+        if (!s_hlo[i]) continue;
+        if constexpr (COARSE)   // 64-bit bins (all-reduced as int64 by the caller)
+            atomicAdd(reinterpret_cast<unsigned long long*>(ghist) + i, (unsigned long long)s_hlo[i]);
+        else
+            atomicAdd(&ghist[i], s_hlo[i]);
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -472,6 +498,7 @@ __device__ __forceinline__ void store_window(const uint64_t* __restrict__ s_w, u
 struct SegOut {
     uint32_t* rank;
     uint32_t* member;
+    uint64_t rank_off;   // global SA position of this rank's first suffix (0 on one GPU)
     uint32_t* tmp_pos;
     uint32_t* tmp_idx;
     uint32_t* tmp_g;
@@ -564,7 +591,7 @@ __device__ __forceinline__ void window_segments(const uint64_t* __restrict__ s_w
             const uint32_t ku = bu + (uint32_t)((pre >> 32) & 0xFFFFu) + (uint32_t)__popcll(mu & lt);
             const uint32_t kg = bg + (uint32_t)(pre >> 48) + (uint32_t)__popcll(muh & lem) - 1u;
             const uint32_t x = (uint32_t)(s_w[rb0 + lane] & imask);
-            so.rank[x] = (uint32_t)(a + hpos) + 1u;
+            so.rank[x] = (uint32_t)(so.rank_off + a + hpos + 1u);
             atomicOr(&so.member[x >> 5], 1u << (x & 31));
             so.tmp_pos[a + ku] = (uint32_t)(a + rb0 + lane);
             so.tmp_idx[a + ku] = x;
@@ -953,7 +980,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                     if (!eqp && eqn) ++kg;
                     if (eqp || eqn) {
                         const uint32_t xi = (uint32_t)(x & imask);
-                        so.rank[xi] = (uint32_t)(a + head) + 1u;
+                        so.rank[xi] = (uint32_t)(so.rank_off + a + head + 1u);
                         atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
                         so.tmp_pos[a + ku] = (uint32_t)(a + k);
                         so.tmp_idx[a + ku] = xi;

@@ -106,6 +106,8 @@ static Chunking plan_chunks(uint64_t n) {
 
 }  // namespace sa
 
+namespace sa { struct DistState; }
+
 struct sa_context {
     int device = 0;
     uint64_t cap = 0;      // rank / keys / vals_alt capacity (symbols)
@@ -131,9 +133,11 @@ struct sa_context {
     uint32_t* words = nullptr;     // [0..2] = D, m, G; [3] = check error flags
     uint32_t* alpha = nullptr;     // 256 byte counts
     uint16_t* code = nullptr;      // 256 byte -> dense code 1..sigma
-    uint32_t* host_words = nullptr;  // pinned: 64 words, 256 counts, 128 words of codes
+    uint32_t* host_words = nullptr;  // pinned (4096 words): 64 words, 256 counts, 128 words of codes at 320,
+                                     // per-rank counts of the range-partitioned build at 1024
     hipEvent_t ev[sa::kEvPool];
     int ev_ready = 0;
+    sa::DistState* dist = nullptr;   // range-partitioned build state (sa_dist.h)
 };
 
 namespace sa {
@@ -544,7 +548,10 @@ template <class Pos>
 static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
                     bool sparse_ok, bool* sparse_out,
                     uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
-                    uint64_t* G) {
+                    uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0) {
+    // rank_arr / rank_off: the range-partitioned build's n-entry rank array and
+    // its SA offset (sa_dist.h); the context's rank array and 0 on one GPU
+    if (!rank_arr) rank_arr = c->rank;
     uint32_t* c_h = c->counts;
     uint32_t* c_u = c->counts + kMaxChunks;
     uint32_t* c_uh = c->counts + 2 * kMaxChunks;
@@ -572,8 +579,8 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     if (sparse_out) *sparse_out = sparse;
     tm.begin(SA_K_SEG_WRITE);
     hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
-                       (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, c->rank, sa,
-                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1);
+                       (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, rank_arr, sa,
+                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1, (uint32_t)rank_off);
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);
@@ -622,7 +629,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint64_t seg1[3] = {0, 0, 0};
     if (bucketed) {
         bool done = false;
-        rc = round1_bucketed(c, d_text, n, d_sa, bp, s, tm, st, &done, &fused, seg1);
+        rc = round1_bucketed(c, d_text, n, d_sa, bp, full_range(bp, n), s, tm, st, &done, &fused, seg1);
         if (rc) return rc;
         bucketed = done;
         if (done) {
@@ -809,6 +816,8 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     if (st) st->total_ms = elapsed(ev.e[0], ev.e[1]);
     return SA_OK;
 }
+
+#include "sa_dist.h"
 
 // ---------------------------------------------------------------------------
 // O(n) checker (replaces is_valid_suffix_array, manber_myers.c:184-202)
@@ -1124,7 +1133,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
         hipMalloc(&c->segw, (kBstartOff + 2 * kBstartWords) * 4) != hipSuccess ||
-        hipHostMalloc(&c->host_words, 4096, hipHostMallocDefault) != hipSuccess) {
+        hipHostMalloc(&c->host_words, 16384, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
         sa_context_destroy(c);
         return set_err(SA_E_NOMEM, "context allocation failed");
@@ -1150,6 +1159,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
 void sa_context_destroy(sa_context* c) {
     if (!c) return;
     hipSetDevice(c->device);
+    free_dist(c);
     free_ctx_buffers(c);
     free_u_buffers(c);
     hipFree(c->alpha);
@@ -1526,6 +1536,45 @@ int sa_generate_text_device(uint8_t* d_out, uint64_t n, uint64_t seed, const uin
     hipLaunchKernelGGL(k_gen_text, dim3(grid), dim3(kBlock), 0, (hipStream_t)stream, d_out, n, seed, a, sigma);
     SA_HIP(hipGetLastError());
     return SA_OK;
+}
+
+// ---- range-partitioned multi-GPU build (sa_dist.h) ----------------------
+int sa_dist_begin(sa_context* ctx, const uint8_t* d_text, uint64_t n, int world, int rank,
+                  const uint32_t present[8], uint64_t* d_coarse, void* stream, sa_dist_info* info) {
+    if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_begin(ctx, d_text, n, world, rank, present, d_coarse, (hipStream_t)stream, info);
+}
+
+int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info) {
+    if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_cuts(ctx, h_coarse, info);
+}
+
+int sa_dist_round1(sa_context* ctx, uint32_t* d_sa_local, void* stream, sa_dist_info* info, sa_stats* stats) {
+    if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
+    if (!ctx->dist) return set_err(SA_E_INVALID, "sa_dist_round1 before sa_dist_begin");
+    return dist_round1(ctx, ctx->dist->text, d_sa_local, (hipStream_t)stream, info, stats);
+}
+
+int sa_dist_req_count(sa_context* ctx, uint64_t h, uint64_t* counts_out, void* stream, sa_dist_info* info) {
+    if (!ctx || !counts_out || !info) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_req_count(ctx, h, counts_out, (hipStream_t)stream, info);
+}
+
+int sa_dist_req_fill(sa_context* ctx, uint64_t h, uint32_t* d_req, void* stream) {
+    if (!ctx) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_req_fill(ctx, h, d_req, (hipStream_t)stream);
+}
+
+int sa_dist_answer(sa_context* ctx, const uint32_t* d_req, uint64_t nreq, uint64_t* d_ans, void* stream) {
+    if (!ctx) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_answer(ctx, d_req, nreq, d_ans, (hipStream_t)stream);
+}
+
+int sa_dist_refine(sa_context* ctx, uint64_t h, const uint64_t* d_ans, uint32_t* d_sa_local, void* stream,
+                   sa_dist_info* info) {
+    if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_refine(ctx, h, d_ans, d_sa_local, (hipStream_t)stream, info);
 }
 
 int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width) {

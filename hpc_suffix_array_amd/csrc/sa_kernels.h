@@ -953,7 +953,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ sa,
                                                       uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
                                                       uint32_t* __restrict__ u_g, uint32_t* __restrict__ member,
-                                                      int dense_rank) {
+                                                      int dense_rank, uint32_t rank_off) {
     __shared__ uint64_t s_m[kWaves][kItems][3];
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
@@ -1020,7 +1020,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                 const uint32_t x = idx[s];
                 const uint32_t p = pos(s);
                 const bool in_u = (mu >> lane) & 1ull;
-                if (dense_rank || in_u) rank[x] = (hs == s ? p : pos(hs)) + 1u;
+                if (dense_rank || in_u) rank[x] = rank_off + (hs == s ? p : pos(hs)) + 1u;
                 if (sa) sa[p] = x;
                 if (member && in_u) atomicOr(&member[x >> 5], 1u << (x & 31));
                 if (in_u) {

@@ -35,12 +35,20 @@ struct BucketPlan {
 };
 
 // round1: SA_ROUND1_AUTO / SA_ROUND1_LSD / SA_ROUND1_BUCKETED (sa_opts.round1)
-static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p) {
+// world: GPUs the bucket range is split over (sa_dist.h); one GPU sorts at
+// most 2^18 buckets (the second pass's 10 digit bits), a rank of a wider
+// build 2^bb / world of them.
+static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p,
+                          int world = 1) {
     if (round1 == SA_ROUND1_LSD || radix != 0 || sigma < 2 || n < 2) return false;
     if (round1 == SA_ROUND1_AUTO && n < kBucketMinN) return false;
     // bucket bits: windows of about n / 2^bb suffixes must fit the
-    // 9216-suffix LDS tile with room for random fluctuation
-    const uint32_t bb = (n <= (1ull << 29) ? 16u : (n <= (1ull << 30) ? 17u : 18u)) + SA_BB_EXTRA;
+    // 9216-suffix LDS tile with room for random fluctuation (16 up to 2^29
+    // suffixes, 17 up to 2^30, 18 up to 2^31, 19 up to 2^32)
+    uint32_t bb = std::max<uint32_t>(16u, bit_width(n - 1) > 13 ? bit_width(n - 1) - 13 : 0u);
+    if (world <= 1) bb = std::min<uint32_t>(bb, 18u);
+    bb += SA_BB_EXTRA;
+    if (bb > 18 + (uint32_t)bit_width((uint64_t)std::max(world, 1) - 1) || bb > 24) return false;
     uint64_t ps = 1;   // sigma^s >= 2^bb: the bb-bit bucket is dense
     uint32_t s = 0;
     while (ps < (1ull << bb)) {
@@ -51,11 +59,13 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     // equal range of D values.  Otherwise buckets hold floor or ceil of
     // sigma^s / 2^bb values -- up to 2x apart when the ratio is ~1 (alnum:
     // 9472-suffix windows at 2^30, over the LDS tile) -- so s grows until the
-    // ratio is >= 64 (sizes within 1/64), which keeps D < 64 sigma 2^bb <= 2^32
-    while (ps % (1ull << bb) != 0 && ps < (64ull << bb) && s + 1 < K) {
+    // ratio is >= 64 (sizes within 1/64) while D stays below 2^32 (it rolls
+    // in 32 bits)
+    while (ps % (1ull << bb) != 0 && ps < (64ull << bb) && s + 1 < K && ps * sigma <= (1ull << 32)) {
         ps *= sigma;
         ++s;
     }
+    if (ps > (1ull << 32)) return false;
     if (K <= s || K > (uint32_t)kMaxK) return false;
     const uint32_t ib = bit_width(n - 1);
     const uint32_t bd = bit_width(ps - 1);
@@ -87,15 +97,47 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     return false;
 }
 
+// The buckets [blo, bhi) this build sorts (local bucket = bucket - blo): all
+// of them on one GPU; one rank's contiguous range in the range-partitioned
+// build (sa_dist.h), whose m suffixes occupy SA positions [sa_off, sa_off + m)
+// -- the SA, sorted keys and bucket starts written here are that range's,
+// the ranks of unsorted suffixes global (rank_off).
+struct BucketRange {
+    uint32_t blo = 0, bhi = 0;
+    uint64_t m = 0;
+    uint64_t sa_off = 0;
+    bool always_u = false;      // compact the unsorted set whatever its size
+    uint32_t* rank = nullptr;   // n-entry rank array / n-bit member map of the
+    uint32_t* member = nullptr; // unsorted set (null: the context's)
+};
+
+static BucketRange full_range(const BucketPlan& bp, uint64_t n) {
+    BucketRange r;
+    r.blo = 0;
+    r.bhi = 1u << bp.bs.bb;
+    r.m = n;
+    return r;
+}
+
+// second-pass digit bits for a range of nb local buckets (7..10)
+static uint32_t range_hb(uint32_t nb) {
+    const uint32_t w = bit_width(nb > 1 ? nb - 1 : 1);
+    return std::max<uint32_t>(7u, w > kLoBits ? w - kLoBits : 0u);
+}
+
 // *done: the SA and keys[0] hold the sorted first round.  *fused: the
 // round-1 segments were produced with it (few unsorted suffixes): rank[] for
 // the unsorted set only (member bitmap), the unsorted set compacted in
 // u_pos/u_idx/u_g[0], and seg = {D, m, G}; otherwise the caller runs
 // segments() on keys[0].
 static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
-                           hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused, uint64_t seg[3]) {
+                           const BucketRange& br_, hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused,
+                           uint64_t seg[3]) {
     *done = false;
     *fused = false;
+    const uint64_t m = br_.m;   // suffixes of this range (= n on one GPU)
+    const uint32_t blo = br_.blo, bhi = br_.bhi;
+    if (bhi <= blo || bhi - blo > (1u << 18)) return set_err(SA_E_INTERNAL, "bucket range [%u, %u)", blo, bhi);
     int rc = onesweep_prepare(c, s);
     if (rc) return rc;
     // [0..2] D, m, G of the fused segments, [5] largest window, [6] local-sort
@@ -108,15 +150,18 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
         if ((bp.bs.sigma & (bp.bs.sigma - 1)) == 0)
-            hipLaunchKernelGGL(k_bucket_hist<true>, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code,
-                               bp.bs, os_ghist(c));
+            hipLaunchKernelGGL((k_bucket_hist<true, false>), dim3(g), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi);
         else
-            hipLaunchKernelGGL(k_bucket_hist<false>, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code,
-                               bp.bs, os_ghist(c));
+            hipLaunchKernelGGL((k_bucket_hist<false, false>), dim3(g), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi);
     }
     tm.end();
     add_bytes(st, SA_K_PACK, n);
-    const uint32_t hb = bp.bs.bb - kLoBits;   // second-pass digit bits (7..10)
+    // second-pass digit bits (7..10): bb - kLoBits on one GPU
+    const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
+    if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
+    const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
     // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
     // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
     // low, [kLoRadix, +2^hb) high
@@ -140,13 +185,13 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #define SA_TEXT_PASS(P)                                                                                       \
     hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,       \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0],    \
-                       c->vals_alt, g_hi, cursor)
+                       c->vals_alt, g_hi, cursor, m, blo, bhi)
         if (pow2) SA_TEXT_PASS(true);
         else SA_TEXT_PASS(false);
 #undef SA_TEXT_PASS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, 13 * n);
+    add_bytes(st, SA_K_SCATTER_FIRST, n + 12 * m);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
@@ -156,16 +201,16 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         // 12288-pair units cut at the first pass's digit boundaries, places
         // claimed per (low digit, high digit) by atomic cursors (sa_split.h)
         constexpr int kItemsB = SA_ITEMS_B;
-        const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul};
+        const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul, blo};
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
         SA_HIP(hipMemsetAsync(c->segw, 0, segw_words(1u << hb) * 4, s));   // <= 3 MiB
-        const uint64_t units = (n + kSpBlock * kItemsB - 1) / (kSpBlock * kItemsB) + kSegs;
+        const uint64_t units = (m + kSpBlock * kItemsB - 1) / (kSpBlock * kItemsB) + kSegs;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)c->cus));
         switch (hb) {
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
-        hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, n, kLoBits, \
+        hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, m, kLoBits, \
                            (const uint32_t*)os_base(c), hbase, c->segw, tk, bp.ib, c->keys_u, c->words + 4);    \
         break;
             SA_SEG_PASS(7)
@@ -177,12 +222,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         }
         // bucket starts and smallest D values (the local sort rebuilds key1
         // from them; sparse rank look-ups search one bucket)
-        const uint32_t gb = (uint32_t)std::min<uint64_t>(((1ull << bp.bs.bb) + kBlock) / kBlock, 1024);
+        const uint32_t gb = (uint32_t)std::min<uint64_t>(((uint64_t)nb_tab + kBlock) / kBlock, 1024);
         uint32_t* bstart = c->segw + kBstartOff;
         uint32_t* bdmin = bstart + kBstartWords;
 #define SA_BSTARTS(R)                                                                                         \
     hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase,     \
-                       (const uint32_t*)c->segw, n, bp.bs.cmul, bp.bs.bsh, bstart, bdmin)
+                       (const uint32_t*)c->segw, m, bp.bs.cmul, bp.bs.bsh, bstart, bdmin, blo)
         switch (hb) {
             case 7: SA_BSTARTS(128); break;
             case 8: SA_BSTARTS(256); break;
@@ -192,17 +237,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_BSTARTS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_KEYS, 20 * n);
+    add_bytes(st, SA_K_SCATTER_KEYS, 20 * m);
     SA_HIP(hipGetLastError());
-    // windows of whole buckets; ws lives in vals_alt (free again; nw + 1 <= n)
-    const uint64_t nw = (n + kWinStride - 1) / kWinStride;
+    // windows of whole buckets; ws lives in vals_alt (free again; nw + 1 <= m)
+    const uint64_t nw = (m + kWinStride - 1) / kWinStride;
     uint32_t* ws = c->vals_alt;
     uint32_t* list = c->vals_alt + nw + 1;   // non-empty windows (2 nw + 1 <= n)
     tm.begin(SA_K_WINDOWS);
     {
         const uint32_t g1 = (uint32_t)std::min<uint64_t>((nw + kBlock) / kBlock, 8192);
         hipLaunchKernelGGL(k_window_starts_tab, dim3(g1), dim3(kBlock), 0, s, (const uint32_t*)(c->segw + kBstartOff),
-                           1u << bp.bs.bb, n, nw, ws, list + 4 * nw + 2);   // wb: see br below
+                           nb_tab, m, nw, ws, list + 4 * nw + 2);   // wb: see br below
         const uint32_t g2 = (uint32_t)std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024);
         hipLaunchKernelGGL(k_window_list, dim3(g2), dim3(kBlock), 0, s, (const uint32_t*)ws, nw, list, c->words);
     }
@@ -225,8 +270,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* cnt_g = cnt_u + nw + 1;
     const BucketRel br{cnt_g + nw + 1, c->segw + kBstartOff, c->segw + kBstartOff + kBstartWords, bp.bs.rb};
     SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
-    SA_HIP(hipMemsetAsync(c->member, 0, (n + 31) / 32 * 4, s));
-    const SegOut so{c->rank, c->member, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g};
+    uint32_t* const rank_arr = br_.rank ? br_.rank : c->rank;
+    uint32_t* const member = br_.member ? br_.member : c->member;
+    SA_HIP(hipMemsetAsync(member, 0, (n + 31) / 32 * 4, s));
+    const SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g};
     tm.begin(SA_K_LOCAL_SORT);
     {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
@@ -241,7 +288,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                            c->keys[0], d_sa, so);
     }
     tm.end();
-    add_bytes(st, SA_K_LOCAL_SORT, 20 * n);
+    add_bytes(st, SA_K_LOCAL_SORT, 20 * m);
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
@@ -253,7 +300,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     seg[1] = c->host_words[1];
     seg[2] = c->host_words[2];
     add_bytes(st, SA_K_LOCAL_SORT, seg[1] * 28);   // unsorted set: rank, member bit, 3 tmp words
-    if (seg[1] <= n / kSparseDiv) {
+    if (br_.always_u || seg[1] <= n / kSparseDiv) {
         // the unsorted set, in SA order
         tm.begin(SA_K_SEG_WRITE);
         const uint32_t wb = (uint32_t)((nw + 1 + kWsBlock - 1) / kWsBlock);

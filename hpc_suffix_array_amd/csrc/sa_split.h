@@ -296,13 +296,17 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // (BLOCK 512, two workgroups per CU, measured slower: 5.5 -> 6.3 ms)
 // POW2: sigma a power of two -- D and the remainder roll by shifts and masks
 // and the bucket is a bit field of D (no multiplications)
+// Bucket range (range-partitioned build, sa_dist.h): only positions whose
+// bucket lies in [blo, bhi) are kept, digits of the local bucket bk - blo;
+// m = the number kept (the output's length).  One GPU: [0, 2^bb), m = n.
 template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
                                                          uint32_t* __restrict__ out_vals,
-                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
+                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor,
+                                                         uint64_t m, uint32_t blo, uint32_t bhi) {
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int TILE = BLOCK * ITEMS;
@@ -319,8 +323,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (bucket >> kLoBits)
+    __shared__ uint32_t s_kept;
+    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (local bucket >> kLoBits)
     const uint8_t* s_dc = reinterpret_cast<const uint8_t*>(s_dcw);
+    const uint32_t bspan = bhi - blo;
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -421,11 +427,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                     low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
                 }
                 k[j] = ((uint64_t)D << b.rb) | low;
-                const bool ok = l0 + j < valid;
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
-                const uint32_t d = ok ? (bk & (RADIX - 1)) : (uint32_t)RADIX;
+                const uint32_t lb = bk - blo;
+                const bool ok = l0 + j < valid && lb < bspan;
+                const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
                 dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
-                if (ok) atomicAdd(&s_hhi[bk >> kLoBits], 1u);
+                if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
             }
         }
         __syncthreads();
@@ -447,6 +454,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
 #pragma unroll
             for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+            if (dg == (uint32_t)RADIX - 1) s_kept = off + inc;   // pairs kept in this tile
         }
         // the next tile's ticket and text loads (see k_split)
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
@@ -463,14 +471,15 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             }
         }
         __syncthreads();
+        const uint32_t kept = s_kept;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t q = j * BLOCK + dg;
-            if (q < valid) {
+            if (q < kept) {
                 const uint64_t key = s_keys[q];
-                const uint32_t dd = (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh) & (RADIX - 1);
+                const uint32_t dd = ((uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh) - blo) & (RADIX - 1);
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                if (g < n) {
+                if (g < m) {
                     out_keys[g] = key;
                     out_vals[g] = (uint32_t)(tb + s_idx[q]);
                 }
@@ -643,7 +652,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
             s_gofs[dg] = bh + s_claim[dg];
             s_claim[dg] = bh;
-            s_dmin[dg] = bucket_dmin((dg << kLoBits) | l, src.cmul, src.bsh);
+            s_dmin[dg] = bucket_dmin(((dg << kLoBits) | l) + src.bofs, src.cmul, src.bsh);
         }
         __syncthreads();
         if (s_last) {
@@ -709,12 +718,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
 // bucket's smallest D is bdmin[b].  The local sort rebuilds key1 from the
 // bucket-relative items with them; the sparse rank look-ups of later rounds
 // search key1 only inside the bucket.
+// (local buckets b of a range starting at global bucket bofs: Dmin of b + bofs)
 template <int RADIX>
 __global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __restrict__ lo_base,
                                                           const uint32_t* __restrict__ digit_base,
                                                           const uint32_t* __restrict__ segw, uint64_t n,
                                                           uint64_t cmul, uint32_t bsh, uint32_t* __restrict__ bstart,
-                                                          uint32_t* __restrict__ bdmin) {
+                                                          uint32_t* __restrict__ bdmin, uint32_t bofs) {
     const uint64_t* sbase = reinterpret_cast<const uint64_t*>(segw + (uint64_t)kSegs * RADIX);
     const uint32_t nb = (uint32_t)RADIX << kLoBits;
     for (uint32_t b = blockIdx.x * kBlock + threadIdx.x; b <= nb; b += gridDim.x * kBlock) {
@@ -724,7 +734,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __rest
         }
         const uint32_t h = b >> kLoBits, l = b & (kSegs - 1);
         bstart[b] = lo_base[l] == 0 ? digit_base[h] : (uint32_t)sbase[(uint64_t)l * RADIX + h];
-        bdmin[b] = bucket_dmin(b, cmul, bsh);
+        bdmin[b] = bucket_dmin(b + bofs, cmul, bsh);
     }
 }
 

@@ -1,40 +1,42 @@
 """Range-partitioned multi-GPU suffix-array build.
 
 One process per GPU (torch.distributed; backend "nccl" is RCCL over xGMI on
-MI355X, "gloo" for the CPU tests).  Rank r owns text positions
-[r n / G, (r+1) n / G) and, at the end, the same slice of the SA.  Every
-rank holds the text (the packed keys of its positions read up to K-1 bytes
-past its slice).  Per round the local work runs on the HIP kernels of
-libsa_hip (``HipOps``); the exchange steps are collectives:
+MI355X, "gloo" for the CPU tests).  Every rank holds the text in HBM (1 byte
+per suffix -- the reference's MPI driver broadcasts it too, main_mpi.c:51);
+the suffix array and all working state are split into G contiguous SA
+ranges.  The product path is ``DistributedSA`` over ``HipRangeOps`` (the
+sa_dist_* phases of libsa_hip, include/sa_hip.h):
 
-  round 1   packed K-symbol keys of the rank's positions (sa_pack_keys_device)
-            -> global sort: local radix sort, G*64 samples all_gathered,
-               (key, rank, position) splitters, all_to_all_v of the buckets,
-               local radix sort of the received runs (stable, so the order
-               is (key, source rank, source position))
-            -> group heads with the neighbours' boundary keys (all_gather)
-            -> rank[i] = global head position + 1, sent to the owner of i
-               (all_to_all_v); singletons are final
-  round h   (only suffixes whose group is not a singleton)
-            -> rank[i + h] fetched from its owner (request / reply all_to_all_v)
-            -> global stable sort by (dense group id, rank[i + h])
-            -> new positions / heads inside each group, cross-rank carries
-               through all_gather; new ranks to their owners
-  end       (SA position, suffix) pairs all_to_all_v'd to the SA slice owners.
+  alphabet   each rank's slice -> all_reduce MAX of the 256 presence flags
+  begin      K and the bucket plan (bucket = the first s symbols); coarse
+             bucket histogram of the rank's text slice
+  cuts       all_reduce SUM of the coarse histograms -> every rank derives
+             the same G contiguous bucket ranges of ~n/G suffixes; rank q's
+             suffixes occupy SA positions [sa_off_q, sa_off_q + m_q)
+  round 1    each rank scans its text copy, keeps the suffixes of its bucket
+             range and sorts them by their first K symbols (bucket passes +
+             per-window LDS sort): no records cross xGMI
+  round h    while any rank has unsorted suffixes (all_gather of counts):
+             rank[x + h] requests to the rank owning x + h's bucket
+             (all_to_all), answers back (all_to_all), local sort of the
+             unsorted set by (group, rank[x + h]) and re-rank -- groups never
+             straddle ranks, so only rank look-ups cross the links
 
 This replaces the reference's MPI strategy (src/mpi/manber_myers_mpi.c:
 108-144: qsort per rank, Gatherv of all records to rank 0, serial qsort
 there, Bcast of the whole rank array every round), which is centralised and
-does not scale; here no rank ever holds more than its share plus buckets.
+does not scale.  Texts whose buckets cannot balance (one repeated symbol,
+very short periods) fall back to ``SampleSortSA`` (all ranks agree through a
+collective).
 
-The same code runs under gloo on CPU with the CPU stand-in of the local
-operations in tests/ (test infrastructure); the product path is HipOps and
-fails loudly without the HIP library.
+The same drivers run under gloo on CPU with CPU stand-ins of the local
+operations in tests/ (test infrastructure); the product path fails loudly
+without the HIP library.
 """
 from __future__ import annotations
 
 import ctypes
-from typing import List, Sequence, Tuple
+from typing import List, Optional, Sequence, Tuple
 
 import torch
 import torch.distributed as dist
@@ -42,13 +44,323 @@ import torch.distributed as dist
 from . import _native as N
 
 I64 = torch.int64
+I32 = torch.int32
 SAMPLES = 64
 # torch's index / scan kernels are used on slices of at most CHUNK elements:
 # on 2^30-element tensors (1 GiB, world size 1) torch.bincount raised SIGFPE
 # and an index_put faulted on ROCm; permutations go through HIP kernels
 CHUNK = 1 << 26
-# elements per peer pair in one all_to_all_single (see _alltoallv)
+# elements per peer pair in one all_to_all_single (see alltoallv)
 XCHUNK = 1 << 25
+COARSE = 4096   # coarse buckets of the cut plan (sa_bucket.h kCoarse)
+
+
+# -- collectives shared by both drivers -----------------------------------------
+# gloo has no device collectives: with a gloo group and HIP tensors (several
+# ranks sharing one GPU -- the multi-rank HIP tests of tests/test_gpu_parity.py)
+# each collective is staged through host memory; RCCL groups use HBM directly.
+def _staged(t: torch.Tensor, group) -> bool:
+    return t.is_cuda and dist.get_backend(group) == "gloo"
+
+
+def _all_reduce(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> None:
+    if _staged(t, group):
+        h = t.cpu()
+        dist.all_reduce(h, op=op, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+
+
+def _all_gather(out: List[torch.Tensor], t: torch.Tensor, group=None) -> None:
+    if _staged(t, group):
+        ho = [torch.empty_like(x, device="cpu") for x in out]
+        dist.all_gather(ho, t.cpu(), group=group)
+        for x, y in zip(out, ho):
+            x.copy_(y)
+    else:
+        dist.all_gather(out, t, group=group)
+
+
+def _all_to_all_single(out: torch.Tensor, inp: torch.Tensor, rs=None, ss=None, group=None) -> None:
+    if _staged(inp, group):
+        ho = torch.empty_like(out, device="cpu")
+        dist.all_to_all_single(ho, inp.cpu(), rs, ss, group=group)
+        out.copy_(ho)
+    else:
+        dist.all_to_all_single(out, inp, rs, ss, group=group)
+
+
+def alltoallv(tensors: List[torch.Tensor], send: List[int], recv: Optional[List[int]] = None,
+              group=None) -> Tuple[List[torch.Tensor], List[int]]:
+    """all_to_all_v of each tensor (send[j] elements to rank j, in rank order).
+    Each collective moves at most XCHUNK elements per peer pair: one
+    all_to_all_single of 2^28 int64 (2 GiB) returned half garbage on this
+    ROCm stack, so larger exchanges run in slices, the slice count agreed by a
+    MAX all_reduce (tests/test_distributed.py pins the sliced path)."""
+    G = dist.get_world_size(group)
+    if G == 1:
+        return list(tensors), list(send)
+    dev = tensors[0].device
+    if recv is None:
+        sc = torch.tensor(send, dtype=I64, device=dev)
+        rc = torch.empty_like(sc)
+        _all_to_all_single(rc, sc, group=group)
+        recv = rc.tolist()
+    C = XCHUNK
+    t_loc = torch.tensor([max([0] + [(x + C - 1) // C for x in list(send) + list(recv)])], dtype=I64, device=dev)
+    _all_reduce(t_loc, op=dist.ReduceOp.MAX, group=group)
+    T = int(t_loc.item())
+    so = [sum(send[:j]) for j in range(G)]
+    ro = [sum(recv[:j]) for j in range(G)]
+    outs = []
+    for t in tensors:
+        t = t.contiguous()
+        o = torch.empty(sum(recv), dtype=t.dtype, device=dev)
+        if T <= 1:
+            _all_to_all_single(o, t, list(recv), list(send), group=group)
+            outs.append(o)
+            continue
+        for k in range(T):
+            sl = [min(C, max(0, x - k * C)) for x in send]
+            rl = [min(C, max(0, x - k * C)) for x in recv]
+            inp = torch.cat([t[so[j] + k * C: so[j] + k * C + sl[j]] for j in range(G)])
+            got = torch.empty(sum(rl), dtype=t.dtype, device=dev)
+            _all_to_all_single(got, inp, rl, sl, group=group)
+            a = 0
+            for j in range(G):
+                o[ro[j] + k * C: ro[j] + k * C + rl[j]] = got[a: a + rl[j]]
+                a += rl[j]
+        outs.append(o)
+    return outs, list(recv)
+
+
+def _all_gather_rows(row: torch.Tensor, group=None) -> List[List[int]]:
+    G = dist.get_world_size(group)
+    if G == 1:
+        return [row.tolist()]
+    out = [torch.empty_like(row) for _ in range(G)]
+    _all_gather(out, row.contiguous(), group=group)
+    return torch.stack(out).cpu().tolist()
+
+
+def _present_words(flags: Sequence[int]) -> List[int]:
+    words = [0] * 8
+    for b in range(256):
+        if flags[b]:
+            words[b >> 5] |= 1 << (b & 31)
+    return words
+
+
+# -- product local operations: libsa_hip's sa_dist_* phases -------------------------
+class HipRangeOps:
+    """One rank's local phases of the range-partitioned build on its GPU
+    (include/sa_hip.h sa_dist_*; kernels in csrc/sa_dist.h)."""
+
+    def __init__(self, max_n: int, device: int):
+        from .builder import DeviceBuilder
+        self.dev = torch.device("cuda", device)
+        self.b = DeviceBuilder(0, device=device)
+        self.L = N.lib()
+        self.info = N.SaDistInfo()
+        self.coarse = torch.zeros(COARSE, dtype=I64, device=self.dev)
+        self.round1_stats = N.SaStats()
+        self.profile = False
+
+    def _s(self):
+        return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def _info(self) -> dict:
+        i = self.info
+        return {k: getattr(i, k) for k, _ in N.SaDistInfo._fields_}
+
+    def alphabet(self, text_slice: torch.Tensor) -> List[int]:
+        out = (ctypes.c_uint32 * 8)()
+        if text_slice.numel():
+            N.check(self.L.sa_alphabet_device(text_slice.data_ptr(), text_slice.numel(), out, self._s()),
+                    "sa_alphabet_device")
+        return list(out)
+
+    def begin(self, text: torch.Tensor, n: int, world: int, rank: int, present: Sequence[int]):
+        self.text = text
+        pw = (ctypes.c_uint32 * 8)(*present)
+        N.check(self.L.sa_dist_begin(self.b.ctx, text.data_ptr(), n, world, rank, pw, self.coarse.data_ptr(),
+                                     self._s(), ctypes.byref(self.info)), "sa_dist_begin")
+        return self._info(), self.coarse
+
+    def cuts(self, coarse_host: Optional[torch.Tensor]) -> dict:
+        if coarse_host is None:
+            N.check(self.L.sa_dist_cuts(self.b.ctx, None, ctypes.byref(self.info)), "sa_dist_cuts")
+        else:
+            h = coarse_host.to(I64).contiguous().numpy().astype("uint64")
+            N.check(self.L.sa_dist_cuts(self.b.ctx, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        ctypes.byref(self.info)), "sa_dist_cuts")
+        return self._info()
+
+    def empty(self, m: int, dtype) -> torch.Tensor:
+        return torch.empty(m, dtype=dtype, device=self.dev)
+
+    def round1(self, sa_local: torch.Tensor) -> dict:
+        st = ctypes.byref(self.round1_stats) if self.profile else None
+        N.check(self.L.sa_dist_round1(self.b.ctx, sa_local.data_ptr() if sa_local.numel() else None, self._s(),
+                                      ctypes.byref(self.info), st), "sa_dist_round1")
+        return self._info()
+
+    def req_count(self, h: int, world: int) -> Tuple[List[int], dict]:
+        c = (ctypes.c_uint64 * world)()
+        N.check(self.L.sa_dist_req_count(self.b.ctx, h, c, self._s(), ctypes.byref(self.info)), "sa_dist_req_count")
+        return [int(x) for x in c], self._info()
+
+    def req_fill(self, h: int, nsend: int) -> torch.Tensor:
+        req = torch.empty(nsend, dtype=I32, device=self.dev)
+        N.check(self.L.sa_dist_req_fill(self.b.ctx, h, req.data_ptr() if nsend else None, self._s()),
+                "sa_dist_req_fill")
+        return req
+
+    def answer(self, req: torch.Tensor) -> torch.Tensor:
+        ans = torch.empty(req.numel(), dtype=I64, device=self.dev)
+        if req.numel():
+            N.check(self.L.sa_dist_answer(self.b.ctx, req.data_ptr(), req.numel(), ans.data_ptr(), self._s()),
+                    "sa_dist_answer")
+        return ans
+
+    def refine(self, h: int, ans: torch.Tensor, sa_local: torch.Tensor) -> dict:
+        N.check(self.L.sa_dist_refine(self.b.ctx, h, ans.data_ptr() if ans.numel() else None,
+                                      sa_local.data_ptr() if sa_local.numel() else None, self._s(),
+                                      ctypes.byref(self.info)), "sa_dist_refine")
+        return self._info()
+
+    def fallback_ops(self) -> "HipOps":
+        if not hasattr(self, "_fb"):
+            self._fb = HipOps(0, self.dev.index)
+        return self._fb
+
+
+def _trace(*a):
+    import os
+    import sys
+    if os.environ.get("SA_DIST_TRACE"):
+        print("[dist]", *a, file=sys.stderr, flush=True)
+
+
+class DistributedSA:
+    """Range-partitioned build over an initialised process group.
+
+    ``build(text, n)`` -> (sa_local, sa_off): this rank's slice of the SA,
+    SA positions [sa_off, sa_off + len(sa_local)) (uint32 values stored as
+    int32 by the HIP path; int64 from the sample-sort fallback)."""
+
+    def __init__(self, ops, group=None):
+        self.ops = ops
+        self.group = group
+        self.G = dist.get_world_size(group)
+        self.r = dist.get_rank(group)
+        self.stats = {}
+
+    def _min_all(self, x: int, dev) -> int:
+        if self.G == 1:
+            return int(x)
+        t = torch.tensor([int(x)], dtype=I64, device=dev)
+        _all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return int(t.item())
+
+    def build(self, text: torch.Tensor, n: int):
+        G, r = self.G, self.r
+        dev = text.device
+        lo, hi = n * r // G, n * (r + 1) // G
+        self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": []}
+        # alphabet of the whole text: OR of the slices' masks (MAX of flags;
+        # the NCCL backend has no bitwise-or reduction)
+        _trace("alphabet", r, G, n)
+        words = self.ops.alphabet(text[lo:hi])
+        flags = torch.tensor([(words[b >> 5] >> (b & 31)) & 1 for b in range(256)], dtype=I32, device=dev)
+        if G > 1:
+            _all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
+        present = _present_words(flags.tolist())
+        if n < 2:
+            return self._fallback(text, n, "n < 2")
+        _trace("begin")
+        info, coarse = self.ops.begin(text, n, G, r, present)
+        self.stats.update(sigma=info["sigma"], K=info["K"], bucket_bits=info["bucket_bits"])
+        if info["status"] != N.DIST_OK:   # identical on every rank (global alphabet and n)
+            return self._fallback(text, n, "unsupported alphabet / size")
+        ch = None
+        if G > 1:
+            _all_reduce(coarse, group=self.group)
+            ch = coarse.cpu()
+        _trace("cuts")
+        info = self.ops.cuts(ch)
+        _trace("cut", info)
+        self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
+        if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
+            return self._fallback(text, n, "unbalanced bucket ranges")
+        sa_local = self.ops.empty(info["m"], I32)
+        info = self.ops.round1(sa_local)
+        _trace("round1", info)
+        if self._min_all(info["round1_ok"], dev) == 0:
+            return self._fallback(text, n, "a bucket window exceeds the LDS tile")
+        sa_off = info["sa_off"] if "sa_off" in info else self.stats["sa_off"]
+        self.stats["rounds"] = 1
+        self.stats["heads_round1"] = info["heads"]
+        h = self.stats["K"]
+        while True:
+            counts, info = self.ops.req_count(h, G)
+            _trace("req_count", h, counts)
+            mat = _all_gather_rows(torch.tensor([info["unsorted"]] + counts, dtype=I64, device=dev), self.group)
+            total_u = sum(row[0] for row in mat)
+            self.stats["unsorted"].append(total_u)
+            if total_u == 0:
+                break
+            if h >= 2 * n:
+                raise RuntimeError("distributed doubling did not converge")
+            recv_counts = [row[1 + r] for row in mat]
+            self.stats["requests"].append(sum(sum(row[1:]) for row in mat))
+            req = self.ops.req_fill(h, sum(counts))
+            (got,), _ = alltoallv([req], counts, recv_counts, self.group)
+            _trace("requests in", got.numel())
+            ans = self.ops.answer(got)
+            (back,), _ = alltoallv([ans], recv_counts, counts, self.group)
+            self.ops.refine(h, back, sa_local)
+            _trace("refined", h)
+            self.stats["rounds"] += 1
+            h *= 2
+        return sa_local, self.stats["sa_off"]
+
+    def _fallback(self, text, n, why):
+        self.stats["path"] = "sample-sort"
+        self.stats["fallback_reason"] = why
+        ops = self.ops.fallback_ops()
+        d = SampleSortSA(ops, self.group)
+        sa = d.build(text, n)
+        self.stats.update(d.stats)
+        self.stats["path"] = "sample-sort"
+        return sa, n * self.r // self.G
+
+
+def gather_sa(sa_local: torch.Tensor, sa_off: int, n: int, group=None) -> torch.Tensor:
+    """The full SA (int64) on every rank from the ranks' contiguous slices
+    (any sizes); all_gathers of at most CHUNK elements per rank."""
+    G = dist.get_world_size(group)
+    if G == 1:
+        return sa_local.to(I64) if sa_local.dtype != I32 else (sa_local.to(I64) & 0xFFFFFFFF)
+    dev = sa_local.device
+    loc = sa_local.to(I64)
+    if sa_local.dtype == I32:
+        loc = loc & 0xFFFFFFFF
+    rows = _all_gather_rows(torch.tensor([int(sa_off), loc.numel()], dtype=I64, device=dev), group)
+    m = max(x[1] for x in rows)
+    buf = torch.full((max(m, 1),), -1, dtype=I64, device=dev)
+    buf[: loc.numel()] = loc
+    full = torch.full((n,), -1, dtype=I64, device=dev)
+    for a in range(0, max(m, 1), CHUNK):
+        b = min(max(m, 1), a + CHUNK)
+        out = [torch.empty(b - a, dtype=I64, device=dev) for _ in range(G)]
+        _all_gather(out, buf[a:b].contiguous(), group=group)
+        for q, (off, cnt) in enumerate(rows):
+            e = min(b, cnt)
+            if e > a:
+                full[off + a: off + e] = out[q][: e - a]
+    return full
 
 
 def mask_positions(mask: torch.Tensor) -> torch.Tensor:
@@ -147,8 +459,14 @@ class HipOps:
                                              idx.numel(), self._stream()), "sa_scatter_u64_device")
 
 
-class DistributedSA:
-    """Distributed builder over an initialised process group."""
+class SampleSortSA:
+    """General range-partitioned builder by sample sort (the fallback of
+    DistributedSA for texts whose bucket ranges cannot balance: one repeated
+    symbol, very short periods).  Rank r owns text positions and SA positions
+    [r n / G, (r+1) n / G); round 1 sorts packed K-symbol keys globally
+    (local radix sort, G*64 (key, rank, position) splitters, all_to_all_v of
+    the buckets, local re-sort), later rounds fetch rank[i + h] from its
+    position owner and sort the unsorted set globally by (group, rank)."""
 
     def __init__(self, ops, group=None):
         self.ops = ops
@@ -160,53 +478,16 @@ class DistributedSA:
     # -- collectives ---------------------------------------------------------
     def _gather(self, t: torch.Tensor) -> torch.Tensor:
         out = [torch.empty_like(t) for _ in range(self.G)]
-        dist.all_gather(out, t.contiguous(), group=self.group)
+        _all_gather(out, t.contiguous(), group=self.group)
         return torch.stack(out)
 
     def _sum(self, x: int, dev) -> int:
         t = torch.tensor([x], dtype=I64, device=dev)
-        dist.all_reduce(t, group=self.group)
+        _all_reduce(t, group=self.group)
         return int(t.item())
 
     def _alltoallv(self, tensors: List[torch.Tensor], send: List[int]) -> Tuple[List[torch.Tensor], List[int]]:
-        """all_to_all_v of each tensor (send[j] elements to rank j, in rank
-        order).  Each collective moves at most XCHUNK elements per peer pair:
-        one all_to_all_single of 2^28 int64 (2 GiB) returned half garbage on
-        RCCL (a 32-bit byte count), so larger exchanges run in slices, the
-        slice count agreed by a MAX all_reduce."""
-        dev = tensors[0].device
-        if self.G == 1:
-            return list(tensors), list(send)
-        sc = torch.tensor(send, dtype=I64, device=dev)
-        rc = torch.empty_like(sc)
-        dist.all_to_all_single(rc, sc, group=self.group)
-        recv = rc.tolist()
-        C = XCHUNK
-        t_loc = torch.tensor([max([0] + [(x + C - 1) // C for x in send + recv])], dtype=I64, device=dev)
-        dist.all_reduce(t_loc, op=dist.ReduceOp.MAX, group=self.group)
-        T = int(t_loc.item())
-        so = [sum(send[:j]) for j in range(self.G)]
-        ro = [sum(recv[:j]) for j in range(self.G)]
-        outs = []
-        for t in tensors:
-            t = t.contiguous()
-            o = torch.empty(sum(recv), dtype=t.dtype, device=dev)
-            if T <= 1:
-                dist.all_to_all_single(o, t, recv, list(send), group=self.group)
-                outs.append(o)
-                continue
-            for k in range(T):
-                sl = [min(C, max(0, x - k * C)) for x in send]
-                rl = [min(C, max(0, x - k * C)) for x in recv]
-                inp = torch.cat([t[so[j] + k * C: so[j] + k * C + sl[j]] for j in range(self.G)])
-                got = torch.empty(sum(rl), dtype=t.dtype, device=dev)
-                dist.all_to_all_single(got, inp, rl, sl, group=self.group)
-                a = 0
-                for j in range(self.G):
-                    o[ro[j] + k * C: ro[j] + k * C + rl[j]] = got[a: a + rl[j]]
-                    a += rl[j]
-            outs.append(o)
-        return outs, recv
+        return alltoallv(tensors, send, None, self.group)
 
     def _route(self, dest: torch.Tensor, tensors: List[torch.Tensor]):
         # destination order by the local HIP radix sort (stable), counts by
@@ -435,21 +716,3 @@ class DistributedSA:
         return sa
 
 
-def gather_sa(sa_local: torch.Tensor, n: int, group=None) -> torch.Tensor:
-    """Concatenate the SA slices of all ranks (every rank gets the full SA);
-    all_gathers of at most CHUNK elements per rank (see _alltoallv)."""
-    G = dist.get_world_size(group)
-    sizes = [n * (q + 1) // G - n * q // G for q in range(G)]
-    if G == 1:
-        return sa_local[: sizes[0]]
-    m = max(sizes)
-    buf = torch.full((m,), -1, dtype=I64, device=sa_local.device)
-    buf[: sa_local.numel()] = sa_local
-    full = torch.empty(G * m, dtype=I64, device=sa_local.device)
-    for a in range(0, m, CHUNK):
-        b = min(m, a + CHUNK)
-        out = [torch.empty(b - a, dtype=I64, device=buf.device) for _ in range(G)]
-        dist.all_gather(out, buf[a:b].contiguous(), group=group)
-        for q in range(G):
-            full[q * m + a: q * m + b] = out[q]
-    return torch.cat([full[q * m: q * m + sizes[q]] for q in range(G)])

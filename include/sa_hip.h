@@ -172,6 +172,62 @@ int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n,
  * carries of the distributed re-rank); asynchronous on `stream`. */
 int sa_running_max_i64_device(int64_t* d_v, uint64_t m, void* stream);
 
+/* ---- range-partitioned multi-GPU build, per rank ------------------------
+ * Replaces src/mpi/manber_myers_mpi.c:22-160 (and main_mpi.c:43-54).  Every
+ * rank holds the whole text in HBM; the SA is split into `world` contiguous
+ * ranges of buckets (the first symbols of a suffix), rank q sorting the
+ * suffixes of its range, which land at SA positions [sa_off, sa_off + m).
+ * Sequence per build (the caller runs the collectives in brackets; see
+ * hpc_suffix_array_amd/distributed.py):
+ *   [all_reduce MAX of the 256-bit alphabet masks of the ranks' slices]
+ *   sa_dist_begin   -> coarse bucket histogram of this rank's slice (d_coarse)
+ *   [all_reduce SUM of d_coarse, copied to the host]
+ *   sa_dist_cuts    -> m, sa_off (identical cuts on every rank)
+ *   sa_dist_round1  -> the first round of the range into d_sa_local (m uint32)
+ *   per round h = K, 2K, ... while any rank has unsorted suffixes:
+ *     sa_dist_req_count -> requests per owner   [all_gather of counts]
+ *     sa_dist_req_fill  -> requests by owner     [all_to_all]
+ *     sa_dist_answer    -> ranks of the received requests   [all_to_all back]
+ *     sa_dist_refine    -> sort / re-rank the unsorted set
+ * status: SA_DIST_OK, or a reason the caller must build another way (all
+ * ranks agree on it through a collective). */
+#define SA_DIST_OK 0
+#define SA_DIST_UNSUPPORTED 1   /* one symbol, or no bucketed key layout for this n */
+#define SA_DIST_UNBALANCED 2    /* the bucket ranges cannot balance (skewed text) */
+
+typedef struct {
+    int32_t status;         /* SA_DIST_* */
+    int32_t sigma;          /* distinct symbols */
+    int32_t K;              /* symbols sorted by the first round */
+    int32_t bucket_bits;    /* bucket = first symbols, bucket_bits wide */
+    uint64_t m;             /* suffixes of this rank's range */
+    uint64_t sa_off;        /* its first SA position */
+    uint64_t m_max;         /* largest range over all ranks */
+    uint32_t bucket_lo, bucket_hi;   /* this rank's buckets [lo, hi) */
+    int32_t round1_ok;      /* 0: a window exceeded the LDS tile (fall back) */
+    int32_t reserved;
+    uint64_t heads;         /* groups completed in the last phase (local) */
+    uint64_t unsorted;      /* this rank's unsorted suffixes after it */
+    uint64_t groups;        /* their groups */
+} sa_dist_info;
+
+/* present: OR of all ranks' alphabet masks; d_coarse: 4096 uint64 (world > 1) */
+int sa_dist_begin(sa_context* ctx, const uint8_t* d_text, uint64_t n, int world, int rank,
+                  const uint32_t present[8], uint64_t* d_coarse, void* stream, sa_dist_info* info);
+/* h_coarse: the all-reduced coarse histogram on the host (NULL at world 1) */
+int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info);
+/* d_sa_local: info->m uint32 (global text positions, SA order) */
+int sa_dist_round1(sa_context* ctx, uint32_t* d_sa_local, void* stream, sa_dist_info* info, sa_stats* stats);
+/* counts_out: world uint64 -- requests this rank sends to each rank */
+int sa_dist_req_count(sa_context* ctx, uint64_t h, uint64_t* counts_out, void* stream, sa_dist_info* info);
+/* d_req: sum(counts_out) uint32, grouped by destination rank */
+int sa_dist_req_fill(sa_context* ctx, uint64_t h, uint32_t* d_req, void* stream);
+/* ranks of nreq received positions (all in this rank's range) -> d_ans (uint64) */
+int sa_dist_answer(sa_context* ctx, const uint32_t* d_req, uint64_t nreq, uint64_t* d_ans, void* stream);
+/* d_ans: the answers to this rank's requests, in request order */
+int sa_dist_refine(sa_context* ctx, uint64_t h, const uint64_t* d_ans, uint32_t* d_sa_local, void* stream,
+                   sa_dist_info* info);
+
 /* Seeded synthetic text in device memory: the splitmix64 generator of
  * SURVEY.md 8(d) (symbol i = alphabet[((z >> 32) * sigma) >> 32]); the
  * stand-in for scripts/generate_large_datasets.py:12-28, seeded. */

@@ -110,6 +110,9 @@ def main(argv=None):
         if r.get("verified") is not True:
             print(f"REJECTED (suffix array not verified: {r.get('verified')})")
             continue
+        if r.get("scaling") != "strong":
+            print(f"REJECTED (scaling {r.get('scaling')!r}: speedup / efficiency need one string over all GPUs)")
+            continue
         results.append((N, r))
         print(f"OK ({r['ms_per_step']:.2f} ms, {r['value'] / 1e9:.2f} G suffixes/s)")
     if args.dry_run or not results:

@@ -1,8 +1,9 @@
-"""Multi-rank path under gloo on CPU: the range-partitioned
-driver with the CPU stand-in of its local operations, world sizes 2 and 3,
-checked against the oracle.  The same driver runs with HipOps + RCCL on the
-GPU box (tests/test_gpu_parity.py::test_distributed_hip_single_rank and
-bench.py --gpus N)."""
+"""Multi-rank paths under gloo on CPU: the range-partitioned
+driver (DistributedSA) and its sample-sort fallback (SampleSortSA) with the
+CPU stand-ins of their local operations (tests/dist_cpu_ops.py), world sizes
+2 and 3, checked against the oracle.  The same drivers run with the HIP
+phases + RCCL on the GPU box (tests/test_gpu_parity.py::test_distributed_*
+and bench.py --gpus N)."""
 import os
 import socket
 
@@ -36,16 +37,16 @@ def _texts():
     }
 
 
-def _worker(rank, world, port, q, chunks=None):
+def _worker(rank, world, port, q, chunks=None, driver="range"):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import torch.distributed as dist
-    from dist_cpu_ops import CpuOps
+    from dist_cpu_ops import CpuOps, CpuRangeOps
     from hpc_suffix_array_amd import distributed as D
-    from hpc_suffix_array_amd.distributed import DistributedSA, gather_sa
+    from hpc_suffix_array_amd.distributed import DistributedSA, SampleSortSA, gather_sa
     if chunks:
         D.XCHUNK, D.CHUNK = chunks
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -53,9 +54,13 @@ def _worker(rank, world, port, q, chunks=None):
         res = {}
         for name, t in _texts().items():
             text = torch.from_numpy(t.copy())
-            d = DistributedSA(CpuOps())
-            sa_local = d.build(text, len(t))
-            sa = gather_sa(sa_local, len(t))
+            if driver == "range":
+                d = DistributedSA(CpuRangeOps())
+                sa_local, sa_off = d.build(text, len(t))
+            else:
+                d = SampleSortSA(CpuOps())
+                sa_local, sa_off = d.build(text, len(t)), len(t) * rank // world
+            sa = gather_sa(sa_local, sa_off, len(t))
             res[name] = (sa.numpy(), d.stats)
         if rank == 0:
             q.put(res)
@@ -63,11 +68,11 @@ def _worker(rank, world, port, q, chunks=None):
         dist.destroy_process_group()
 
 
-def _run(oracle, world, chunks=None):
+def _run(oracle, world, chunks=None, driver="range"):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks, driver)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -77,13 +82,30 @@ def _run(oracle, world, chunks=None):
     for name, t in _texts().items():
         sa, st = res[name]
         want = oracle.sa_c(t)
-        assert (sa == want.astype(np.int64)).all(), (name, world)
-        assert st["distinct"][-1] == len(t), name
+        assert (sa == want.astype(np.int64)).all(), (name, world, driver)
+        if driver == "range":
+            # one repeated symbol (sigma = 1) has no bucket layout: sample sort
+            want_path = "sample-sort" if len(np.unique(t)) < 2 else "range"
+            assert st["path"] == want_path, (name, st)
+            if want_path == "range":
+                assert st["unsorted"][-1] == 0, (name, st)
+        else:
+            assert st["distinct"][-1] == len(t), name
+    return res
 
 
 @pytest.mark.parametrize("world", [2, 3])
 def test_distributed_gloo(oracle, world):
-    _run(oracle, world)
+    """The range-partitioned driver: bucket-range cuts, local first rounds,
+    rank requests / answers by all_to_all, several doubling rounds (K = 3)."""
+    res = _run(oracle, world)
+    assert max(len(st["unsorted"]) for _, st in res.values()) >= 3
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sample_sort_gloo(oracle, world):
+    """The sample-sort fallback driver (skewed texts)."""
+    _run(oracle, world, driver="sample")
 
 
 def test_choose_chars_keeps_int64_keys():
@@ -108,3 +130,4 @@ def test_chunked_helpers(monkeypatch):
 def test_distributed_gloo_sliced_exchange(oracle):
     """The sliced all_to_all_v / all_gather paths (XCHUNK, CHUNK tiny)."""
     _run(oracle, 3, chunks=(97, 1000))
+    _run(oracle, 2, chunks=(97, 1000), driver="sample")

@@ -224,45 +224,196 @@ def test_config5_degenerate_1gib(gpu):
     b.close()
 
 
-def test_distributed_hip_single_rank(gpu, oracle):
-    """The multi-GPU driver with the HIP local operations and RCCL
-    collectives, at world size 1 (the box has one GPU; world sizes 2-3 run
-    under gloo in tests/test_distributed.py)."""
+def _single_rank_group():
     import socket
 
     import torch
     import torch.distributed as dist
-    from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, gather_sa
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     dist.init_process_group("nccl", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1,
                             device_id=torch.device("cuda", 0))
+
+
+def test_distributed_hip_single_rank(gpu, oracle):
+    """The multi-GPU drivers with the HIP local phases and RCCL collectives at
+    world size 1 (the box has one GPU; world sizes 2-3 run under gloo in
+    tests/test_distributed.py): the range-partitioned build (sa_dist_*) on
+    every alphabet, ragged sizes, periodic text (several request rounds), and
+    its sample-sort fallback (one repeated symbol)."""
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, HipRangeOps, SampleSortSA, gather_sa
+    _single_rank_group()
     try:
-        ops = HipOps(1 << 22, 0)
-        for t in (oracle.gen_text("dna", 3_000_017, seed=8), np.full(70_000, ord("a"), np.uint8),
-                  np.tile(np.frombuffer(b"abaababa", np.uint8), 9_000), oracle.gen_text("byte256", 500_000, seed=2)):
+        ops = HipRangeOps(1 << 22, 0)
+        cases = [("dna", oracle.gen_text("dna", 3_000_017, seed=8), "range"),
+                 ("alnum", oracle.gen_text("alnum", 1_500_007, seed=9), "range"),
+                 ("byte256", oracle.gen_text("byte256", 2_000_003, seed=2), "range"),
+                 ("ascii127", oracle.gen_text("ascii127", 65_537, seed=3), "range"),
+                 ("binary", oracle.gen_text("binary", 1_000_003, seed=4), "range"),
+                 # too short for the bucket layout (K <= s): the sample-sort path
+                 ("tiny", np.frombuffer(b"banana", np.uint8), "sample-sort"),
+                 ("periodic", np.tile(oracle.gen_text("alnum", 1000, seed=11), 300), "range"),
+                 ("degenerate", np.full(70_000, ord("a"), np.uint8), "sample-sort")]
+        for name, t, path in cases:
             text = torch.from_numpy(t.copy()).cuda()
             d = DistributedSA(ops)
-            sa = gather_sa(d.build(text, len(t)), len(t)).cpu().numpy()
+            sa_local, sa_off = d.build(text, len(t))
+            assert d.stats["path"] == path, (name, d.stats)
+            sa = gather_sa(sa_local, sa_off, len(t)).cpu().numpy()
+            assert (sa == oracle.sa_c(t).astype(np.int64)).all(), name
+        # the sample-sort driver on its own
+        hops = HipOps(1 << 22, 0)
+        for t in (oracle.gen_text("dna", 300_017, seed=8), np.tile(np.frombuffer(b"abaababa", np.uint8), 9_000)):
+            text = torch.from_numpy(t.copy()).cuda()
+            sa = gather_sa(SampleSortSA(hops).build(text, len(t)), 0, len(t)).cpu().numpy()
             assert (sa == oracle.sa_c(t).astype(np.int64)).all()
         # running max across tile boundaries (4096 values per tile)
         g = torch.Generator().manual_seed(5)
         for m in (1, 63, 4096, 4097, 300_001):
             v = torch.randint(-1, 1 << 40, (m,), generator=g, dtype=torch.int64)
             v[torch.rand(m, generator=g) < 0.7] = -1
-            got = ops.running_max(v.cuda()).cpu()
+            got = hops.running_max(v.cuda()).cpu()
             assert torch.equal(got, torch.cummax(v, 0)[0]), m
         # owner-side scatter: in-range writes land, out-of-range ones are refused
         dst = torch.full((8,), -1, dtype=torch.int64, device="cuda")
-        ops.scatter(dst, torch.tensor([12, 10], dtype=torch.int64, device="cuda"), 10,
-                    torch.tensor([5, 7], dtype=torch.int64, device="cuda"))
+        hops.scatter(dst, torch.tensor([12, 10], dtype=torch.int64, device="cuda"), 10,
+                     torch.tensor([5, 7], dtype=torch.int64, device="cuda"))
         assert dst.tolist() == [7, -1, 5, -1, -1, -1, -1, -1]
         from hpc_suffix_array_amd._native import SAError
         with pytest.raises(SAError):
-            ops.scatter(dst, torch.tensor([9, 18], dtype=torch.int64, device="cuda"), 10,
-                        torch.tensor([1, 2], dtype=torch.int64, device="cuda"))
+            hops.scatter(dst, torch.tensor([9, 18], dtype=torch.int64, device="cuda"), 10,
+                         torch.tensor([1, 2], dtype=torch.int64, device="cuda"))
         assert dst.tolist() == [7, -1, 5, -1, -1, -1, -1, -1]
+        # zero-length inputs of the sample-sort building blocks (n < world size)
+        e = torch.empty(0, dtype=torch.int64, device="cuda")
+        assert hops.pack_keys(torch.zeros(4, dtype=torch.uint8, device="cuda"), 4, 2, 2, [0] * 256, 5, 3).numel() == 0
+        assert hops.argsort(e, 8)[0].numel() == 0 and hops.gather(e, e).numel() == 0
+        assert hops.running_max(e).numel() == 0
+        hops.scatter(e.clone(), e, 0, e)
+    finally:
+        dist.destroy_process_group()
+
+
+def _multi_rank_worker(rank, world, port, q):
+    """One rank of a world sharing the box's GPU: HIP phases on cuda:0, the
+    collectives through a gloo group (staged via host memory)."""
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa
+    from oracle import oracle as O
+    import faulthandler
+    logdir = os.path.join(root, "gpurun_out")
+    os.makedirs(logdir, exist_ok=True)
+    log = open(os.path.join(logdir, f"multi_rank_w{world}_r{rank}.log"), "w")
+    os.dup2(log.fileno(), 2)   # the library's SA_TRACE lines and faulthandler land in the log
+    os.environ["SA_DIST_TRACE"] = "1"
+    faulthandler.dump_traceback_later(40, exit=True, file=log)   # a hung rank names its stack
+
+    def say(*a):
+        print(*a, file=log, flush=True)
+
+    torch.cuda.set_device(0)
+    say("init")
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    say("group up")
+    try:
+        ops = HipRangeOps(0, 0)
+        res = {}
+        for name, kind, n, seed in (("dna", "dna", 3_000_017, 8), ("byte256", "byte256", 2_000_003, 2),
+                                    ("alnum", "alnum", 1_048_576, 1), ("binary", "binary", 1_000_003, 4),
+                                    ("periodic", None, 300_000, 11), ("degenerate", None, 70_001, 0)):
+            if name == "periodic":
+                t = np.tile(O.gen_text("alnum", 1000, seed=seed), 300)
+            elif name == "degenerate":
+                t = np.full(n, ord("a"), np.uint8)
+            else:
+                t = O.gen_text(kind, n, seed=seed)
+            say("build", name)
+            d = DistributedSA(ops)
+            sa_local, sa_off = d.build(torch.from_numpy(t).cuda(), len(t))
+            say("built", name, d.stats)
+            sa = gather_sa(sa_local, sa_off, len(t))
+            say("gathered", name)
+            if rank == 0:
+                want = O.sa_c(t).astype(np.int64)
+                res[name] = (bool((sa.cpu().numpy() == want).all()), d.stats["path"], len(d.stats["unsorted"]))
+        if rank == 0:
+            q.put(res)
+    except BaseException:
+        import traceback
+        say(traceback.format_exc())
+        q.put({"error": (rank, traceback.format_exc())})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_hip_multi_rank(gpu, world):
+    """The range-partitioned build with real HIP phases on 2-3 ranks (all on
+    the box's one GPU; the 8-GPU RCCL run is the driver's): cuts into
+    unequal ranges, rank requests answered by other ranks, several doubling
+    rounds (periodic text), the sample-sort fallback (one symbol) -- every SA
+    equal to the oracle's."""
+    import socket
+
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_multi_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = q.get(timeout=240)
+    assert "error" not in res, res.get("error")
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for name, (ok, path, rounds) in res.items():
+        assert ok, (name, world)
+        assert path == ("sample-sort" if name == "degenerate" else "range"), (name, path)
+    assert res["periodic"][2] >= 4, res["periodic"]
+
+
+@pytest.mark.slow
+def test_distributed_hip_config4_shape(gpu, oracle, golden):
+    """configs[3]'s path at the largest size one box holds: the range-
+    partitioned driver at world size 1 on byte256 text (NULs and bytes >=
+    0x80 included) of n = 2^31 + 17 suffixes -- 32-bit index fields in the
+    bucket items (ib = 32), 18-bit buckets, 64-bit prefix lengths -- checked
+    by the O(n) checker; plus the byte256 1 MiB known answer through the same
+    driver."""
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa
+    _single_rank_group()
+    try:
+        ops = HipRangeOps(0, 0)
+        k = golden["known"]["byte256_1MiB"]
+        t = oracle.gen_text("byte256", k["n"], seed=k["seed"])
+        d = DistributedSA(ops)
+        sa_local, sa_off = d.build(torch.from_numpy(t).cuda(), len(t))
+        assert d.stats["path"] == "range" and sa_off == 0
+        got = gather_sa(sa_local, sa_off, len(t)).cpu().numpy().astype(np.int32)
+        assert oracle.sha256(got) == k["sa_sha256_i32"]
+        n = (1 << 31) + 17
+        text = torch.empty(n, dtype=torch.uint8, device="cuda")
+        ops.b.generate_text(text, n, bytes(range(256)), seed=1)
+        d = DistributedSA(ops)
+        sa_local, sa_off = d.build(text, n)
+        torch.cuda.synchronize()
+        assert d.stats["path"] == "range" and d.stats["m"] == n, d.stats
+        assert d.stats["unsorted"][-1] == 0
+        assert ops.b.check(text, n, sa_local)   # the context's buffers are free again
     finally:
         dist.destroy_process_group()
 
