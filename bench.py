@@ -280,10 +280,15 @@ def run_distributed(a, torch, dev, world, rank, barrier):
         verified = bool(v.item()) if n <= 0xFFFFFFFF else None
     st = stats[-1]
     m_max = st.get("m_max")
+    phase = {}
+    for x in stats:
+        for k, v in (x.get("phase_ms") or {}).items():
+            phase[k] = phase.get(k, 0.0) + v / len(stats)
     extra = {"rounds": st["rounds"], "unsorted_per_round": st.get("unsorted"),
              "requests_per_round": st.get("requests"), "init_chars": st.get("K"), "sigma": st.get("sigma"),
              "bucket_bits": st.get("bucket_bits"), "path": st.get("path"), "largest_rank_share": (
                  round(m_max / (n / world), 4) if m_max else None),
+             "phase_ms": {k: round(v, 3) for k, v in phase.items()},
              "text_broadcast_ms": round(bcast_ms, 3) if bcast_ms else None, "verified": verified, "roofline": None,
              "note": "range-partitioned build: each rank sorts the suffixes of its bucket range from its text "
                      "copy; rank requests/answers by RCCL all_to_all between doubling rounds"}

@@ -137,13 +137,28 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) 
 constexpr uint32_t kCoarseBits = 12;
 constexpr uint32_t kCoarse = 1u << kCoarseBits;
 
-template <bool POW2 = false, bool COARSE = false>
+// LIST: the suffixes counted (one rank's bucket range) are also written as
+// compacted records (key1 -> lkeys, position -> lpos) for the record-driven
+// first pass (k_split_list): key1 rolls here from the LDS-staged digits at
+// full occupancy, and the first pass only ranks and scatters the range's
+// ~n/G.  Two sweeps over the workgroup's tiles: count (and histogram), one
+// claim of the workgroup's output range from *cursor, then the records --
+// a claim per 4096-position tile (262 K claims on one counter at 2^30)
+// serialised at ~10 ns each.
+template <bool POW2 = false, bool COARSE = false, bool LIST = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
                                                         uint32_t* __restrict__ ghist, uint64_t p0, uint64_t p1,
-                                                        uint32_t blo, uint32_t bhi) {
+                                                        uint32_t blo, uint32_t bhi,
+                                                        uint64_t* __restrict__ lkeys = nullptr,
+                                                        uint32_t* __restrict__ lpos = nullptr,
+                                                        uint32_t* __restrict__ cursor = nullptr) {
     constexpr int RUN = kTile / kBlock;   // 16
     constexpr uint32_t NB = COARSE ? kCoarse : kLoRadix;
+    __shared__ uint32_t s_tmp[kWaves];
+    __shared__ uint32_t s_base;
+    // LIST: the tile's kept positions (tile offsets), compacted
+    __shared__ uint16_t s_rp[LIST ? kTile : 1];
     __shared__ uint8_t s_map[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
     uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
@@ -159,6 +174,16 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     const uint32_t bspan = bhi - blo;
     __syncthreads();
     const uint64_t tiles = (p1 - p0 + kTile - 1) / kTile;
+    uint32_t kept_lane = 0;   // LIST sweep 0: this lane's kept positions
+    uint32_t run = 0;         // LIST sweep 1: the workgroup's next record slot
+    for (int sweep = 0; sweep < (LIST ? 2 : 1); ++sweep) {
+    if (LIST && sweep == 1) {
+        uint32_t tot;
+        block_exclusive_sum(kept_lane, s_tmp, &tot);
+        if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, tot) : 0u;
+        __syncthreads();
+        run = s_base;
+    }
     for (uint64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
         const uint64_t tb = p0 + tt * kTile;
         {
@@ -205,6 +230,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         uint32_t xo[RUN / 4], xi[RUN / 4];
         lds_bytes<RUN>(s_dcw, l0, xo);
         lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
+        uint32_t keep = 0;   // LIST: bit j = position l0 + j is in the range
 #pragma unroll
         for (int j = 0; j < RUN; ++j) {
             if (j > 0) {
@@ -217,11 +243,48 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                     atomicAdd(&s_hlo[bk >> cshift], 1u);
                 } else {
                     const uint32_t lb = bk - blo;
-                    if (lb < bspan) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
+                    if (lb < bspan) {
+                        if (sweep == 0) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
+                        keep |= 1u << j;
+                    }
                 }
             }
         }
+        if (LIST && sweep == 0) kept_lane += (uint32_t)__popc(keep);
+        if (LIST && sweep == 1) {
+            // the tile's kept positions compacted into LDS in order, then one
+            // thread per record computes key1 from the staged digits (only
+            // ~1/G of the positions) and writes it coalesced
+            uint32_t tot;
+            uint32_t off = block_exclusive_sum((uint32_t)__popc(keep), s_tmp, &tot);
+            while (keep) {
+                const int j = __builtin_ctz(keep);
+                keep &= keep - 1;
+                s_rp[off++] = (uint16_t)(l0 + j);
+            }
+            __syncthreads();
+            const uint32_t K = b.s + b.R;
+            for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
+                const uint32_t l = s_rp[t];
+                uint32_t Dk = 0;
+                uint64_t r = 0;
+                for (uint32_t q = 0; q < b.s; ++q) Dk = POW2 ? ((Dk << lg) | s_dc[l + q]) : Dk * sig + s_dc[l + q];
+                for (uint32_t q = b.s; q < K; ++q) r = POW2 ? ((r << lg) | s_dc[l + q]) : r * sig + s_dc[l + q];
+                const uint64_t L = n - (tb + l);
+                uint64_t low;
+                if (L >= K) {
+                    low = b.s + r * (b.R + 1) + b.R;
+                } else {
+                    const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+                    low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
+                }
+                lkeys[run + t] = ((uint64_t)Dk << b.rb) | low;
+                lpos[run + t] = (uint32_t)(tb + l);
+            }
+            run += tot;
+        }
         __syncthreads();
+    }
     }
     for (uint32_t i = threadIdx.x; i < NB; i += kBlock) {
         if (!s_hlo[i]) continue;

@@ -136,6 +136,76 @@ static int ensure_dist_m(sa_context* c, uint64_t m) {
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
+// key1 of suffix j (sa_bucket.h layout) from the text in HBM: the bytes of
+// [j, j + K) arrive as independent aligned words (one memory latency instead
+// of K dependent byte + table loads), digits through the LDS byte map (code -
+// 1; 0 past the end).  FULL = false: only D (the bucket's input).
+constexpr int kKeyWords = 8;   // K <= 29 symbols; longer keys take the byte loop
+
+template <bool FULL>
+__device__ __forceinline__ uint64_t key1_words(const uint8_t* __restrict__ text, uint64_t n,
+                                               const uint8_t* __restrict__ s_map, const BucketSpec& b, uint64_t j,
+                                               uint32_t* D_out) {
+    const uint32_t K = FULL ? b.s + b.R : b.s;
+    uint64_t D = 0, r = 0;
+    if (K + 3 <= 4 * kKeyWords) {
+        const uint64_t base = j & ~3ull;
+        const uint32_t sh = (uint32_t)(j & 3);
+        uint32_t w[kKeyWords + 1];
+#pragma unroll
+        for (int q = 0; q <= kKeyWords; ++q) {
+            const uint64_t a = base + 4ull * q;
+            if (a + 4 <= n) {
+                w[q] = *reinterpret_cast<const uint32_t*>(text + a);
+            } else {
+                uint32_t v = 0;
+                for (int i = 0; i < 4; ++i)
+                    if (a + i < n) v |= (uint32_t)text[a + i] << (8 * i);
+                w[q] = v;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kKeyWords; ++q) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t t = 4 * q + i;
+                if (t < K) {
+                    const uint32_t c = (j + t < n) ? (uint32_t)s_map[(x >> (8 * i)) & 0xFFu] : 0u;
+                    if (t < b.s) D = D * b.sigma + c;
+                    else r = r * b.sigma + c;
+                }
+            }
+        }
+    } else {
+        for (uint32_t t = 0; t < K; ++t) {
+            const uint32_t c = (j + t < n) ? (uint32_t)s_map[text[j + t]] : 0u;
+            if (t < b.s) D = D * b.sigma + c;
+            else r = r * b.sigma + c;
+        }
+    }
+    *D_out = (uint32_t)D;
+    if (!FULL) return 0;
+    const uint64_t L = n - j;
+    uint64_t low;
+    if (L < b.s) {
+        low = L - 1;
+    } else {
+        const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+        low = b.s + r * (b.R + 1) + tl;
+    }
+    return (D << b.rb) | low;
+}
+
+// the 256-entry byte -> dense digit map in LDS (code - 1, absent bytes 0)
+__device__ __forceinline__ void load_map(const uint16_t* __restrict__ code, uint8_t* s_map) {
+    for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
+        const uint32_t cv = code[i];
+        s_map[i] = (uint8_t)(cv ? cv - 1u : 0u);
+    }
+    __syncthreads();
+}
+
 // Owner of rank[x + h] for each unsorted x (x + h < n): the rank whose bucket
 // range holds x + h's bucket (its first s symbols, read from the text);
 // counts per owner, aggregated per wave (few owners, many requests).
@@ -144,6 +214,8 @@ __global__ __launch_bounds__(kBlock) void k_dist_owner(const uint32_t* __restric
                                                        const uint16_t* __restrict__ code, BucketSpec b,
                                                        const uint16_t* __restrict__ owner_tab, uint32_t cshift,
                                                        uint32_t* __restrict__ owner, uint32_t* __restrict__ counts) {
+    __shared__ uint8_t s_map[256];
+    load_map(code, s_map);
     const uint32_t lane = lane_id();
     for (uint64_t e0 = (uint64_t)blockIdx.x * kBlock; e0 < mu; e0 += (uint64_t)gridDim.x * kBlock) {
         const uint64_t e = e0 + threadIdx.x;
@@ -151,12 +223,9 @@ __global__ __launch_bounds__(kBlock) void k_dist_owner(const uint32_t* __restric
         if (e < mu) {
             const uint64_t j = (uint64_t)u_idx[e] + h;
             if (j < n) {
-                uint64_t D = 0;
-                for (uint32_t t = 0; t < b.s; ++t) {
-                    const uint32_t cv = (j + t < n) ? code[text[j + t]] : 0u;
-                    D = D * b.sigma + (cv ? cv - 1u : 0u);
-                }
-                const uint32_t bk = (uint32_t)((D * b.cmul) >> b.bsh);
+                uint32_t D;
+                key1_words<false>(text, n, s_map, b, j, &D);
+                const uint32_t bk = (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 o = owner_tab[bk >> cshift];
             }
             owner[e] = o;
@@ -218,36 +287,56 @@ struct DistLookup {
     uint64_t sa_off;
 };
 
+// rank[j] (j < n) by the owner of j's bucket; *bad set on a j outside the range
+__device__ __forceinline__ uint64_t dist_rank_of(const DistLookup& L, const uint8_t* s_map, uint64_t j, bool* bad) {
+    if ((L.gmember[j >> 5] >> (j & 31)) & 1u) return L.grank[j];
+    uint32_t D;
+    const uint64_t x = key1_words<true>(L.text, L.n, s_map, L.bs, j, &D);
+    const uint32_t b = (uint32_t)(((uint64_t)D * L.bs.cmul) >> L.bs.bsh) - L.blo;
+    if (b >= L.nb) {
+        *bad = true;
+        return 0;
+    }
+    uint64_t lo = L.bstart[b], len = L.bstart[b + 1] - lo;
+    while (len > 0) {
+        const uint64_t half = len >> 1;
+        if (L.keys1[lo + half] < x) {
+            lo += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    return L.sa_off + lo + 1;
+}
+
 __global__ __launch_bounds__(kBlock) void k_dist_answer(const uint32_t* __restrict__ req, uint64_t nreq, DistLookup L,
                                                         uint64_t* __restrict__ ans, uint32_t* __restrict__ err) {
+    __shared__ uint8_t s_map[256];
+    load_map(L.code, s_map);
+    bool bad = false;
     for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < nreq; t += (uint64_t)gridDim.x * kBlock) {
         const uint64_t j = req[t];
         uint64_t r = 0;
-        if (j >= L.n) {
-            atomicOr(err, 1u);
-        } else if ((L.gmember[j >> 5] >> (j & 31)) & 1u) {
-            r = L.grank[j];
-        } else {
-            const uint64_t x = key1_at(L.text, L.code, L.n, L.bs, j);
-            const uint32_t b = (uint32_t)(((x >> L.bs.rb) * L.bs.cmul) >> L.bs.bsh) - L.blo;
-            if (b >= L.nb) {
-                atomicOr(err, 1u);
-            } else {
-                uint64_t lo = L.bstart[b], len = L.bstart[b + 1] - lo;
-                while (len > 0) {
-                    const uint64_t half = len >> 1;
-                    if (L.keys1[lo + half] < x) {
-                        lo += half + 1;
-                        len -= half + 1;
-                    } else {
-                        len = half;
-                    }
-                }
-                r = L.sa_off + lo + 1;
-            }
-        }
+        if (j >= L.n) bad = true;
+        else r = dist_rank_of(L, s_map, j, &bad);
         ans[t] = r;
     }
+    if (bad) atomicOr(err, 1u);
+}
+
+// one rank (world 1): rank[x + h] looked up in place, no requests
+__global__ __launch_bounds__(kBlock) void k_dist_r1_local(const uint32_t* __restrict__ u_idx, uint64_t mu, uint64_t h,
+                                                          DistLookup L, uint64_t* __restrict__ r1,
+                                                          uint32_t* __restrict__ err) {
+    __shared__ uint8_t s_map[256];
+    load_map(L.code, s_map);
+    bool bad = false;
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < mu; e += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t j = (uint64_t)u_idx[e] + h;
+        r1[e] = j < L.n ? dist_rank_of(L, s_map, j, &bad) : 0;
+    }
+    if (bad) atomicOr(err, 1u);
 }
 
 // answers back into unsorted order (r1 zeroed first: x + h >= n keeps 0)
@@ -446,7 +535,7 @@ static int dist_req_count(sa_context* c, uint64_t h, uint64_t* h_counts, hipStre
     d->nsend = 0;
     info->unsorted = d->mu;
     info->groups = d->gu;
-    if (d->mu > 0) {
+    if (d->mu > 0 && W > 1) {
         SA_HIP(hipMemsetAsync(d->cnt, 0, W * 4, s));
         const uint32_t grid = (uint32_t)std::min<uint64_t>((d->mu + kBlock - 1) / kBlock, 8192);
         hipLaunchKernelGGL(k_dist_owner, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[d->uo], d->mu, h,
@@ -520,8 +609,17 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     if (h >= 2 * d->n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)", (unsigned long long)h);
     Timer tm{c, s, false, nullptr};
     const uint64_t m = d->mu, G = d->gu;
-    SA_HIP(hipMemsetAsync(d->r1, 0, m * 8, s));
-    if (d->nsend) {
+    if (d->world == 1) {   // every look-up is local: no request / answer exchange
+        const DistLookup L{d->grank, d->gmember, c->keys[0], c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
+                           d->n, d->bp.bs, d->blo, d->bhi - d->blo, d->sa_off};
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
+        hipLaunchKernelGGL(k_dist_r1_local, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[d->uo], m, h, L,
+                           d->r1, d->cnt + 2 * kDistMaxWorld);
+        SA_HIP(hipGetLastError());
+    } else {
+        SA_HIP(hipMemsetAsync(d->r1, 0, m * 8, s));
+    }
+    if (d->world > 1 && d->nsend) {
         const uint32_t grid = (uint32_t)std::min<uint64_t>((d->nsend + kBlock - 1) / kBlock, 8192);
         hipLaunchKernelGGL(k_dist_place, dim3(grid), dim3(kBlock), 0, s, d_ans, d->nsend, (const uint32_t*)d->perm,
                            d->r1);
@@ -563,6 +661,10 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     int rc = segments(c, sorted, c->vals_u, plan_chunks(m), PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm,
                       nullptr, &Du, &m2, &G2, d->grank, d->sa_off);
     if (rc) return rc;
+    if (d->world == 1) {   // the local look-ups' range check (segments() synchronised the stream)
+        SA_HIP(hipMemcpy(hc, d->cnt + 2 * kDistMaxWorld, 4, hipMemcpyDeviceToHost));
+        if (hc[0]) return set_err(SA_E_INTERNAL, "rank look-up outside the bucket range");
+    }
     d->mu = m2;
     d->gu = G2;
     d->uo = uo;

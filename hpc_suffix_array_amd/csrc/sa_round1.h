@@ -145,19 +145,30 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     SA_HIP(hipMemsetAsync(c->words, 0, 12, s));
     SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
     // digit totals of both bucket passes (one read of the text)
+    // a rank's range of a multi-GPU build holding at most a quarter of the
+    // text: the histogram pass also emits the range's (key1, position)
+    // records and the first pass scatters those (sim_ranks at 2^30 DNA, G = 8:
+    // ...; at G = 2 streaming the text through k_split_text is cheaper than
+    // writing and reading 12-byte records for half of it)
+    const bool listed = m <= n / 4;
+    uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
+    uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
     tm.begin(SA_K_PACK);
     {
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
-        if ((bp.bs.sigma & (bp.bs.sigma - 1)) == 0)
-            hipLaunchKernelGGL((k_bucket_hist<true, false>), dim3(g), dim3(kBlock), 0, s, d_text, n,
-                               (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi);
-        else
-            hipLaunchKernelGGL((k_bucket_hist<false, false>), dim3(g), dim3(kBlock), 0, s, d_text, n,
-                               (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi);
+        const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
+#define SA_HIST(P, L)                                                                                         \
+    hipLaunchKernelGGL((k_bucket_hist<P, false, L>), dim3(g), dim3(kBlock), 0, s, d_text, n,                  \
+                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, os_tickets(c) + 2)
+        if (pow2 && listed) SA_HIST(true, true);
+        else if (pow2) SA_HIST(true, false);
+        else if (listed) SA_HIST(false, true);
+        else SA_HIST(false, false);
+#undef SA_HIST
     }
     tm.end();
-    add_bytes(st, SA_K_PACK, n);
+    add_bytes(st, SA_K_PACK, n + (listed ? 12 * m : 0));
     // second-pass digit bits (7..10): bb - kLoBits on one GPU
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
@@ -186,12 +197,22 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,       \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0],    \
                        c->vals_alt, g_hi, cursor, m, blo, bhi)
-        if (pow2) SA_TEXT_PASS(true);
-        else SA_TEXT_PASS(false);
+        if (listed) {
+            constexpr int kItemsL = SA_ITEMS_B;
+            const uint64_t tl = (uint64_t)kSpBlock * kItemsL;
+            const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((m + tl - 1) / tl, (uint64_t)c->cus));
+            hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
+                               (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
+                               os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
+        } else if (pow2) {
+            SA_TEXT_PASS(true);
+        } else {
+            SA_TEXT_PASS(false);
+        }
 #undef SA_TEXT_PASS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, n + 12 * m);
+    add_bytes(st, SA_K_SCATTER_FIRST, listed ? 24 * m : n + 12 * m);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);

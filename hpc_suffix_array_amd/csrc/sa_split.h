@@ -494,6 +494,131 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
 }
 
 // ---------------------------------------------------------------------------
+// The first bucket pass of one rank's bucket range in the range-partitioned
+// build (sa_dist.h) from the range's records (key1, position) that
+// k_bucket_hist<LIST> compacted: a rank of G keeps ~n/G of the text's
+// suffixes, and rolling key1 over every position of the text inside this
+// pass cost k_split_text 2.9 of a 5.0 ms first round at G = 8.  Ranking,
+// claims and the scatter by the low kLoBits of the local bucket are those of
+// k_split_text.
+// ---------------------------------------------------------------------------
+template <int ITEMS, int BLOCK = kSpBlock>
+__global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b, const uint64_t* __restrict__ lkeys,
+                                                         const uint32_t* __restrict__ lpos, uint64_t m, uint32_t blo,
+                                                         const uint32_t* __restrict__ digit_base,
+                                                         uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
+                                                         uint32_t* __restrict__ out_vals,
+                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
+    constexpr int RADIX = kLoRadix;
+    constexpr int RWAVES = RADIX / kWave;
+    constexpr int WTILE = kWave * ITEMS;
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE <= 65535, "16-bit tile offsets");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_pos[TILE];
+    __shared__ uint32_t s_cnt[RADIX];
+    __shared__ uint16_t s_start[RADIX];
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[RWAVES];
+    __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (local bucket >> kLoBits)
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint64_t tiles = (m + TILE - 1) / TILE;
+    for (uint32_t i = dg; i < 1024u; i += BLOCK) s_hhi[i] = 0;
+    if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
+    if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
+    __syncthreads();
+    uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    auto load = [&](uint64_t tt, uint64_t* kk, uint32_t* vv) {   // clamped, unpredicated (see k_split)
+        const uint64_t tb = tt * TILE;
+        const uint32_t last = (uint32_t)min(m - 1 - tb, (uint64_t)(TILE - 1));
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const uint64_t e = tb + (le < last ? le : last);
+            kk[j] = lkeys[e];
+            vv[j] = lpos[e];
+        }
+    };
+    if (t < tiles) load(t, k, v);
+    uint32_t par = 0;
+    while (t < tiles) {
+        const uint64_t tb = t * TILE;
+        const uint32_t valid = (uint32_t)((m - tb) < (uint64_t)TILE ? (m - tb) : (uint64_t)TILE);
+        uint32_t dr[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const bool ok = le < valid;
+            const uint32_t lb = bucket_of(k[j], b.rb, b.cmul, b.bsh) - blo;
+            const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
+            dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
+            if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
+        }
+        __syncthreads();
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)RADIX) {
+            tile_cnt = s_cnt[dg];
+            s_cnt[dg] = 0;
+            s_gofs[dg] = digit_base[dg] + (tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u);
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        uint64_t kn[ITEMS];
+        uint32_t vn[ITEMS];
+        load(tn < tiles ? tn : tiles - 1, kn, vn);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t d = dr[j] >> 16;
+            if (d < (uint32_t)RADIX) {
+                const uint32_t q = s_start[d] + (dr[j] & 0xFFFFu);
+                s_keys[q] = k[j];
+                s_pos[q] = v[j];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * BLOCK + dg;
+            if (q < valid) {
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = (bucket_of(key, b.rb, b.cmul, b.bsh) - blo) & (RADIX - 1);
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < m) {
+                    out_keys[g] = key;
+                    out_vals[g] = s_pos[q];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            k[j] = kn[j];
+            v[j] = vn[j];
+        }
+        t = tn;
+        par ^= 1u;
+    }
+    for (uint32_t i = dg; i < 1024u; i += BLOCK)
+        if (s_hhi[i]) atomicAdd(&ghist_hi[i], s_hhi[i]);
+}
+
+// ---------------------------------------------------------------------------
 // The second bucket pass without a look-back.  Its input is ordered by the
 // first pass's digit l (the bucket's low kLoBits): segment l of the input is
 // [lo_base[l], lo_base[l + 1]).  The pass must keep l's order only, and

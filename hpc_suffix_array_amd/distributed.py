@@ -257,6 +257,22 @@ class DistributedSA:
         self.r = dist.get_rank(group)
         self.stats = {}
 
+    def _mark(self, name: str, dev) -> None:
+        """HIP event on the build stream at a phase boundary (stats["phase_ms"])."""
+        if dev.type != "cuda":
+            return
+        e = torch.cuda.Event(enable_timing=True)
+        e.record(torch.cuda.current_stream(dev))
+        self._events.append((name, e))
+
+    def _phase_ms(self) -> dict:
+        out = {}
+        if len(self._events) > 1:
+            self._events[-1][1].synchronize()
+            for (a, ea), (_, eb) in zip(self._events, self._events[1:]):
+                out[a] = round(out.get(a, 0.0) + ea.elapsed_time(eb), 4)
+        return out
+
     def _min_all(self, x: int, dev) -> int:
         if self.G == 1:
             return int(x)
@@ -269,6 +285,8 @@ class DistributedSA:
         dev = text.device
         lo, hi = n * r // G, n * (r + 1) // G
         self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": []}
+        self._events = []
+        self._mark("alphabet", dev)
         # alphabet of the whole text: OR of the slices' masks (MAX of flags;
         # the NCCL backend has no bitwise-or reduction)
         _trace("alphabet", r, G, n)
@@ -280,6 +298,7 @@ class DistributedSA:
         if n < 2:
             return self._fallback(text, n, "n < 2")
         _trace("begin")
+        self._mark("begin", dev)
         info, coarse = self.ops.begin(text, n, G, r, present)
         self.stats.update(sigma=info["sigma"], K=info["K"], bucket_bits=info["bucket_bits"])
         if info["status"] != N.DIST_OK:   # identical on every rank (global alphabet and n)
@@ -295,6 +314,7 @@ class DistributedSA:
         if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
             return self._fallback(text, n, "unbalanced bucket ranges")
         sa_local = self.ops.empty(info["m"], I32)
+        self._mark("round1", dev)
         info = self.ops.round1(sa_local)
         _trace("round1", info)
         if self._min_all(info["round1_ok"], dev) == 0:
@@ -304,6 +324,7 @@ class DistributedSA:
         self.stats["heads_round1"] = info["heads"]
         h = self.stats["K"]
         while True:
+            self._mark("requests", dev)
             counts, info = self.ops.req_count(h, G)
             _trace("req_count", h, counts)
             mat = _all_gather_rows(torch.tensor([info["unsorted"]] + counts, dtype=I64, device=dev), self.group)
@@ -316,14 +337,20 @@ class DistributedSA:
             recv_counts = [row[1 + r] for row in mat]
             self.stats["requests"].append(sum(sum(row[1:]) for row in mat))
             req = self.ops.req_fill(h, sum(counts))
+            self._mark("exchange", dev)
             (got,), _ = alltoallv([req], counts, recv_counts, self.group)
             _trace("requests in", got.numel())
+            self._mark("answer", dev)
             ans = self.ops.answer(got)
+            self._mark("exchange", dev)
             (back,), _ = alltoallv([ans], recv_counts, counts, self.group)
+            self._mark("refine", dev)
             self.ops.refine(h, back, sa_local)
             _trace("refined", h)
             self.stats["rounds"] += 1
             h *= 2
+        self._mark("end", dev)
+        self.stats["phase_ms"] = self._phase_ms()
         return sa_local, self.stats["sa_off"]
 
     def _fallback(self, text, n, why):

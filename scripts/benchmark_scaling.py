@@ -53,6 +53,18 @@ def last_json(text):
     raise ValueError("no JSON line in the bench output")
 
 
+def rejected(r):
+    """Why a bench.py line cannot enter the speedup / efficiency table (None
+    when it can): an unverified suffix array, or a weak-scaling (replicas)
+    run -- the reference's sweep divides ONE workload over the processes
+    (benchmark_mpi.py:191-210)."""
+    if r.get("verified") is not True:
+        return f"suffix array not verified: {r.get('verified')}"
+    if r.get("scaling") != "strong":
+        return f"scaling {r.get('scaling')!r}: speedup / efficiency need one string over all GPUs"
+    return None
+
+
 def rows_from(results, workload, n, seq_sa_time=None):
     """results: [(N, bench JSON)] -> CSV rows with speedup/efficiency."""
     base = {N: r for N, r in results}
@@ -107,11 +119,9 @@ def main(argv=None):
             print(f"FAILED (exit {p.returncode}): {p.stderr.strip().splitlines()[-1:]}")
             continue
         r = last_json(p.stdout)
-        if r.get("verified") is not True:
-            print(f"REJECTED (suffix array not verified: {r.get('verified')})")
-            continue
-        if r.get("scaling") != "strong":
-            print(f"REJECTED (scaling {r.get('scaling')!r}: speedup / efficiency need one string over all GPUs)")
+        why = rejected(r)
+        if why:
+            print(f"REJECTED ({why})")
             continue
         results.append((N, r))
         print(f"OK ({r['ms_per_step']:.2f} ms, {r['value'] / 1e9:.2f} G suffixes/s)")

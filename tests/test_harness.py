@@ -111,3 +111,8 @@ def test_scaling_harness_columns_and_commands():
     assert rows[1]["speedup"] == pytest.approx(1.6) and rows[1]["efficiency"] == pytest.approx(0.8)
     assert rows[0]["speedup_vs_cpu"] == pytest.approx(2500.0)
     assert S.last_json('noise\n{"a": 1}\n') == {"a": 1}
+    # only verified strong-scaling lines (one string over all GPUs) enter
+    assert S.rejected({"verified": True, "scaling": "strong"}) is None
+    assert "scaling" in S.rejected({"verified": True, "scaling": "weak"})
+    assert "verified" in S.rejected({"verified": False, "scaling": "strong"})
+    assert "verified" in S.rejected({"scaling": "strong"})
