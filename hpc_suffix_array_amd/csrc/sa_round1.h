@@ -27,6 +27,14 @@
 #ifndef SA_ITEMS_B
 #define SA_ITEMS_B 10
 #endif
+// local sort: 1 = size-classed sub-bucket networks (k_bucket_sort_cls), 0 =
+// 16-input network per sub-bucket (k_bucket_sort).  Measured at 2^30 DNA on
+// one box: 8.5 ms (class lists + per-thread re-count of the groups; 12.7 ms
+// with row-ballot segments) against 7.3 ms -- the list building and the
+// re-count cost more than the smaller networks save; kept for A/B runs.
+#ifndef SA_LOCAL_SORT_CLS
+#define SA_LOCAL_SORT_CLS 0
+#endif
 
 struct BucketPlan {
     BucketSpec bs{};
@@ -298,9 +306,15 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_LOCAL_SORT);
     {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
+#if SA_LOCAL_SORT_CLS
+        hipLaunchKernelGGL((k_bucket_sort_cls<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
+                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
+                           c->keys[0], d_sa, skew, so);
+#else
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
                            c->keys[0], d_sa, skew, so);
+#endif
         // skewed windows are rare: a small grid loops over them (one
         // workgroup per listed window spent 0.1 ms on empty workgroups)
         const uint32_t gl = std::min<uint32_t>(g, 1024);
