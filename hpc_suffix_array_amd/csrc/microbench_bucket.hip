@@ -147,7 +147,16 @@ int main(int argc, char** argv) {
                                words, ib, okeys, ovals, skew, SegOut{});
         });
     }
-    for (uint32_t g : {512u, 1024u}) {
+    for (uint32_t g : {512u, hw[7]}) {
+        char nm[64];
+        std::snprintf(nm, sizeof nm, "bucket_sort_cls + seg grid %u", g);
+        timeit(nm, [&] {
+            hipLaunchKernelGGL((k_bucket_sort_cls<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys,
+                               ovals, skew, so);
+        });
+    }
+    for (uint32_t g : {512u, 1024u, hw[7]}) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "bucket_sort 512x18 + seg grid %u", g);
         timeit(nm, [&] {
