@@ -357,6 +357,7 @@ def main():
         line = json.dumps(out)
         print(line, flush=True)
         if a.json_out:
+            os.makedirs(os.path.dirname(os.path.abspath(a.json_out)), exist_ok=True)
             with open(a.json_out, "w") as f:
                 f.write(line + "\n")
     if use_pg:

@@ -131,3 +131,18 @@ def test_distributed_gloo_sliced_exchange(oracle):
     """The sliced all_to_all_v / all_gather paths (XCHUNK, CHUNK tiny)."""
     _run(oracle, 3, chunks=(97, 1000))
     _run(oracle, 2, chunks=(97, 1000), driver="sample")
+
+
+def test_exchange_slice_limit():
+    """The all_to_all slice bound the exchanges rely on: one all_to_all_single
+    of 2^28 int64 (2 GiB) returned half garbage on this ROCm stack, so every
+    collective moves at most XCHUNK elements per peer pair -- below 2^31 bytes
+    for the widest payload (int64) -- and gather_sa's all_gather slices stay
+    below 2^31 bytes per rank too."""
+    from hpc_suffix_array_amd import distributed as D
+    assert D.XCHUNK * 8 < (1 << 31)
+    assert D.CHUNK * 8 < (1 << 31)
+    # the 1 GiB DNA build's request exchange at G = 2 (~0.5 M int32 per peer)
+    # and the sample-sort fallback's bucket exchange at 2^30 / 8 ranks (2^27
+    # int64 per peer) are sliced into 1 and 4 collectives
+    assert -(-(1 << 19) // D.XCHUNK) == 1 and -(-(1 << 27) // D.XCHUNK) == 4
