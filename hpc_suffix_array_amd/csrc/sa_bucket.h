@@ -137,28 +137,28 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t (&v)[NB / 4], int j) 
 constexpr uint32_t kCoarseBits = 12;
 constexpr uint32_t kCoarse = 1u << kCoarseBits;
 
-// LIST: the suffixes counted (one rank's bucket range) are also written as
-// compacted records (key1 -> lkeys, position -> lpos) for the record-driven
-// first pass (k_split_list): key1 rolls here from the LDS-staged digits at
-// full occupancy, and the first pass only ranks and scatters the range's
-// ~n/G.  Two sweeps over the workgroup's tiles: count (and histogram), one
-// claim of the workgroup's output range from *cursor, then the records --
-// a claim per 4096-position tile (262 K claims on one counter at 2^30)
-// serialised at ~10 ns each.
-template <bool POW2 = false, bool COARSE = false, bool LIST = false>
+// LM (list mode), for the record-driven first pass (k_split_list) of one
+// rank's bucket range: the suffixes counted are written as compacted records
+// (key1 -> lkeys, position -> lpos), key1 computed from the LDS-staged digits
+// for the kept positions only (~1/G of them).  Two launches over the same
+// grid: LM = 1 histograms and counts each workgroup's kept positions (wg[]),
+// an exclusive scan (k_exscan_u32) turns the counts into offsets, LM = 2
+// writes each workgroup's records from its offset (no claims: a claim per
+// 4096-position tile on one counter serialised; LM = 1 keeps the plain
+// histogram's occupancy).
+template <bool POW2 = false, bool COARSE = false, int LM = 0>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
                                                         uint32_t* __restrict__ ghist, uint64_t p0, uint64_t p1,
                                                         uint32_t blo, uint32_t bhi,
                                                         uint64_t* __restrict__ lkeys = nullptr,
                                                         uint32_t* __restrict__ lpos = nullptr,
-                                                        uint32_t* __restrict__ cursor = nullptr) {
+                                                        uint32_t* __restrict__ wg = nullptr) {
     constexpr int RUN = kTile / kBlock;   // 16
     constexpr uint32_t NB = COARSE ? kCoarse : kLoRadix;
     __shared__ uint32_t s_tmp[kWaves];
-    __shared__ uint32_t s_base;
-    // LIST: the tile's kept positions (tile offsets), compacted
-    __shared__ uint16_t s_rp[LIST ? kTile : 1];
+    // LM = 2: the tile's kept positions (tile offsets), compacted
+    __shared__ uint16_t s_rp[LM == 2 ? kTile : 1];
     __shared__ uint8_t s_map[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
     uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
@@ -174,16 +174,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     const uint32_t bspan = bhi - blo;
     __syncthreads();
     const uint64_t tiles = (p1 - p0 + kTile - 1) / kTile;
-    uint32_t kept_lane = 0;   // LIST sweep 0: this lane's kept positions
-    uint32_t run = 0;         // LIST sweep 1: the workgroup's next record slot
-    for (int sweep = 0; sweep < (LIST ? 2 : 1); ++sweep) {
-    if (LIST && sweep == 1) {
-        uint32_t tot;
-        block_exclusive_sum(kept_lane, s_tmp, &tot);
-        if (threadIdx.x == 0) s_base = tot ? atomicAdd(cursor, tot) : 0u;
-        __syncthreads();
-        run = s_base;
-    }
+    uint32_t kept_lane = 0;                        // LM = 1: this lane's kept positions
+    uint32_t run = LM == 2 ? wg[blockIdx.x] : 0u;  // LM = 2: the workgroup's next record slot
     for (uint64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
         const uint64_t tb = p0 + tt * kTile;
         {
@@ -244,14 +236,14 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 } else {
                     const uint32_t lb = bk - blo;
                     if (lb < bspan) {
-                        if (sweep == 0) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
+                        if (LM != 2) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
                         keep |= 1u << j;
                     }
                 }
             }
         }
-        if (LIST && sweep == 0) kept_lane += (uint32_t)__popc(keep);
-        if (LIST && sweep == 1) {
+        if (LM == 1) kept_lane += (uint32_t)__popc(keep);
+        if (LM == 2) {
             // the tile's kept positions compacted into LDS in order, then one
             // thread per record computes key1 from the staged digits (only
             // ~1/G of the positions) and writes it coalesced
@@ -285,6 +277,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         }
         __syncthreads();
     }
+    if (LM == 1) {
+        uint32_t tot;
+        block_exclusive_sum(kept_lane, s_tmp, &tot);
+        if (threadIdx.x == 0) wg[blockIdx.x] = tot;
     }
     for (uint32_t i = threadIdx.x; i < NB; i += kBlock) {
         if (!s_hlo[i]) continue;
@@ -292,6 +288,32 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
             atomicAdd(reinterpret_cast<unsigned long long*>(ghist) + i, (unsigned long long)s_hlo[i]);
         else
             atomicAdd(&ghist[i], s_hlo[i]);
+    }
+}
+
+// exclusive scan of cnt u32 entries into out (one workgroup of kBlock lanes,
+// 16 entries per lane per step, carried across steps)
+__global__ __launch_bounds__(kBlock) void k_exscan_u32(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                       uint32_t cnt) {
+    __shared__ uint32_t s_tmp[kWaves];
+    uint32_t carry = 0;
+    for (uint32_t base = 0; base < cnt; base += kBlock * 16) {
+        uint32_t v[16], sum = 0;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t i = base + threadIdx.x * 16 + k;
+            v[k] = i < cnt ? in[i] : 0u;
+            sum += v[k];
+        }
+        uint32_t tot;
+        uint32_t off = block_exclusive_sum(sum, s_tmp, &tot) + carry;
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const uint32_t i = base + threadIdx.x * 16 + k;
+            if (i < cnt) out[i] = off;
+            off += v[k];
+        }
+        carry += tot;
     }
 }
 

@@ -154,10 +154,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
     // digit totals of both bucket passes (one read of the text)
     // a rank's range of a multi-GPU build holding at most a quarter of the
-    // text: the histogram pass also emits the range's (key1, position)
-    // records and the first pass scatters those (sim_ranks at 2^30 DNA, G = 8:
-    // ...; at G = 2 streaming the text through k_split_text is cheaper than
-    // writing and reading 12-byte records for half of it)
+    // text: the histogram pass counts the range's suffixes per workgroup, a
+    // second launch over the same tiles emits their (key1, position) records
+    // and the first pass scatters those (scripts/sim_ranks.py at 2^30 DNA,
+    // G = 8: per-rank round 1 5.0 -> 4.0 ms against k_split_text filtering the
+    // whole text; at G = 2 streaming the text through k_split_text is cheaper
+    // than writing and reading 12-byte records for half of it)
     const bool listed = m <= n / 4;
     uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
     uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
@@ -166,13 +168,20 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
-#define SA_HIST(P, L)                                                                                         \
+        uint32_t* const wgcnt = c->hist;       // per-workgroup kept counts, then offsets (the
+        uint32_t* const wgoff = c->hist + g;   // chunk histograms are free in the bucketed round)
+#define SA_HIST(P, L, W)                                                                                      \
     hipLaunchKernelGGL((k_bucket_hist<P, false, L>), dim3(g), dim3(kBlock), 0, s, d_text, n,                  \
-                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, os_tickets(c) + 2)
-        if (pow2 && listed) SA_HIST(true, true);
-        else if (pow2) SA_HIST(true, false);
-        else if (listed) SA_HIST(false, true);
-        else SA_HIST(false, false);
+                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
+        if (pow2 && listed) SA_HIST(true, 1, wgcnt);
+        else if (pow2) SA_HIST(true, 0, wgcnt);
+        else if (listed) SA_HIST(false, 1, wgcnt);
+        else SA_HIST(false, 0, wgcnt);
+        if (listed) {
+            hipLaunchKernelGGL(k_exscan_u32, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)wgcnt, wgoff, g);
+            if (pow2) SA_HIST(true, 2, wgoff);
+            else SA_HIST(false, 2, wgoff);
+        }
 #undef SA_HIST
     }
     tm.end();
