@@ -448,7 +448,10 @@ __global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restri
 // appended to `skew` (count in words[10]) and left to k_bucket_sort_lsd.
 // err bit 0: window larger than the LDS tile; bit 1: key span too wide.
 // ---------------------------------------------------------------------------
-constexpr int kSubBits = 11;
+#ifndef SA_SUB_BITS
+#define SA_SUB_BITS 11
+#endif
+constexpr int kSubBits = SA_SUB_BITS;
 constexpr int kSubBuckets = 1 << kSubBits;
 constexpr uint32_t kMaxSub = 64;
 

@@ -153,14 +153,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     SA_HIP(hipMemsetAsync(c->words, 0, 12, s));
     SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
     // digit totals of both bucket passes (one read of the text)
-    // a rank's range of a multi-GPU build holding at most a quarter of the
+    // a rank's range of a multi-GPU build holding at most ~a quarter of the
     // text: the histogram pass counts the range's suffixes per workgroup, a
     // second launch over the same tiles emits their (key1, position) records
     // and the first pass scatters those (scripts/sim_ranks.py at 2^30 DNA,
     // G = 8: per-rank round 1 5.0 -> 4.0 ms against k_split_text filtering the
     // whole text; at G = 2 streaming the text through k_split_text is cheaper
     // than writing and reading 12-byte records for half of it)
-    const bool listed = m <= n / 4;
+    const bool listed = m * 10 <= n * 3;   // G >= 4: every rank's ~n/G (balanced cuts are within a few %)
     uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
     uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
     tm.begin(SA_K_PACK);

@@ -92,7 +92,7 @@ def _all_to_all_single(out: torch.Tensor, inp: torch.Tensor, rs=None, ss=None, g
 
 
 def alltoallv(tensors: List[torch.Tensor], send: List[int], recv: Optional[List[int]] = None,
-              group=None) -> Tuple[List[torch.Tensor], List[int]]:
+              group=None, slices: Optional[int] = None) -> Tuple[List[torch.Tensor], List[int]]:
     """all_to_all_v of each tensor (send[j] elements to rank j, in rank order).
     Each collective moves at most XCHUNK elements per peer pair: one
     all_to_all_single of 2^28 int64 (2 GiB) returned half garbage on this
@@ -108,9 +108,12 @@ def alltoallv(tensors: List[torch.Tensor], send: List[int], recv: Optional[List[
         _all_to_all_single(rc, sc, group=group)
         recv = rc.tolist()
     C = XCHUNK
-    t_loc = torch.tensor([max([0] + [(x + C - 1) // C for x in list(send) + list(recv)])], dtype=I64, device=dev)
-    _all_reduce(t_loc, op=dist.ReduceOp.MAX, group=group)
-    T = int(t_loc.item())
+    if slices is None:   # the slice count, agreed by every rank
+        t_loc = torch.tensor([max([0] + [(x + C - 1) // C for x in list(send) + list(recv)])], dtype=I64, device=dev)
+        _all_reduce(t_loc, op=dist.ReduceOp.MAX, group=group)
+        T = int(t_loc.item())
+    else:                # known to every rank already (e.g. from an all_gathered count matrix)
+        T = int(slices)
     so = [sum(send[:j]) for j in range(G)]
     ro = [sum(recv[:j]) for j in range(G)]
     outs = []
@@ -336,14 +339,17 @@ class DistributedSA:
                 raise RuntimeError("distributed doubling did not converge")
             recv_counts = [row[1 + r] for row in mat]
             self.stats["requests"].append(sum(sum(row[1:]) for row in mat))
+            # every rank holds the whole count matrix: the slice count of both
+            # exchanges needs no extra collective
+            slices = max([0] + [(x + XCHUNK - 1) // XCHUNK for row in mat for x in row[1:]])
             req = self.ops.req_fill(h, sum(counts))
             self._mark("exchange", dev)
-            (got,), _ = alltoallv([req], counts, recv_counts, self.group)
+            (got,), _ = alltoallv([req], counts, recv_counts, self.group, slices)
             _trace("requests in", got.numel())
             self._mark("answer", dev)
             ans = self.ops.answer(got)
             self._mark("exchange", dev)
-            (back,), _ = alltoallv([ans], recv_counts, counts, self.group)
+            (back,), _ = alltoallv([ans], recv_counts, counts, self.group, slices)
             self._mark("refine", dev)
             self.ops.refine(h, back, sa_local)
             _trace("refined", h)
