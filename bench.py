@@ -22,7 +22,10 @@ algorithmic bytes per launch over its mean launch duration, timed in the
 timed region; N = 1; "traffic" from the committed rocprof summary of the same
 workload), "kernels_gbs" (the same for every kernel kind) and "cpu_baseline"
 (the oracle's reference-identical single-thread restatement of src/sequential
-on a bounded sample, rank 0, N = 1 only).
+on a bounded sample, rank 0, N = 1 only) and "reference_schedule" (N = 1: the
+same text built with the north-star schedule -- one LSD-sorted doubling round
+per h, manber_myers.c:97-125 -- so its ms/doubling-round compares with the
+reference's rounds; not the headline value).
 """
 from __future__ import annotations
 
@@ -72,7 +75,9 @@ def parse():
     ap.add_argument("--kind", default="dna", choices=sorted(ALPHABETS) + ["degenerate"])
     ap.add_argument("--seed", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample-n", type=int, default=1 << 25)
+    ap.add_argument("--cpu-sample-n", type=int, default=1 << 26)
+    ap.add_argument("--no-reference-schedule", action="store_true",
+                    help="skip the companion build with the north-star schedule (N = 1, packed runs only)")
     ap.add_argument("--no-profile", action="store_true", help="no per-launch HIP events")
     ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("--init-chars", type=int, default=0)
@@ -160,6 +165,27 @@ def timed(steps, warmup, fn, barrier):
     return time.perf_counter() - t0, res
 
 
+def reference_schedule(b, d_text, n, d_sa, sptr, a, torch, dev, reps: int = 2) -> dict:
+    """The north-star-shaped schedule beside the packed headline: one
+    doubling round per h = 1, 2, 4, ... (manber_myers.c:97-125), each a
+    full LSD radix sort of (rank, rank[i+h]) keys.  One warm-up build, then
+    `reps` timed builds (wall clock between stream syncs), and the O(n)
+    check of the last one -- not part of the headline `value`."""
+    kw = dict(stream=sptr, profile=True, schedule="reference", init_chars=0, radix=a.radix)
+    b.build(d_text, n, d_sa, **kw)
+    times, st = [], None
+    for _ in range(reps):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        st = b.build(d_text, n, d_sa, **kw)
+        torch.cuda.synchronize(dev)
+        times.append(time.perf_counter() - t0)
+    ms = 1e3 * statistics.median(times)
+    return {"ms_per_step": round(ms, 3), "value": n / (ms / 1e3), "rounds": st["rounds"],
+            "ms_per_round": [round(x, 3) for x in st["round_ms"]], "prefix_len_per_round": st["prefix_len"],
+            "passes_per_round": st["passes"], "verified": b.check(d_text, n, d_sa, stream=sptr)}
+
+
 def run_single(a, torch, dev, world, rank, barrier):
     """Single-GPU builder; with world > 1 (--mode replicas) one string per rank."""
     from hpc_suffix_array_amd import DeviceBuilder
@@ -174,6 +200,9 @@ def run_single(a, torch, dev, world, rank, barrier):
                round1=a.round1)
     elapsed, stats = timed(a.steps, a.warmup, lambda: b.build(d_text, n, d_sa, **bkw), barrier)
     verified = b.check(d_text, n, d_sa, stream=sptr)
+    ref_sched = None
+    if world == 1 and a.schedule == "packed" and not a.no_reference_schedule:
+        ref_sched = reference_schedule(b, d_text, n, d_sa, sptr, a, torch, dev)
 
     rounds = stats[-1]["rounds"]
     round_ms = [statistics.mean(s["round_ms"][j] for s in stats) for j in range(rounds)]
@@ -225,6 +254,7 @@ def run_single(a, torch, dev, world, rank, barrier):
         "roofline": roofline,
         "kernels_gbs": per_kernel,
         "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
+        "reference_schedule": ref_sched,
     }
     b.close()
     return elapsed, extra
@@ -363,7 +393,7 @@ def main():
     if use_pg:
         dist.destroy_process_group()
     # a build that fails the O(n) check must not pass for a measurement
-    if out.get("verified") is False:
+    if out.get("verified") is False or (out.get("reference_schedule") or {}).get("verified") is False:
         print("bench.py: the suffix array failed the O(n) check", file=sys.stderr, flush=True)
         sys.exit(3)
 

@@ -403,6 +403,43 @@ def mask_positions(mask: torch.Tensor) -> torch.Tensor:
     return torch.cat(parts) if parts else torch.zeros(0, dtype=I64, device=mask.device)
 
 
+def chunked_map(fn, *ts: torch.Tensor) -> torch.Tensor:
+    """fn applied elementwise over CHUNK-element slices of equal-length
+    vectors: torch's own kernels never see 2^30 elements here (bincount and
+    index_put faulted at that size on ROCm)."""
+    m = ts[0].numel()
+    if m <= CHUNK:
+        return fn(*ts)
+    return torch.cat([fn(*(t[a: a + CHUNK] for t in ts)) for a in range(0, m, CHUNK)])
+
+
+def count_below(sorted_x: torch.Tensor, q: torch.Tensor, right: bool = False) -> torch.Tensor:
+    """For each q the number of elements of the sorted vector < q (<= q with
+    right): searchsorted within each CHUNK slice, summed."""
+    out = torch.zeros(q.numel(), dtype=I64, device=q.device)
+    for a in range(0, sorted_x.numel(), CHUNK):
+        out += torch.searchsorted(sorted_x[a: a + CHUNK], q, right=right)
+    return out
+
+
+def cumsum_i64(x: torch.Tensor) -> torch.Tensor:
+    """Inclusive int64 prefix sum over CHUNK slices, carrying the last sum
+    (a device scalar, no host sync) into the next slice."""
+    parts, carry = [], None
+    for a in range(0, x.numel(), CHUNK):
+        s = torch.cumsum(x[a: a + CHUNK].to(I64), 0)
+        if carry is not None:
+            s += carry
+        carry = s[-1]
+        parts.append(s)
+    return torch.cat(parts) if parts else torch.zeros(0, dtype=I64, device=x.device)
+
+
+def count_true(mask: torch.Tensor) -> int:
+    """Number of set elements of a bool vector (summed per CHUNK slice)."""
+    return int(sum(int(mask[a: a + CHUNK].sum().item()) for a in range(0, mask.numel(), CHUNK)))
+
+
 def bit_width(x: int) -> int:
     return int(x).bit_length()
 
@@ -532,7 +569,7 @@ class SampleSortSA:
         else:
             sd, order = self.ops.argsort(dest.to(I64), bit_width(self.G - 1))
             q = torch.arange(self.G + 1, dtype=I64, device=dest.device)
-            send = torch.diff(torch.searchsorted(sd, q)).tolist()
+            send = torch.diff(count_below(sd, q)).tolist()
         outs, recv = self._alltoallv([self.ops.gather(t, order) for t in tensors], send)
         return outs, recv, order, send
 
@@ -565,8 +602,9 @@ class SampleSortSA:
                 cuts.append(m)
                 continue
             ks, rs, ps, _ = allsamp[min(len(allsamp) - 1, j * len(allsamp) // self.G)]
-            lo = int(torch.searchsorted(keys, torch.tensor([ks], dtype=I64, device=dev), right=False).item())
-            hi = int(torch.searchsorted(keys, torch.tensor([ks], dtype=I64, device=dev), right=True).item())
+            kt = torch.tensor([ks], dtype=I64, device=dev)
+            lo = int(count_below(keys, kt).item())
+            hi = int(count_below(keys, kt, right=True).item())
             if self.r < rs:
                 c = hi
             elif self.r > rs:
@@ -631,14 +669,16 @@ class SampleSortSA:
         """For each element the value of idx at the last head at or before it
         (scanning across ranks)."""
         m = head.numel()
-        local_last = int(torch.where(head, idx, torch.full_like(idx, -1)).max().item()) if m else -1
+        local_last = -1
+        for a in range(0, m, CHUNK):
+            local_last = max(local_last, int(torch.where(head[a: a + CHUNK], idx[a: a + CHUNK], -1).max().item()))
         lasts = self._gather(torch.tensor([local_last], dtype=I64, device=dev)).reshape(-1).tolist()
         carry = max([-1] + lasts[: self.r])
         if m == 0:
             return idx
-        v = torch.where(head, idx, torch.full_like(idx, -1))
+        v = chunked_map(lambda hd, ix: torch.where(hd, ix, -1), head, idx)
         v = self.ops.running_max(v)
-        return torch.where(v < 0, torch.full_like(v, carry), v)
+        return chunked_map(lambda x: torch.where(x < 0, carry, x), v)
 
     # -- the build ----------------------------------------------------------------
     def build(self, text: torch.Tensor, n: int) -> torch.Tensor:
@@ -650,7 +690,7 @@ class SampleSortSA:
         bnd_t = torch.tensor(bnd[1:-1], dtype=I64, device=dev)
 
         def owner(x):
-            return torch.searchsorted(bnd_t, x, right=True)
+            return chunked_map(lambda y: torch.searchsorted(bnd_t, y, right=True), x)
 
         # alphabet: OR of the ranks' presence masks (torch's NCCL backend has
         # no BOR reduction, so gather the 8 words and OR them here)
@@ -685,7 +725,7 @@ class SampleSortSA:
         keep = ~single
         sel = mask_positions(keep)
         upos, uidx, uhead = (self.ops.gather(t, sel) for t in (gpos, idx, hpos))
-        D = self._sum(int(head.sum().item()), dev)
+        D = self._sum(count_true(head), dev)
         self.stats["rounds"] = 1
         self.stats["distinct"].append(D)
         wr = bit_width(n)
@@ -710,9 +750,9 @@ class SampleSortSA:
             self.ops.scatter(r1, vsel, 0, tmp)
             # dense group id (groups are contiguous in SA order across ranks)
             ghead, _ = self._run_flags([uhead], dev)
-            gcount = int(ghead.sum().item())
+            gcount = count_true(ghead)
             gcounts = self._gather(torch.tensor([gcount], dtype=I64, device=dev)).reshape(-1).tolist()
-            g = torch.cumsum(ghead.to(I64), 0) - 1 + sum(gcounts[:r])
+            g = cumsum_i64(ghead) + (sum(gcounts[:r]) - 1)
             ngroups = sum(gcounts)
             wg = bit_width(max(ngroups - 1, 0))
             if wg + wr <= 63:
@@ -735,7 +775,7 @@ class SampleSortSA:
             fin_pos.append(self.ops.gather(pos, sel))
             fin_idx.append(self.ops.gather(uidx, sel))
             keep = ~rsingle
-            D = (n - total_u) + self._sum(int(rhead.sum().item()), dev)
+            D = (n - total_u) + self._sum(count_true(rhead), dev)
             self.stats["rounds"] += 1
             self.stats["distinct"].append(D)
             sel = mask_positions(keep)
