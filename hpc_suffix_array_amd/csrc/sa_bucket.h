@@ -553,20 +553,27 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
     return true;
 }
 
+// ksh = 0: every sorted key1 to keys_out[p]; else only the key1 of every
+// 2^ksh-th SA position p, to keys_out[p >> ksh] (the sparse rank look-ups
+// search these samples, then the last 2^ksh slots by key1 rebuilt from SA and
+// text: lower_bound_sampled in sa_kernels.h) -- 0.5 instead of 8 bytes per
+// suffix written
 template <int BLOCK, int ITEMS>
 __device__ __forceinline__ void store_window(const uint64_t* __restrict__ s_w, uint64_t a, uint32_t m, uint32_t ib,
                                              uint64_t mn, uint64_t* __restrict__ keys_out,
-                                             uint32_t* __restrict__ sa_out) {
+                                             uint32_t* __restrict__ sa_out, uint32_t ksh) {
     constexpr int WT = kWave * ITEMS;
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
+    const uint64_t smask = (1ull << ksh) - 1ull;
 #pragma unroll 2
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t le = wave * WT + i * kWave + lane;
         if (le < m) {
             const uint64_t x = s_w[le];
-            keys_out[a + le] = (x >> ib) + mn;
-            sa_out[a + le] = (uint32_t)(x & imask);
+            const uint64_t p = a + le;
+            if ((p & smask) == 0) keys_out[p >> ksh] = (x >> ib) + mn;
+            sa_out[p] = (uint32_t)(x & imask);
         }
     }
 }
@@ -592,6 +599,7 @@ struct SegOut {
     uint32_t* tmp_g;
     uint32_t* cnt_u;
     uint32_t* cnt_g;
+    uint32_t ksh;   // sorted key1 written for every 2^ksh-th SA position only (store_window)
 };
 
 template <int BLOCK, int ITEMS>
@@ -887,7 +895,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             for (int i = 0; i < ITEMS; ++i)
                 if (wave * WT + i * kWave + lane < m) s_w[wave * WT + i * kWave + lane] = w[i];
             __syncthreads();
-            store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+            store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
             __syncthreads();
             continue;
         }
@@ -1081,7 +1089,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         }
         __syncthreads();
         stamp(5);
-        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
         stamp(6);
     }
@@ -1394,7 +1402,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort_cls(const uint64_t* __
             }
         }
         __syncthreads();
-        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
     }
     flush_totals(words, th, tu, tg);
@@ -1511,7 +1519,7 @@ __global__ __launch_bounds__(BLOCK) void k_bucket_sort_lsd(const uint64_t* __res
         if (so.rank)
             window_segments<BLOCK, ITEMS>(s_w, reinterpret_cast<uint64_t*>(&s_wcnt[0][0]), s_red, a, m, ib, j, so, th,
                                           tu, tg);
-        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out);
+        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
         __syncthreads();
     }
     flush_totals(words, th, tu, tg);

@@ -618,6 +618,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const uint64_t base = (uint64_t)sigma + 1;
     const Chunking ch = plan_chunks(n);
     uint64_t* keys1 = nullptr;
+    uint32_t ksh1 = 0;   // bucketed round 1: keys1 holds every 2^ksh1-th sorted key1
     uint32_t P = 0;
 
     // round 1: sort every suffix by its first K symbols -- bucketed (two
@@ -629,7 +630,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint64_t seg1[3] = {0, 0, 0};
     if (bucketed) {
         bool done = false;
-        rc = round1_bucketed(c, d_text, n, d_sa, bp, full_range(bp, n), s, tm, st, &done, &fused, seg1);
+        rc = round1_bucketed(c, d_text, n, d_sa, bp, full_range(bp, n), s, tm, st, &done, &fused, seg1, &ksh1);
         if (rc) return rc;
         bucketed = done;
         if (done) {
@@ -679,7 +680,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
     uint64_t* ukb1 = c->keys_u;
     const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K,
-                        bucketed ? 1u : 0u, bp.bs, bucketed ? c->segw + kBstartOff : nullptr};
+                        bucketed ? 1u : 0u, bp.bs, bucketed ? c->segw + kBstartOff : nullptr, d_sa, ksh1};
     if (st) st->sparse_ranks = sparse ? 1 : 0;
     SA_HIP(hipEventRecord(ev.e[1], s));
     SA_HIP(hipEventSynchronize(ev.e[1]));

@@ -55,6 +55,8 @@ struct DistState {
     std::vector<uint32_t> cut;
     uint32_t blo = 0, bhi = 0;
     uint64_t m = 0, sa_off = 0, mcap = 0;
+    uint32_t* sa = nullptr;          // this range's SA (the caller's slice, from round 1 on)
+    uint32_t ksh = 0;                // round-1 key samples: every 2^ksh-th key1
     // device
     uint64_t cap_n = 0, cap_m = 0;
     uint16_t* owner_tab = nullptr;   // kCoarse: coarse bucket -> rank
@@ -136,67 +138,6 @@ static int ensure_dist_m(sa_context* c, uint64_t m) {
 // ---------------------------------------------------------------------------
 // kernels
 // ---------------------------------------------------------------------------
-// key1 of suffix j (sa_bucket.h layout) from the text in HBM: the bytes of
-// [j, j + K) arrive as independent aligned words (one memory latency instead
-// of K dependent byte + table loads), digits through the LDS byte map (code -
-// 1; 0 past the end).  FULL = false: only D (the bucket's input).
-constexpr int kKeyWords = 8;   // K <= 29 symbols; longer keys take the byte loop
-
-template <bool FULL>
-__device__ __forceinline__ uint64_t key1_words(const uint8_t* __restrict__ text, uint64_t n,
-                                               const uint8_t* __restrict__ s_map, const BucketSpec& b, uint64_t j,
-                                               uint32_t* D_out) {
-    const uint32_t K = FULL ? b.s + b.R : b.s;
-    uint64_t D = 0, r = 0;
-    if (K + 3 <= 4 * kKeyWords) {
-        const uint64_t base = j & ~3ull;
-        const uint32_t sh = (uint32_t)(j & 3);
-        uint32_t w[kKeyWords + 1];
-#pragma unroll
-        for (int q = 0; q <= kKeyWords; ++q) {
-            const uint64_t a = base + 4ull * q;
-            if (a + 4 <= n) {
-                w[q] = *reinterpret_cast<const uint32_t*>(text + a);
-            } else {
-                uint32_t v = 0;
-                for (int i = 0; i < 4; ++i)
-                    if (a + i < n) v |= (uint32_t)text[a + i] << (8 * i);
-                w[q] = v;
-            }
-        }
-#pragma unroll
-        for (int q = 0; q < kKeyWords; ++q) {
-            const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
-#pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint32_t t = 4 * q + i;
-                if (t < K) {
-                    const uint32_t c = (j + t < n) ? (uint32_t)s_map[(x >> (8 * i)) & 0xFFu] : 0u;
-                    if (t < b.s) D = D * b.sigma + c;
-                    else r = r * b.sigma + c;
-                }
-            }
-        }
-    } else {
-        for (uint32_t t = 0; t < K; ++t) {
-            const uint32_t c = (j + t < n) ? (uint32_t)s_map[text[j + t]] : 0u;
-            if (t < b.s) D = D * b.sigma + c;
-            else r = r * b.sigma + c;
-        }
-    }
-    *D_out = (uint32_t)D;
-    if (!FULL) return 0;
-    const uint64_t L = n - j;
-    uint64_t low;
-    if (L < b.s) {
-        low = L - 1;
-    } else {
-        const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
-        low = b.s + r * (b.R + 1) + tl;
-    }
-    return (D << b.rb) | low;
-}
-
 // the 256-entry byte -> dense digit map in LDS (code - 1, absent bytes 0)
 __device__ __forceinline__ void load_map(const uint16_t* __restrict__ code, uint8_t* s_map) {
     for (uint32_t i = threadIdx.x; i < 256; i += blockDim.x) {
@@ -277,7 +218,9 @@ __global__ __launch_bounds__(kBlock) void k_dist_fill(const uint32_t* __restrict
 struct DistLookup {
     const uint32_t* __restrict__ grank;
     const uint32_t* __restrict__ gmember;
-    const uint64_t* __restrict__ keys1;    // this range's sorted key1 (m)
+    const uint64_t* __restrict__ keys1;    // this range's sorted key1: every 2^ksh-th of m
+    const uint32_t* __restrict__ sa;       // this range's SA (m; key1 of the other slots)
+    uint32_t ksh;
     const uint32_t* __restrict__ bstart;   // local bucket starts
     const uint8_t* __restrict__ text;
     const uint16_t* __restrict__ code;
@@ -297,17 +240,11 @@ __device__ __forceinline__ uint64_t dist_rank_of(const DistLookup& L, const uint
         *bad = true;
         return 0;
     }
-    uint64_t lo = L.bstart[b], len = L.bstart[b + 1] - lo;
-    while (len > 0) {
-        const uint64_t half = len >> 1;
-        if (L.keys1[lo + half] < x) {
-            lo += half + 1;
-            len -= half + 1;
-        } else {
-            len = half;
-        }
-    }
-    return L.sa_off + lo + 1;
+    auto key_at = [&](uint64_t p) {
+        uint32_t d;
+        return key1_words<true>(L.text, L.n, s_map, L.bs, p, &d);
+    };
+    return L.sa_off + lower_bound_sampled(L.keys1, L.ksh, L.sa, L.bstart[b], L.bstart[b + 1], x, key_at) + 1;
 }
 
 __global__ __launch_bounds__(kBlock) void k_dist_answer(const uint32_t* __restrict__ req, uint64_t nreq, DistLookup L,
@@ -510,7 +447,8 @@ static int dist_round1(sa_context* c, const uint8_t* d_text, uint32_t* d_sa, hip
     br.member = d->gmember;
     bool done = false, fused = false;
     uint64_t seg[3] = {0, 0, 0};
-    int rc = round1_bucketed(c, d_text, d->n, d_sa, d->bp, br, s, tm, st, &done, &fused, seg);
+    int rc = round1_bucketed(c, d_text, d->n, d_sa, d->bp, br, s, tm, st, &done, &fused, seg, &d->ksh);
+    d->sa = d_sa;
     tm.flush();
     if (rc) return rc;
     if (!done || !fused) {
@@ -582,7 +520,7 @@ static int dist_answer(sa_context* c, const uint32_t* d_req, uint64_t nreq, uint
     if (nreq == 0) return SA_OK;
     if (!d_req || !d_ans) return set_err(SA_E_INVALID, "NULL request / answer buffer");
     const uint32_t nbl = d->bhi - d->blo;
-    const DistLookup L{d->grank, d->gmember, c->keys[0], c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
+    const DistLookup L{d->grank, d->gmember, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
                        d->n, d->bp.bs, d->blo, nbl, d->sa_off};
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nreq + kBlock - 1) / kBlock, 8192);
     hipLaunchKernelGGL(k_dist_answer, dim3(grid), dim3(kBlock), 0, s, d_req, nreq, L, d_ans, d->cnt + 2 * kDistMaxWorld);
@@ -610,7 +548,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     Timer tm{c, s, false, nullptr};
     const uint64_t m = d->mu, G = d->gu;
     if (d->world == 1) {   // every look-up is local: no request / answer exchange
-        const DistLookup L{d->grank, d->gmember, c->keys[0], c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
+        const DistLookup L{d->grank, d->gmember, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
                            d->n, d->bp.bs, d->blo, d->bhi - d->blo, d->sa_off};
         const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
         hipLaunchKernelGGL(k_dist_r1_local, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[d->uo], m, h, L,

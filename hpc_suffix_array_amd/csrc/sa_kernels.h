@@ -94,28 +94,123 @@ struct BucketSpec {
     uint32_t bb, bsh;  // bucket bits (16..18), bsh = 48 - bb
 };
 
-// key1 of position i, computed from the text (rank look-ups of later rounds)
-__device__ __forceinline__ uint64_t key1_at(const uint8_t* __restrict__ text, const uint16_t* __restrict__ code,
-                                            uint64_t n, const BucketSpec& b, uint64_t i) {
-    uint64_t D = 0;
-    for (uint32_t t = 0; t < b.s; ++t) {
-        const uint32_t c = (i + t < n) ? code[text[i + t]] : 0u;
-        D = D * b.sigma + (c ? c - 1u : 0u);
+// byte -> dense digit (code - 1, absent bytes 0) from the global code table
+struct CodeMap {
+    const uint16_t* __restrict__ code;
+    __device__ __forceinline__ uint32_t operator[](uint32_t b) const {
+        const uint32_t c = code[b];
+        return c ? c - 1u : 0u;
     }
-    const uint64_t L = n - i;
+};
+
+// key1 of suffix j (sa_bucket.h layout) from the text in HBM: the bytes of
+// [j, j + K) arrive as independent aligned words (one memory latency instead
+// of K dependent byte + table loads), digits through the LDS byte map (code -
+// 1; 0 past the end).  FULL = false: only D (the bucket's input).
+constexpr int kKeyWords = 8;   // K <= 29 symbols; longer keys take the byte loop
+
+// Map: byte -> digit by operator[] (the LDS byte map of load_map, or
+// CodeMap over the global code table).
+template <bool FULL, class Map>
+__device__ __forceinline__ uint64_t key1_words(const uint8_t* __restrict__ text, uint64_t n, const Map& s_map,
+                                               const BucketSpec& b, uint64_t j, uint32_t* D_out) {
+    const uint32_t K = FULL ? b.s + b.R : b.s;
+    uint64_t D = 0, r = 0;
+    if (K + 3 <= 4 * kKeyWords) {
+        const uint64_t base = j & ~3ull;
+        const uint32_t sh = (uint32_t)(j & 3);
+        uint32_t w[kKeyWords + 1];
+#pragma unroll
+        for (int q = 0; q <= kKeyWords; ++q) {
+            const uint64_t a = base + 4ull * q;
+            if (a + 4 <= n) {
+                w[q] = *reinterpret_cast<const uint32_t*>(text + a);
+            } else {
+                uint32_t v = 0;
+                for (int i = 0; i < 4; ++i)
+                    if (a + i < n) v |= (uint32_t)text[a + i] << (8 * i);
+                w[q] = v;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < kKeyWords; ++q) {
+            const uint32_t x = __builtin_amdgcn_alignbyte(w[q + 1], w[q], sh);
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint32_t t = 4 * q + i;
+                if (t < K) {
+                    const uint32_t c = (j + t < n) ? (uint32_t)s_map[(x >> (8 * i)) & 0xFFu] : 0u;
+                    if (t < b.s) D = D * b.sigma + c;
+                    else r = r * b.sigma + c;
+                }
+            }
+        }
+    } else {
+        for (uint32_t t = 0; t < K; ++t) {
+            const uint32_t c = (j + t < n) ? (uint32_t)s_map[text[j + t]] : 0u;
+            if (t < b.s) D = D * b.sigma + c;
+            else r = r * b.sigma + c;
+        }
+    }
+    *D_out = (uint32_t)D;
+    if (!FULL) return 0;
+    const uint64_t L = n - j;
     uint64_t low;
     if (L < b.s) {
         low = L - 1;
     } else {
-        uint64_t r = 0;
-        for (uint32_t t = 0; t < b.R; ++t) {
-            const uint32_t c = (i + b.s + t < n) ? code[text[i + b.s + t]] : 0u;
-            r = r * b.sigma + (c ? c - 1u : 0u);
-        }
         const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
         low = b.s + r * (b.R + 1) + tl;
     }
     return (D << b.rb) | low;
+}
+
+// Lower bound of x among the sorted key1 of SA positions [lo, hi) when the
+// first round kept only every 2^ksh-th of them (keys[t] = key1 at position
+// t << ksh, store_window in sa_bucket.h): a binary search of the samples
+// inside [lo, hi) narrows it to at most 2^ksh slots, searched by key1
+// rebuilt from the text at sa[p] (key_at).  ksh = 0: keys holds every key1.
+template <class KeyAt>
+__device__ __forceinline__ uint64_t lower_bound_sampled(const uint64_t* __restrict__ keys, uint32_t ksh,
+                                                        const uint32_t* __restrict__ sa, uint64_t lo, uint64_t hi,
+                                                        uint64_t x, const KeyAt& key_at) {
+    if (ksh == 0) {
+        uint64_t len = hi - lo;
+        while (len > 0) {
+            const uint64_t half = len >> 1;
+            if (keys[lo + half] < x) {
+                lo += half + 1;
+                len -= half + 1;
+            } else {
+                len = half;
+            }
+        }
+        return lo;
+    }
+    const uint64_t s0 = (lo + (1ull << ksh) - 1) >> ksh, s1 = (hi + (1ull << ksh) - 1) >> ksh;
+    uint64_t t = s0, len = s1 - s0;   // first sample in [s0, s1) with key >= x
+    while (len > 0) {
+        const uint64_t half = len >> 1;
+        if (keys[t + half] < x) {
+            t += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    uint64_t l = t > s0 ? ((t - 1) << ksh) + 1 : lo;   // sample t - 1 is < x
+    const uint64_t r = t < s1 ? (t << ksh) : hi;       // sample t is >= x
+    len = r - l;
+    while (len > 0) {
+        const uint64_t half = len >> 1;
+        if (key_at(sa[l + half]) < x) {
+            l += half + 1;
+            len -= half + 1;
+        } else {
+            len = half;
+        }
+    }
+    return l;
 }
 
 // Packed schedule, later rounds: only the suffixes whose group is not yet a
@@ -140,17 +235,26 @@ struct RankLookup {
     uint32_t bucketed;                     // 1: keys1 holds key1 (BucketSpec layout)
     BucketSpec bs;
     const uint32_t* __restrict__ bstart;   // bucketed: bucket start positions (2^bb + 1), or null
+    const uint32_t* __restrict__ sa;       // bucketed: the SA (key1 of the sampled-out slots)
+    uint32_t ksh;                          // bucketed: keys1 holds every 2^ksh-th key1
     __device__ __forceinline__ uint32_t sparse(uint64_t j) const {
         if ((member[j >> 5] >> (j & 31)) & 1u) return rank[j];
         uint64_t x = 0;
         uint64_t lo = 0, len = n;      // lower_bound(keys1, x), inside x's bucket when known
         if (bucketed) {
-            x = key1_at(text, code, n, bs, j);
+            const CodeMap map{code};
+            uint32_t D;
+            x = key1_words<true>(text, n, map, bs, j, &D);
             if (bstart) {
-                const uint32_t b = (uint32_t)(((x >> bs.rb) * bs.cmul) >> bs.bsh);
+                const uint32_t b = (uint32_t)(((uint64_t)D * bs.cmul) >> bs.bsh);
                 lo = bstart[b];
                 len = bstart[b + 1] - lo;
             }
+            auto key_at = [&](uint64_t p) {
+                uint32_t d;
+                return key1_words<true>(text, n, map, bs, p, &d);
+            };
+            return (uint32_t)lower_bound_sampled(keys1, ksh, sa, lo, lo + len, x, key_at) + 1u;
         } else {
             for (uint32_t t = 0; t < K; ++t) x = x * base + ((j + t < n) ? code[text[j + t]] : 0u);
         }

@@ -32,6 +32,12 @@
 // one box: 8.5 ms (class lists + per-thread re-count of the groups; 12.7 ms
 // with row-ballot segments) against 7.3 ms -- the list building and the
 // re-count cost more than the smaller networks save; kept for A/B runs.
+// the sorted key1 of every 2^kKeySample-th SA position is kept for the rank
+// look-ups of later rounds (lower_bound_sampled)
+#ifndef SA_KEY_SAMPLE
+#define SA_KEY_SAMPLE 4
+#endif
+constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
 #ifndef SA_LOCAL_SORT_CLS
 #define SA_LOCAL_SORT_CLS 0
 #endif
@@ -133,16 +139,18 @@ static uint32_t range_hb(uint32_t nb) {
     return std::max<uint32_t>(7u, w > kLoBits ? w - kLoBits : 0u);
 }
 
-// *done: the SA and keys[0] hold the sorted first round.  *fused: the
+// *done: the SA and keys[0] hold the sorted first round (keys[0]: the key1
+// of every 2^*ksh-th SA position when *fused, else every key1).  *fused: the
 // round-1 segments were produced with it (few unsorted suffixes): rank[] for
 // the unsorted set only (member bitmap), the unsorted set compacted in
 // u_pos/u_idx/u_g[0], and seg = {D, m, G}; otherwise the caller runs
 // segments() on keys[0].
 static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
                            const BucketRange& br_, hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused,
-                           uint64_t seg[3]) {
+                           uint64_t seg[3], uint32_t* ksh) {
     *done = false;
     *fused = false;
+    *ksh = 0;
     const uint64_t m = br_.m;   // suffixes of this range (= n on one GPU)
     const uint32_t blo = br_.blo, bhi = br_.bhi;
     if (bhi <= blo || bhi - blo > (1u << 18)) return set_err(SA_E_INTERNAL, "bucket range [%u, %u)", blo, bhi);
@@ -311,28 +319,32 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* const rank_arr = br_.rank ? br_.rank : c->rank;
     uint32_t* const member = br_.member ? br_.member : c->member;
     SA_HIP(hipMemsetAsync(member, 0, (n + 31) / 32 * 4, s));
-    const SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g};
-    tm.begin(SA_K_LOCAL_SORT);
-    {
+    // sorted key1 sampled (every 2^kKeySample-th SA position) for the sparse
+    // rank look-ups; a round that turns out dense re-runs the sort with every
+    // key1 below (segments() reads them all)
+    const SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g, kKeySample};
+    auto local_sort = [&](const SegOut& o) {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
 #if SA_LOCAL_SORT_CLS
         hipLaunchKernelGGL((k_bucket_sort_cls<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
-                           c->keys[0], d_sa, skew, so);
+                           c->keys[0], d_sa, skew, o);
 #else
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
-                           c->keys[0], d_sa, skew, so);
+                           c->keys[0], d_sa, skew, o);
 #endif
         // skewed windows are rare: a small grid loops over them (one
         // workgroup per listed window spent 0.1 ms on empty workgroups)
         const uint32_t gl = std::min<uint32_t>(g, 1024);
         hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(gl), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)skew, c->words, bp.ib,
-                           c->keys[0], d_sa, so);
-    }
+                           c->keys[0], d_sa, o);
+    };
+    tm.begin(SA_K_LOCAL_SORT);
+    local_sort(so);
     tm.end();
-    add_bytes(st, SA_K_LOCAL_SORT, 20 * m);
+    add_bytes(st, SA_K_LOCAL_SORT, 12 * m + (m >> kKeySample) * 8);
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
@@ -344,6 +356,20 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     seg[1] = c->host_words[1];
     seg[2] = c->host_words[2];
     add_bytes(st, SA_K_LOCAL_SORT, seg[1] * 28);   // unsorted set: rank, member bit, 3 tmp words
+    if (!br_.always_u && seg[1] > n / kSparseDiv) {
+        // dense ranks follow (segments() over every key1): the same sort
+        // again, writing every key1 and nothing of the unsorted set
+        SegOut full{};
+        full.ksh = 0;
+        SA_HIP(hipMemsetAsync(c->words + 10, 0, 4, s));   // the skewed-window list is rebuilt
+        tm.begin(SA_K_LOCAL_SORT);
+        local_sort(full);
+        tm.end();
+        add_bytes(st, SA_K_LOCAL_SORT, 20 * m);
+        SA_HIP(hipGetLastError());
+    } else {
+        *ksh = kKeySample;
+    }
     if (br_.always_u || seg[1] <= n / kSparseDiv) {
         // the unsorted set, in SA order
         tm.begin(SA_K_SEG_WRITE);
