@@ -51,6 +51,11 @@ namespace sa {
 // overlap the other's sorting (1024 x 9 ran one per CU: 11.1 -> 8.3 ms at
 // 2^30 in microbench_bucket)
 constexpr int kBsBlock = 512;
+// 1: single-bucket windows load without rebuilding key1, group counts of a
+// sorted sub-bucket from an equal-neighbour bit mask (0: the v31 code, A/B)
+#ifndef SA_LS_FAST
+#define SA_LS_FAST 1
+#endif
 #ifndef SA_BS_ITEMS
 #define SA_BS_ITEMS 18
 #endif
@@ -510,9 +515,48 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
         }
         return br.bdmin[lo];
     };
-    uint32_t v[ITEMS];
     uint64_t mx = 0;
     mn = ~0ull;
+#if SA_LS_FAST
+    if (nbk == 1) {
+        // one bucket (the common case from 2^29 suffixes): the items are
+        // (key1 - Dmin) << ib | idx already, so w = item - (min's key part
+        // << ib) -- one 64-bit subtract per suffix, min / max on the items
+        const uint32_t l0 = wave * WT + lane;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t le = l0 + i * kWave;
+            const uint64_t x = w_in[a + (le < m ? le : m - 1)];
+            w[i] = x;
+            mn = x < mn ? x : mn;
+            mx = x > mx ? x : mx;
+        }
+#pragma unroll
+        for (int o = kWave / 2; o > 0; o >>= 1) {
+            const uint64_t y0 = __shfl_xor(mn, o, kWave), y1 = __shfl_xor(mx, o, kWave);
+            mn = y0 < mn ? y0 : mn;
+            mx = y1 > mx ? y1 : mx;
+        }
+        if (lane == 0) {
+            s_red[0][wave] = mn;
+            s_red[1][wave] = mx;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int x = 0; x < WAVES; ++x) {
+            mn = s_red[0][x] < mn ? s_red[0][x] : mn;
+            mx = s_red[1][x] > mx ? s_red[1][x] : mx;
+        }
+        const uint64_t mrel = mn >> ib, span = (mx >> ib) - mrel;
+        bits = span ? 64u - (uint32_t)__clzll(span) : 0u;
+        const uint64_t base = mrel << ib;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) w[i] -= base;
+        mn = ((uint64_t)dmin0 << br.rb) + mrel;
+        return true;
+    }
+#endif
+    uint32_t v[ITEMS];
     // unpredicated loads (slots past m re-read the last suffix: no per-item
     // exec masks, which cost SGPRs and spills at 128 VGPRs); later phases
     // skip those slots by le < m
@@ -990,6 +1034,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 uint64_t x[kNet];
 #pragma unroll
                 for (int t = 0; t < kNet; ++t) x[t] = (uint32_t)t < cnt ? s_w[lo + (v[t] & 15u)] : 0ull;
+#if SA_LS_FAST
+                // bit t: slots t and t + 1 hold equal keys (one group)
+                uint32_t eqm = 0;
+#pragma unroll
+                for (int t = 0; t + 1 < kNet; ++t) eqm |= ((v[t] ^ v[t + 1]) < 16u ? 1u : 0u) << t;
+                eqm &= (1u << (cnt - 1)) - 1u;   // pairs inside the sub-bucket (1 <= cnt <= kNet)
+#pragma unroll
+                for (int t = 0; t < kNet; ++t)
+                    if ((uint32_t)t < cnt) s_w[lo + t] = x[t];
+                nh += cnt - (uint32_t)__popc(eqm);
+                nu += (uint32_t)__popc(eqm | (eqm << 1));
+                ng += (uint32_t)__popc(eqm & ~(eqm << 1));
+#else
 #pragma unroll
                 for (int t = 0; t < kNet; ++t) {
                     if ((uint32_t)t < cnt) {
@@ -1002,6 +1059,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                         ng += (!eqp && eqn) ? 1u : 0u;
                     }
                 }
+#endif
             } else {
                 for (uint32_t k = lo + 1; k < hi; ++k) {
                     const uint64_t x = s_w[k];

@@ -473,3 +473,21 @@ def test_bucketed_round1_known_answers(gpu, oracle, golden):
         got, st = build_suffix_array(t, return_stats=True)
         assert st["round1"] == "bucketed", key
         assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"], key
+
+
+def test_bucketed_round1_dense_ranks(gpu, oracle):
+    """A repeated random block: the bucketed first round leaves almost every
+    suffix unsorted, so the later rounds keep dense ranks and read every
+    sorted key1 -- the local sort runs again writing all of them (the sparse
+    path keeps only every 16th, sa_round1.h kKeySample)."""
+    from hpc_suffix_array_amd import build_suffix_array
+    block = oracle.gen_text("dna", 100_003, seed=11)
+    t = np.concatenate([np.tile(block, 20), oracle.gen_text("dna", 1001, seed=12)])
+    got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+    assert st["round1"] == "bucketed" and not st["sparse_ranks"], st
+    assert (got == oracle.sa_c(t)).all()
+    # random text of the same size: sparse ranks through the key samples
+    t = oracle.gen_text("dna", len(t), seed=13)
+    got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+    assert st["round1"] == "bucketed" and st["sparse_ranks"], st
+    assert (got == oracle.sa_c(t)).all()
