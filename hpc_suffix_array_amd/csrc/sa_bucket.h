@@ -56,6 +56,11 @@ constexpr int kBsBlock = 512;
 #ifndef SA_LS_FAST
 #define SA_LS_FAST 1
 #endif
+// 1: each thread sorts its sub-buckets largest first, 8-input networks where
+// no lane of the wave has more than 8 (A/B)
+#ifndef SA_LS_ORDER
+#define SA_LS_ORDER 1
+#endif
 #ifndef SA_BS_ITEMS
 #define SA_BS_ITEMS 18
 #endif
@@ -879,6 +884,58 @@ __device__ __forceinline__ void sort_net32(uint32_t (&v)[N]) {
 
 constexpr int kNet = 16;   // sub-buckets up to this size are sorted in registers
 
+// Sort one sub-bucket s_w[lo, lo + cnt) (cnt <= N) in registers: u32 sort
+// keys = the key bits below the sub-bucket's (exact: equal <=> same group)
+// over the slot, an N-input network, the items gathered by slot and written
+// back; the sorted keys also give the groups: unsorted members (U, groups of
+// two or more) and U groups added to nu / ng.
+template <int N>
+__device__ __forceinline__ void sort_sub(uint64_t* __restrict__ s_w, uint32_t lo, uint32_t cnt, uint32_t ib,
+                                         uint32_t low_mask, uint32_t& nu, uint32_t& ng) {
+    static_assert(N <= 16, "slot in 4 bits");
+    uint32_t v[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        v[t] = (uint32_t)t < cnt ? (((uint32_t)(s_w[lo + t] >> ib) & low_mask) << 4) | (uint32_t)t : ~0u;
+    sort_net32<N>(v);
+    uint64_t x[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) x[t] = (uint32_t)t < cnt ? s_w[lo + (v[t] & 15u)] : 0ull;
+    // bit t: slots t and t + 1 hold equal keys (one group)
+    uint32_t eqm = 0;
+#pragma unroll
+    for (int t = 0; t + 1 < N; ++t) eqm |= ((v[t] ^ v[t + 1]) < 16u ? 1u : 0u) << t;
+    eqm &= (1u << (cnt - 1)) - 1u;   // pairs inside the sub-bucket (1 <= cnt <= N)
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        if ((uint32_t)t < cnt) s_w[lo + t] = x[t];
+    nu += (uint32_t)__popc(eqm | (eqm << 1));
+    ng += (uint32_t)__popc(eqm & ~(eqm << 1));
+}
+
+// a larger sub-bucket (rare on random text): insertion sort in LDS
+__device__ __forceinline__ void sort_sub_lds(uint64_t* __restrict__ s_w, uint32_t lo, uint32_t hi, uint32_t ib,
+                                             uint32_t& nu, uint32_t& ng) {
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+        const uint64_t x = s_w[k];
+        uint32_t y = k;
+        while (y > lo && s_w[y - 1] > x) {
+            s_w[y] = s_w[y - 1];
+            --y;
+        }
+        s_w[y] = x;
+    }
+    uint64_t pr = ~0ull, cur = s_w[lo] >> ib;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint64_t nx = k + 1 < hi ? (s_w[k + 1] >> ib) : ~0ull;
+        const bool eqp = k > lo && pr == cur, eqn = k + 1 < hi && nx == cur;
+        nu += (eqp || eqn) ? 1u : 0u;
+        ng += (!eqp && eqn) ? 1u : 0u;
+        pr = cur;
+        cur = nx;
+    }
+}
+
 // kVariant (microbenchmarks only; 0 in the product): 1 skips the sort (the
 // loaded window is written back in input order); 2 accumulates per-phase
 // clock64() spans of thread 0 into words[16..23] (words must hold 24 u64)
@@ -1015,100 +1072,70 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         // insertion in LDS.  Equal keys share a sub-bucket, so the sorted
         // sub-bucket also gives the groups: heads, unsorted members (U, groups
         // of two or more) and U heads, counted per thread in SA order.
-        uint32_t nh = 0, nu = 0, ng = 0;
+        uint32_t nu = 0, ng = 0;
         const uint32_t sb0 = 2 * WPT * dg;
         const uint32_t low_bits = bits > (uint32_t)kSubBits ? bits - kSubBits : bits;
         const uint32_t low_mask = low_bits >= 32 ? ~0u : ((1u << low_bits) - 1u);
+#if SA_LS_ORDER
+        // the thread's four sub-buckets largest first: one of Poisson(~4.5)
+        // sizes in 64 lanes exceeds 8 in most waves, but the second largest
+        // of four rarely does, so iterations 2-4 mostly run the 8-input
+        // network (wave-uniform choice) instead of the 16-input one
+        static_assert(2 * WPT == 4, "four sub-buckets per thread");
+        uint32_t order = 0;
+        {
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t sb = sb0 + k;
+                o[k] = ((end_of(sb) - (sb ? end_of(sb - 1) : 0u)) << 2) | (uint32_t)k;
+            }
+            sort_net32<4>(o);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) order |= (o[3 - k] & 3u) << (2 * k);
+        }
+#pragma unroll 1
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t sb = sb0 + ((order >> (2 * i)) & 3u);
+            const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
+            const bool wide = __ballot(cnt > 8u) != 0ull;   // uniform
+            if (cnt == 0) continue;
+            if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
+        }
+#else
 #pragma unroll 1
         for (uint32_t sb = sb0; sb < sb0 + 2 * WPT; ++sb) {
             const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
             if (cnt == 0) continue;
-            if (cnt <= (uint32_t)kNet && low_bits <= 28) {
-                // u32 sort keys: the key bits below the sub-bucket's (exact:
-                // equal ⇔ same group) over the slot in the sub-bucket
-                uint32_t v[kNet];
-#pragma unroll
-                for (int t = 0; t < kNet; ++t)
-                    v[t] = (uint32_t)t < cnt ? (((uint32_t)(s_w[lo + t] >> ib) & low_mask) << 4) | (uint32_t)t : ~0u;
-                sort_net32<kNet>(v);
-                uint64_t x[kNet];
-#pragma unroll
-                for (int t = 0; t < kNet; ++t) x[t] = (uint32_t)t < cnt ? s_w[lo + (v[t] & 15u)] : 0ull;
-#if SA_LS_FAST
-                // bit t: slots t and t + 1 hold equal keys (one group)
-                uint32_t eqm = 0;
-#pragma unroll
-                for (int t = 0; t + 1 < kNet; ++t) eqm |= ((v[t] ^ v[t + 1]) < 16u ? 1u : 0u) << t;
-                eqm &= (1u << (cnt - 1)) - 1u;   // pairs inside the sub-bucket (1 <= cnt <= kNet)
-#pragma unroll
-                for (int t = 0; t < kNet; ++t)
-                    if ((uint32_t)t < cnt) s_w[lo + t] = x[t];
-                nh += cnt - (uint32_t)__popc(eqm);
-                nu += (uint32_t)__popc(eqm | (eqm << 1));
-                ng += (uint32_t)__popc(eqm & ~(eqm << 1));
-#else
-#pragma unroll
-                for (int t = 0; t < kNet; ++t) {
-                    if ((uint32_t)t < cnt) {
-                        s_w[lo + t] = x[t];
-                        const uint32_t r = v[t] >> 4;
-                        const bool eqp = t > 0 && (v[t > 0 ? t - 1 : 0] >> 4) == r;
-                        const bool eqn = (uint32_t)t + 1 < cnt && (v[t + 1 < kNet ? t + 1 : t] >> 4) == r;
-                        nh += eqp ? 0u : 1u;
-                        nu += (eqp || eqn) ? 1u : 0u;
-                        ng += (!eqp && eqn) ? 1u : 0u;
-                    }
-                }
-#endif
-            } else {
-                for (uint32_t k = lo + 1; k < hi; ++k) {
-                    const uint64_t x = s_w[k];
-                    uint32_t y = k;
-                    while (y > lo && s_w[y - 1] > x) {
-                        s_w[y] = s_w[y - 1];
-                        --y;
-                    }
-                    s_w[y] = x;
-                }
-                uint64_t pr = ~0ull, cur = s_w[lo] >> ib;
-                for (uint32_t k = lo; k < hi; ++k) {
-                    const uint64_t nx = k + 1 < hi ? (s_w[k + 1] >> ib) : ~0ull;
-                    const bool eqp = k > lo && pr == cur, eqn = k + 1 < hi && nx == cur;
-                    nh += eqp ? 0u : 1u;
-                    nu += (eqp || eqn) ? 1u : 0u;
-                    ng += (!eqp && eqn) ? 1u : 0u;
-                    pr = cur;
-                    cur = nx;
-                }
-            }
+            if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
         }
+#endif
         stamp(4);
         // exclusive U / U-group offsets of this thread's sub-buckets in the
         // window, and the window totals
         uint32_t bu, bg, th_w, tu_w, tg_w;
         {
-            const uint32_t iu = wave_inclusive_sum(nu), ig = wave_inclusive_sum(ng), ih = wave_inclusive_sum(nh);
+            // nu, ng < 2^16 (a window holds <= kBsCap suffixes): one scan of
+            // both; heads = singletons + U groups = m - U + G
+            const uint32_t iug = wave_inclusive_sum(nu | (ng << 16));
             __syncthreads();   // s_red / s_tmp reads of the scan above are done
-            if (lane == kWave - 1) {
-                s_tmp[wave] = iu;
-                s_red[0][wave] = (uint64_t)ig | ((uint64_t)ih << 32);
-            }
+            if (lane == kWave - 1) s_tmp[wave] = iug;
             __syncthreads();
-            uint32_t ou = 0, og = 0;
-            th_w = tu_w = tg_w = 0;
+            uint32_t oug = 0, tug = 0;
 #pragma unroll
             for (int x = 0; x < WAVES; ++x) {
-                const uint32_t xu = s_tmp[x], xg = (uint32_t)s_red[0][x], xh = (uint32_t)(s_red[0][x] >> 32);
-                if (x < (int)wave) {
-                    ou += xu;
-                    og += xg;
-                }
-                tu_w += xu;
-                tg_w += xg;
-                th_w += xh;
+                const uint32_t xug = s_tmp[x];
+                oug += (x < (int)wave) ? xug : 0u;
+                tug += xug;
             }
-            bu = ou + iu - nu;
-            bg = og + ig - ng;
+            tu_w = tug & 0xFFFFu;
+            tg_w = tug >> 16;
+            th_w = m - tu_w + tg_w;
+            bu = (oug & 0xFFFFu) + (iug & 0xFFFFu) - nu;
+            bg = (oug >> 16) + (iug >> 16) - ng;
         }
         if (so.rank) {
             if (threadIdx.x == 0) {
