@@ -55,11 +55,13 @@ ALPHABETS = {
 
 # bench kernel kind -> the HIP kernel it times (sa_build.hip Timer kinds)
 KERNEL_NAMES = {
-    "scatter_keys": "k_split<SrcBucketKeys,1024x12> (second bucket pass: persistent single-pass scatter, stable, "
-                    "look-back) | k_onesweep<SrcKeys,1024,4> (LSD first round)",
+    "scatter_keys": "k_split_seg<SrcBucketKeys,9,10> (second bucket pass: units cut at the first pass's digit "
+                    "segments, places by per-(low, high digit) cursors, no look-back) | k_onesweep<SrcKeys,1024,4> "
+                    "(LSD first round)",
     "scatter_first": "k_split_text<12> (first bucket pass: key1 from the text, scatter by atomic cursors) | "
                      "k_onesweep<SrcKeysIota,1024,4> (LSD first round)",
-    "local_sort": "k_bucket_sort<512,18> (per-window LDS sort: counting scatter + register sorting networks)",
+    "local_sort": "k_bucket_sort<512,18> (per-window LDS sort: counting scatter + register sorting networks, "
+                  "largest sub-bucket first; SA + every 16th key1 written)",
     "pack": "k_bucket_hist (first-pass digit totals) | k_pack_text (LSD first round keys)",
     "seg_count": "k_seg_count", "seg_write": "k_seg_write | k_wscan_* + k_u_gather",
     "sort_u": "unsorted-set sorts (k_materialize + k_onesweep<SrcKeys>)",

@@ -1073,6 +1073,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         // sub-bucket also gives the groups: heads, unsorted members (U, groups
         // of two or more) and U heads, counted per thread in SA order.
         uint32_t nu = 0, ng = 0;
+        uint32_t umask = 0;   // bit k: sub-bucket sb0 + k holds a group
         const uint32_t sb0 = 2 * WPT * dg;
         const uint32_t low_bits = bits > (uint32_t)kSubBits ? bits - kSubBits : bits;
         const uint32_t low_mask = low_bits >= 32 ? ~0u : ((1u << low_bits) - 1u);
@@ -1100,17 +1101,21 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
             const bool wide = __ballot(cnt > 8u) != 0ull;   // uniform
             if (cnt == 0) continue;
+            const uint32_t nu0 = nu;
             if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
+            if (nu != nu0) umask |= 1u << (sb - sb0);
         }
 #else
 #pragma unroll 1
         for (uint32_t sb = sb0; sb < sb0 + 2 * WPT; ++sb) {
             const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
             if (cnt == 0) continue;
+            const uint32_t nu0 = nu;
             if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
+            if (nu != nu0) umask |= 1u << (sb - sb0);
         }
 #endif
         stamp(4);
@@ -1148,27 +1153,31 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // the unsorted members of this thread's sub-buckets (rare): rank =
             // group head position + 1, member bit, (p, x, U group) at their
             // window-local U index
-            if (nu) {
+            if (umask) {   // only the sub-buckets holding groups (never straddled)
                 const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
-                const uint32_t lo0 = sb0 ? end_of(sb0 - 1) : 0u, hi0 = end_of(sb0 + 2 * WPT - 1);
-                uint32_t head = lo0, ku = bu, kg = bg;
-                uint64_t pr = ~0ull;
-                for (uint32_t k = lo0; k < hi0; ++k) {
-                    const uint64_t x = s_w[k], r = x >> ib;
-                    const uint64_t nx = k + 1 < hi0 ? (s_w[k + 1] >> ib) : ~0ull;
-                    const bool eqp = k > lo0 && pr == r, eqn = k + 1 < hi0 && nx == r;
-                    if (!eqp) head = k;
-                    if (!eqp && eqn) ++kg;
-                    if (eqp || eqn) {
-                        const uint32_t xi = (uint32_t)(x & imask);
-                        so.rank[xi] = (uint32_t)(so.rank_off + a + head + 1u);
-                        atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
-                        so.tmp_pos[a + ku] = (uint32_t)(a + k);
-                        so.tmp_idx[a + ku] = xi;
-                        so.tmp_g[a + ku] = kg - 1u;
-                        ++ku;
+                uint32_t ku = bu, kg = bg;
+                for (uint32_t um = umask; um; um &= um - 1u) {
+                    const uint32_t sb = sb0 + (uint32_t)__builtin_ctz(um);
+                    const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
+                    uint32_t head = lo;
+                    uint64_t pr = ~0ull;
+                    for (uint32_t k = lo; k < hi; ++k) {
+                        const uint64_t x = s_w[k], r = x >> ib;
+                        const uint64_t nx = k + 1 < hi ? (s_w[k + 1] >> ib) : ~0ull;
+                        const bool eqp = k > lo && pr == r, eqn = k + 1 < hi && nx == r;
+                        if (!eqp) head = k;
+                        if (!eqp && eqn) ++kg;
+                        if (eqp || eqn) {
+                            const uint32_t xi = (uint32_t)(x & imask);
+                            so.rank[xi] = (uint32_t)(so.rank_off + a + head + 1u);
+                            atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
+                            so.tmp_pos[a + ku] = (uint32_t)(a + k);
+                            so.tmp_idx[a + ku] = xi;
+                            so.tmp_g[a + ku] = kg - 1u;
+                            ++ku;
+                        }
+                        pr = r;
                     }
-                    pr = r;
                 }
             }
         }
