@@ -23,6 +23,19 @@
 #include "sa_bucket.h"
 #include "sa_onesweep.h"
 
+// When the bucket passes take the next tile's ticket (A/B at 2^30 DNA):
+// pass 1 (SA_EARLY_TICKET1) 0 = after the claims, 1 = after the digit
+// staging with the next tile's text loads right behind it (5.34 -> 5.71 ms:
+// slower), 2 = the ticket there, the loads after the claims; pass 2
+// (SA_EARLY_TICKET2) 0 = after the claims, 1 = at the start of the unit
+// (5.885 -> 5.83 ms)
+#ifndef SA_EARLY_TICKET1
+#define SA_EARLY_TICKET1 2
+#endif
+#ifndef SA_EARLY_TICKET2
+#define SA_EARLY_TICKET2 1
+#endif
+
 namespace sa {
 
 constexpr int kSpBlock = 1024;
@@ -378,7 +391,16 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 s_dcw[w] = o;
             }
         }
+#if SA_EARLY_TICKET1
+        // the next tile's ticket now: its round trip overlaps this tile's key
+        // computation (no look-back depends on the ticket order)
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+#endif
         __syncthreads();
+#if SA_EARLY_TICKET1 == 1
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        load(tn < tiles ? tn : tiles - 1);
+#endif
         // key1 of positions tb + ITEMS dg + j (D < 64 sigma 2^bb <= 2^32 rolls
         // in 32 bits; the remainder in 64)
         uint64_t k[ITEMS];
@@ -456,11 +478,17 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
             if (dg == (uint32_t)RADIX - 1) s_kept = off + inc;   // pairs kept in this tile
         }
-        // the next tile's ticket and text loads (see k_split)
+#if SA_EARLY_TICKET1 == 1
+        __syncthreads();
+#else
+        // the next tile's ticket (unless taken already) and text loads
+#if SA_EARLY_TICKET1 == 0
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+#endif
         __syncthreads();
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         load(tn < tiles ? tn : tiles - 1);
+#endif
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
@@ -477,7 +505,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t q = j * BLOCK + dg;
             if (q < kept) {
                 const uint64_t key = s_keys[q];
-                const uint32_t dd = ((uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh) - blo) & (RADIX - 1);
+                // POW2: the bucket is a bit field of key1 (no 64-bit multiply)
+                const uint32_t bq = POW2 ? (uint32_t)(key >> (b.rb + (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb))
+                                         : (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh);
+                const uint32_t dd = (bq - blo) & (RADIX - 1);
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
                 if (g < m) {
                     out_keys[g] = key;
@@ -729,6 +760,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     }
     uint32_t par = 0;
     while (u < units) {
+#if SA_EARLY_TICKET2
+        // the next unit's ticket: its round trip overlaps the ranking and
+        // claims (read after the claims' barrier)
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+#endif
         // ranks within the unit (any order: one segment, one value of l)
         uint32_t dr[ITEMS];
 #pragma unroll
@@ -794,7 +830,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
         }
         // the next unit's ticket and loads (see k_split)
+#if !SA_EARLY_TICKET2
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+#endif
         __syncthreads();
         const uint32_t un = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         uint32_t ln = l, validn = valid;
