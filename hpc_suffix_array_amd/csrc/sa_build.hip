@@ -198,6 +198,8 @@ static int ensure_capacity(sa_context* c, uint64_t n) {
                        (double)ws_bytes(n) / (1ull << 30));
     }
     c->cap = n;
+    SA_TRACE("workspace: rank %p keys0 %p keys1 %p vals_alt %p", (void*)c->rank, (void*)c->keys[0], (void*)c->keys[1],
+             (void*)c->vals_alt);
     return SA_OK;
 }
 
@@ -217,6 +219,7 @@ static int ensure_u_capacity(sa_context* c, uint64_t n) {
         return set_err(SA_E_NOMEM, "device allocation of the unsorted-set buffers failed");
     }
     c->ucap = n;
+    SA_TRACE("unsorted-set buffers: vals_u %p keys_u %p", (void*)c->vals_u, (void*)c->keys_u);
     return SA_OK;
 }
 
