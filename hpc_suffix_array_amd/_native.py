@@ -71,6 +71,7 @@ class SaStats(ctypes.Structure):
         ("kern_ms", ctypes.c_double * SA_K_COUNT),
         ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
         ("kern_bytes", ctypes.c_uint64 * SA_K_COUNT),
+        ("round1_segments", ctypes.c_int32),
     ]
 
     def to_dict(self) -> dict:
@@ -91,6 +92,7 @@ class SaStats(ctypes.Structure):
             "sparse_ranks": bool(self.sparse_ranks),
             "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed"}.get(self.round1, "lsd"),
             "largest_window": self.largest_window,
+            "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow"}.get(self.round1_segments, "exact"),
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

@@ -445,6 +445,78 @@ __global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restri
 }
 
 // ---------------------------------------------------------------------------
+// Padded first-pass segments (one GPU, 2^26 <= n <= 2^31): instead of the
+// exact digit totals of k_bucket_hist (one more read of the text, 0.48 ms at
+// 2^30), the low-digit totals are estimated from one position per 2^ssh
+// (pseudo-random inside each block, so a periodic text cannot alias the
+// stride) and each digit's segment of the first pass's output gets the
+// Poisson upper bound S (k + 4 sqrt k + 16) (1 + 1/32) slots.  The first
+// pass claims within its segment and flags a claim past the segment's end
+// (words[11]); the host then runs the round again with the exact totals.
+// The second pass reads segment l as [start(l), start(l) + count(l)).
+// ---------------------------------------------------------------------------
+template <bool POW2>
+__global__ __launch_bounds__(kBlock) void k_bucket_sample(const uint8_t* __restrict__ text, uint64_t n,
+                                                          const uint16_t* __restrict__ code, BucketSpec b,
+                                                          uint32_t ssh, uint32_t* __restrict__ ghist) {
+    __shared__ uint8_t s_map[256];
+    __shared__ uint32_t s_h[kLoRadix];
+    {
+        const uint32_t cv = code[threadIdx.x];
+        s_map[threadIdx.x] = (uint8_t)(cv ? cv - 1u : 0u);
+    }
+    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+    const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(b.sigma) : 0u;
+    const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;
+    const uint64_t ns = n >> ssh;   // whole blocks only
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < ns; i += (uint64_t)gridDim.x * kBlock) {
+        uint32_t hsh = (uint32_t)i * 0x9E3779B1u;
+        hsh ^= hsh >> 15;
+        hsh *= 0x85EBCA6Bu;
+        hsh ^= hsh >> 13;
+        const uint64_t p = (i << ssh) + (hsh >> (32 - ssh));
+        uint32_t D = 0;
+        for (uint32_t q = 0; q < b.s; ++q) {
+            const uint32_t c = p + q < n ? (uint32_t)s_map[text[p + q]] : 0u;
+            D = POW2 ? ((D << lg) | c) : D * b.sigma + c;
+        }
+        const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
+        atomicAdd(&s_h[bk & (kLoRadix - 1)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kLoRadix; i += kBlock)
+        if (s_h[i]) atomicAdd(&ghist[i], s_h[i]);
+}
+
+// sample counts -> padded segment starts pstart[0 .. kLoRadix] (one workgroup)
+// (a total above `limit`, the buffers' capacity -- not expected: the bound
+// sums to < 1.1 n -- gives every segment 0 slots: the first pass overflows
+// and the round re-runs with the exact totals)
+__global__ __launch_bounds__(kLoRadix) void k_pad_starts(const uint32_t* __restrict__ samples, uint32_t ssh,
+                                                         uint32_t slack_off, uint32_t limit,
+                                                         uint32_t* __restrict__ pstart) {
+    __shared__ uint32_t s_tmp[kLoRadix / kWave];
+    const uint32_t k = samples[threadIdx.x];
+    const float bound = slack_off ? (float)k : (float)k + 4.0f * sqrtf((float)k) + 16.0f;
+    uint64_t cap = (uint64_t)bound << ssh;
+    cap = slack_off ? cap : cap + (cap >> 5);
+    cap = (cap + 63) & ~63ull;
+    const uint32_t c32 = (uint32_t)cap;   // host: n <= 2^31, total < 2^32
+    const uint32_t inc = wave_inclusive_sum(c32);
+    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+    __syncthreads();
+    if (threadIdx.x == kLoRadix - 1) s_tmp[0] = off + inc;
+    __syncthreads();
+    const bool fits = s_tmp[0] <= limit;
+    pstart[threadIdx.x] = fits ? off + inc - c32 : 0u;
+    if (threadIdx.x == kLoRadix - 1) pstart[kLoRadix] = fits ? off + inc : 0u;
+}
+
+// ---------------------------------------------------------------------------
 // Local sort of each listed window [ws[j], ws[j+1]) (whole buckets, at most
 // CAP suffixes).  w = (key1 - min) << ib | idx (ib = bit width of n - 1) is
 // unique per suffix, so no step has to be stable:

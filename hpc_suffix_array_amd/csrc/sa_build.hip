@@ -111,6 +111,7 @@ namespace sa { struct DistState; }
 struct sa_context {
     int device = 0;
     uint64_t cap = 0;      // rank / keys / vals_alt capacity (symbols)
+    uint64_t cap_pad = 0;  // keys[0] / vals_alt capacity in elements (>= cap; padded first-pass segments)
     uint64_t ucap = 0;     // unsorted-set buffers capacity
     uint32_t* rank = nullptr;
     uint64_t* keys[2] = {nullptr, nullptr};
@@ -142,11 +143,23 @@ struct sa_context {
 
 namespace sa {
 
+// keys[0] / vals_alt elements for the padded first-pass segments of the
+// bucketed round (sa_round1.h kPadMinN..kPadMaxN; their bound sums to < 1.1 n)
+static uint64_t pad_capacity(uint64_t n) { return n + n / 8 + (1ull << 22); }
+
+// keys[0] / vals_alt capacity (elements) of a context for n symbols
+static uint64_t pad_elems(uint64_t n) {
+    const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
+    return (n >= (1ull << 26) && n <= (1ull << 31)) ? align_up(pad_capacity(n), 64) : m;
+}
+
 // Device memory a context holds for n symbols: rank + 2 key + 1 index buffer
-// (the reference schedule), plus 7 u32 arrays for the unsorted set (packed).
+// (the reference schedule; keys[0] and the index buffer padded, pad_elems),
+// plus 7 u32 arrays for the unsorted set (packed).
 static uint64_t ws_bytes(uint64_t n) {
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
-    return m * 4 + 2 * m * 8 + m * 4 + 7 * m * 4 + m * 8 + m / 8 + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
+    return m * 4 + 2 * m * 8 + m * 4 + (pad_elems(n) - m) * 12 + 7 * m * 4 + m * 8 + m / 8 +
+           (uint64_t)kRadix * kMaxChunks * 4 + 8192;
 }
 
 // tile states for the widest digit (the bucketed first round's high pass
@@ -165,6 +178,7 @@ static void free_ctx_buffers(sa_context* c) {
     c->vals_alt = nullptr;
     c->states = nullptr;
     c->cap = 0;
+    c->cap_pad = 0;
 }
 
 static void free_u_buffers(sa_context* c) {
@@ -188,8 +202,11 @@ static int ensure_capacity(sa_context* c, uint64_t n) {
     SA_HIP(hipSetDevice(c->device));
     free_ctx_buffers(c);
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
-    if (hipMalloc(&c->rank, m * 4) != hipSuccess || hipMalloc(&c->keys[0], m * 8) != hipSuccess ||
-        hipMalloc(&c->keys[1], m * 8) != hipSuccess || hipMalloc(&c->vals_alt, m * 4) != hipSuccess ||
+    // padded segments from 2^26 up to 2^31 suffixes (the bucketed round's
+    // one-GPU maximum)
+    const uint64_t mp = pad_elems(n);
+    if (hipMalloc(&c->rank, m * 4) != hipSuccess || hipMalloc(&c->keys[0], mp * 8) != hipSuccess ||
+        hipMalloc(&c->keys[1], m * 8) != hipSuccess || hipMalloc(&c->vals_alt, mp * 4) != hipSuccess ||
         hipMalloc(&c->states, tile_states_bytes(n)) != hipSuccess ||
         hipMemset(c->states, 0, tile_states_bytes(n)) != hipSuccess) {
         free_ctx_buffers(c);
@@ -198,6 +215,7 @@ static int ensure_capacity(sa_context* c, uint64_t n) {
                        (double)ws_bytes(n) / (1ull << 30));
     }
     c->cap = n;
+    c->cap_pad = mp;
     SA_TRACE("workspace: rank %p keys0 %p keys1 %p vals_alt %p", (void*)c->rank, (void*)c->keys[0], (void*)c->keys[1],
              (void*)c->vals_alt);
     return SA_OK;

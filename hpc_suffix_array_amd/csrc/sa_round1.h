@@ -38,6 +38,13 @@
 #define SA_KEY_SAMPLE 4
 #endif
 constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
+// padded first-pass segments (k_bucket_sample) from 2^26 suffixes up to the
+// bucketed round's one-GPU maximum; their starts live in the onesweep base
+// scratch after the second pass's 2^hb (<= 1024) digit bases
+constexpr uint64_t kPadMinN = 1ull << 26;
+constexpr uint64_t kPadMaxN = 1ull << 31;
+constexpr uint32_t kPadStartOff = kLoRadix + 1024;                 // kLoRadix + 1 words
+constexpr uint32_t kPadDenseOff = kPadStartOff + kLoRadix + 64;    // kLoRadix words
 #ifndef SA_LOCAL_SORT_CLS
 #define SA_LOCAL_SORT_CLS 0
 #endif
@@ -147,7 +154,7 @@ static uint32_t range_hb(uint32_t nb) {
 // segments() on keys[0].
 static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
                            const BucketRange& br_, hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused,
-                           uint64_t seg[3], uint32_t* ksh) {
+                           uint64_t seg[3], uint32_t* ksh, bool allow_pad = true) {
     *done = false;
     *fused = false;
     *ksh = 0;
@@ -159,7 +166,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // [0..2] D, m, G of the fused segments, [5] largest window, [6] local-sort
     // flags, [7] windows, [10] skewed windows
     SA_HIP(hipMemsetAsync(c->words, 0, 12, s));
-    SA_HIP(hipMemsetAsync(c->words + 5, 0, 24, s));
+    SA_HIP(hipMemsetAsync(c->words + 5, 0, 28, s));   // [5, 11]
     // digit totals of both bucket passes (one read of the text)
     // a rank's range of a multi-GPU build holding at most ~a quarter of the
     // text: the histogram pass counts the range's suffixes per workgroup, a
@@ -171,8 +178,30 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const bool listed = m * 10 <= n * 3;   // G >= 4: every rank's ~n/G (balanced cuts are within a few %)
     uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
     uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
+    // one GPU, the whole bucket range: padded first-pass segments sized from a
+    // sample instead of the exact totals (k_bucket_sample, sa_bucket.h)
+    const bool padded = allow_pad && !listed && blo == 0 && bhi == (1u << bp.bs.bb) && n >= kPadMinN &&
+                        n <= kPadMaxN && c->cap_pad >= pad_capacity(n) && !std::getenv("SA_NO_PAD");
+    const uint32_t ssh = std::max<uint32_t>(6u, bit_width(n) > 21 ? bit_width(n) - 21 : 0u);
+    uint32_t* const pstart = os_base(c) + kPadStartOff;   // kLoRadix + 1 padded segment starts
+    uint32_t* const dlo = os_base(c) + kPadDenseOff;      // kLoRadix dense segment starts
+    if (st) st->round1_segments = padded ? 1 : 0;
     tm.begin(SA_K_PACK);
-    {
+    if (padded) {
+        const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(((n >> ssh) + kBlock - 1) / kBlock,
+                                                                               4u * (uint32_t)c->cus));
+        if (pow2)
+            hipLaunchKernelGGL(k_bucket_sample<true>, dim3(g), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, bp.bs, ssh, os_ghist(c));
+        else
+            hipLaunchKernelGGL(k_bucket_sample<false>, dim3(g), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, bp.bs, ssh, os_ghist(c));
+        // SA_PAD_TEST_OVERFLOW (tests): segments of exactly the sampled
+        // estimate, so the first pass overflows and the round re-runs exactly
+        hipLaunchKernelGGL(k_pad_starts, dim3(1), dim3(kLoRadix), 0, s, (const uint32_t*)os_ghist(c), ssh,
+                           std::getenv("SA_PAD_TEST_OVERFLOW") ? 1u : 0u, (uint32_t)c->cap_pad, pstart);
+    } else {
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
@@ -193,7 +222,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_HIST
     }
     tm.end();
-    add_bytes(st, SA_K_PACK, n + (listed ? 12 * m : 0));
+    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? 12 * m : 0));
     // second-pass digit bits (7..10): bb - kLoBits on one GPU
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
@@ -204,9 +233,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* const g_lo = os_ghist(c);
     uint32_t* const g_hi = os_ghist(c) + kLoRadix;
     uint32_t* const cursor = os_ghist(c) + 5 * kRadix;
-    tm.begin(SA_K_SCAN);
-    hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_lo, kLoRadix, os_base(c));
-    tm.end();
+    if (!padded) {
+        tm.begin(SA_K_SCAN);
+        hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_lo, kLoRadix, os_base(c));
+        tm.end();
+    }
     // two passes over the bucket: its low kLoBits (any order within a
     // digit), then its high hb bits, keeping the low digit's order (text
     // order -> bucket order; sa_split.h)
@@ -220,8 +251,9 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
 #define SA_TEXT_PASS(P)                                                                                       \
     hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,       \
-                       (const uint16_t*)c->code, bp.bs, (const uint32_t*)os_base(c), os_tickets(c), c->keys[0],    \
-                       c->vals_alt, g_hi, cursor, m, blo, bhi)
+                       (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
+                       os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
+                       padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr)
         if (listed) {
             constexpr int kItemsL = SA_ITEMS_B;
             const uint64_t tl = (uint64_t)kSpBlock * kItemsL;
@@ -241,6 +273,9 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
+    // padded: the dense segment starts from the first pass's final cursors
+    if (padded)
+        hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)cursor, kLoRadix, dlo);
     tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
@@ -257,7 +292,9 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
         hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, m, kLoBits, \
-                           (const uint32_t*)os_base(c), hbase, c->segw, tk, bp.ib, c->keys_u, c->words + 4);    \
+                           (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,      \
+                           c->words + 4, padded ? (const uint32_t*)cursor : nullptr,                                 \
+                           padded ? (const uint32_t*)dlo : nullptr);                                                 \
         break;
             SA_SEG_PASS(7)
             SA_SEG_PASS(8)
@@ -272,7 +309,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         uint32_t* bstart = c->segw + kBstartOff;
         uint32_t* bdmin = bstart + kBstartWords;
 #define SA_BSTARTS(R)                                                                                         \
-    hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)os_base(c), hbase,     \
+    hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)(padded ? dlo : os_base(c)), hbase, \
                        (const uint32_t*)c->segw, m, bp.bs.cmul, bp.bs.bsh, bstart, bdmin, blo)
         switch (hb) {
             case 7: SA_BSTARTS(128); break;
@@ -300,9 +337,15 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     add_bytes(st, SA_K_WINDOWS, 8 * nw);
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 32, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 48, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
+    if (padded && c->host_words[11]) {   // a digit outgrew its sampled segment: exact totals
+        SA_TRACE("  bucketed round 1: padded segment overflow, again with exact digit totals");
+        const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false);
+        if (st) st->round1_segments = 2;
+        return rc;
+    }
     if (st) st->largest_window = (int32_t)std::min<uint32_t>(c->host_words[5], INT32_MAX);
     if (c->host_words[5] > (uint32_t)kBsCap) {
         SA_TRACE("  bucketed round 1: window of %u > %d suffixes, full sort instead", c->host_words[5], kBsCap);

@@ -319,7 +319,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
                                                          uint32_t* __restrict__ out_vals,
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor,
-                                                         uint64_t m, uint32_t blo, uint32_t bhi) {
+                                                         uint64_t m, uint32_t blo, uint32_t bhi,
+                                                         const uint32_t* __restrict__ seg_end = nullptr,
+                                                         uint32_t* __restrict__ ovf = nullptr) {
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int TILE = BLOCK * ITEMS;
@@ -338,14 +340,17 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_kept;
     __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (local bucket >> kLoBits)
+    __shared__ uint32_t s_gend[RADIX]; // padded segments: the end of digit d's segment
     const uint8_t* s_dc = reinterpret_cast<const uint8_t*>(s_dcw);
     const uint32_t bspan = bhi - blo;
+    bool over = false;
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t K = b.s + b.R;
     for (uint32_t i = dg; i < 1024u; i += BLOCK) s_hhi[i] = 0;
+    if (seg_end && dg < (uint32_t)RADIX) s_gend[dg] = seg_end[dg];
     if (dg < 256u) {
         const uint32_t cv = code[dg];
         s_map[dg] = (uint8_t)(cv ? cv - 1u : 0u);
@@ -510,9 +515,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                                          : (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh);
                 const uint32_t dd = (bq - blo) & (RADIX - 1);
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                if (g < m) {
+                if (seg_end ? g < s_gend[dd] : g < m) {
                     out_keys[g] = key;
                     out_vals[g] = (uint32_t)(tb + s_idx[q]);
+                } else {
+                    over = true;
                 }
             }
         }
@@ -522,6 +529,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     }
     for (uint32_t i = dg; i < 1024u; i += BLOCK)
         if (s_hhi[i]) atomicAdd(&ghist_hi[i], s_hhi[i]);
+    if (over && ovf) atomicOr(ovf, 1u);
 }
 
 // ---------------------------------------------------------------------------
@@ -682,7 +690,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                                                         const uint32_t* __restrict__ digit_base,
                                                         uint32_t* __restrict__ segw, uint32_t* __restrict__ ticket,
                                                         uint32_t ib, uint64_t* __restrict__ out_w,
-                                                        uint32_t* __restrict__ err) {
+                                                        uint32_t* __restrict__ err,
+                                                        const uint32_t* __restrict__ seg_cnt = nullptr,
+                                                        const uint32_t* __restrict__ dense_lo = nullptr) {
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
@@ -708,8 +718,15 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint32_t mask = RADIX - 1;
+    // segment l of the input: [lo_base[l], the next segment's start) or,
+    // padded (seg_cnt), [lo_base[l], lo_base[l] + seg_cnt[l]); dense_lo: the
+    // pairs before segment l (0: every earlier segment is empty)
     auto seg_lo = [&](uint32_t l) -> uint64_t { return lo_base[l]; };
-    auto seg_hi = [&](uint32_t l) -> uint64_t { return l + 1 < kSegs ? (uint64_t)lo_base[l + 1] : n; };
+    auto seg_hi = [&](uint32_t l) -> uint64_t {
+        if (seg_cnt) return (uint64_t)lo_base[l] + seg_cnt[l];
+        return l + 1 < kSegs ? (uint64_t)lo_base[l + 1] : n;
+    };
+    const uint32_t* const dlo = dense_lo ? dense_lo : lo_base;
     auto units_of = [&](uint32_t l) -> uint32_t { return (uint32_t)((seg_hi(l) - seg_lo(l) + TILE - 1) / TILE); };
     // unit numbering: segment by segment
     {
@@ -796,7 +813,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         // published (with its ready bit) by segment l - 1's last claimer
         if (dg < (uint32_t)RADIX) {
             uint32_t bh;
-            if (seg_lo(l) == 0) {
+            if (dlo[l] == 0) {
                 bh = digit_base[dg];
             } else {
                 uint64_t w;

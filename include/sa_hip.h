@@ -98,6 +98,8 @@ typedef struct {
     double kern_ms[SA_K_COUNT];          /* profile only */
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */
     uint64_t kern_bytes[SA_K_COUNT];     /* algorithmic bytes moved per kind */
+    int32_t round1_segments;             /* bucketed round 1: 0 exact digit totals, 1 sampled padded segments,
+                                            2 padded segments overflowed and the round ran again exactly */
 } sa_stats;
 
 typedef struct sa_context sa_context;

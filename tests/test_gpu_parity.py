@@ -491,3 +491,45 @@ def test_bucketed_round1_dense_ranks(gpu, oracle):
     got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
     assert st["round1"] == "bucketed" and st["sparse_ranks"], st
     assert (got == oracle.sa_c(t)).all()
+
+
+@pytest.mark.parametrize("mode", ["padded", "overflow", "exact"])
+def test_round1_padded_segments(gpu, oracle, golden, mode, monkeypatch):
+    """From 2^26 suffixes the first bucket pass writes into segments sized
+    from a 1-in-2^ssh sample (k_bucket_sample, sa_bucket.h) instead of exact
+    digit totals; a segment that overflows (forced here by
+    SA_PAD_TEST_OVERFLOW: no slack) makes the round run again with the exact
+    totals; SA_NO_PAD takes the exact totals at once.  Config-2 known answer
+    (64 MiB DNA) through all three."""
+    from hpc_suffix_array_amd import build_suffix_array
+    if mode == "overflow":
+        monkeypatch.setenv("SA_PAD_TEST_OVERFLOW", "1")
+    if mode == "exact":
+        monkeypatch.setenv("SA_NO_PAD", "1")
+    k = golden["known"]["dna_64MiB"]
+    t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
+    got, st = build_suffix_array(t, return_stats=True)
+    assert st["round1"] == "bucketed"
+    assert st["round1_segments"] == {"padded": "padded", "overflow": "padded-overflow", "exact": "exact"}[mode], st
+    assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
+
+
+def test_round1_padded_segments_skewed(gpu, oracle):
+    """Padded segments on texts whose first-pass digits are far from uniform
+    (a biased alphabet: digit sizes ~2x apart; a long random block repeated):
+    exact SA either way
+    (an overflow falls back to the exact totals)."""
+    from hpc_suffix_array_amd import build_suffix_array, check_suffix_array
+    n = (1 << 26) + 12345
+    rng = np.random.default_rng(5)
+    biased = rng.choice(np.frombuffer(b"ACGT", np.uint8), size=n, p=[0.3, 0.3, 0.2, 0.2])
+    got, st = build_suffix_array(biased, return_stats=True)
+    assert st["round1"] == "bucketed" and st["round1_segments"] in ("padded", "padded-overflow"), st
+    assert (got == oracle.sa_c(biased)).all()
+    # a long random block repeated (dense ranks; the oracle's 20+ rounds over
+    # 64 M suffixes would take minutes: the O(n) checker instead)
+    block = oracle.gen_text("alnum", 3_000_017, seed=9)
+    rep = np.tile(block, n // len(block) + 1)[:n]
+    got, st = build_suffix_array(rep, return_stats=True)
+    assert st["round1"] == "bucketed" and st["round1_segments"] in ("padded", "padded-overflow"), st
+    assert check_suffix_array(rep, got)
