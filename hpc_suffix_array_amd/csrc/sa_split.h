@@ -29,6 +29,14 @@
 // slower), 2 = the ticket there, the loads after the claims; pass 2
 // (SA_EARLY_TICKET2) 0 = after the claims, 1 = at the start of the unit
 // (5.885 -> 5.83 ms)
+// diagnostic: per-phase clock64 spans of k_split_seg printed by two
+// workgroups (scatter 36 %, write 22 %, base wait 18 %, ranking 12 %, claims
+// 12 % at 2^30 DNA).  Batching the per-item LDS reads of the scatter and
+// write loops (one wait instead of one per item) raised VGPR spills 4 -> 17
+// and made both passes slower (5.9 -> 7.2 ms, 5.5 -> 6.3 ms): reverted.
+#ifndef SA_SEG_PROF
+#define SA_SEG_PROF 0
+#endif
 #ifndef SA_EARLY_TICKET1
 #define SA_EARLY_TICKET1 2
 #endif
@@ -776,6 +784,18 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         load(tb, valid, k, v);
     }
     uint32_t par = 0;
+#if SA_SEG_PROF
+    // diagnostic build (-DSA_SEG_PROF=1): clock64 spans of thread 0 per phase
+    uint64_t pacc[7] = {0, 0, 0, 0, 0, 0, 0}, plast = clock64();
+#define SEG_STAMP(k)                                \
+    if (dg == 0) {                                  \
+        const uint64_t now_ = clock64();            \
+        pacc[k] += now_ - plast;                    \
+        plast = now_;                               \
+    }
+#else
+#define SEG_STAMP(k)
+#endif
     while (u < units) {
 #if SA_EARLY_TICKET2
         // the next unit's ticket: its round trip overlaps the ranking and
@@ -791,6 +811,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             dr[j] = (d << 16) | (d < (uint32_t)RADIX ? atomicAdd(&s_cnt[d], 1u) : 0u);
         }
         __syncthreads();
+        SEG_STAMP(0)
         // claim this unit's place in (l, h); count the claim for segment l
         // (the claim's return value is stored first: it has been performed)
         uint32_t tile_cnt = 0;
@@ -808,6 +829,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
         }
+        SEG_STAMP(1)
         if (dg == 0) s_last = atomicAdd(&done[l], 1u) == units_of(l) - 1 ? 1u : 0u;
         // base(h, l): digit_base when every earlier segment is empty, else
         // published (with its ready bit) by segment l - 1's last claimer
@@ -833,6 +855,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             s_dmin[dg] = bucket_dmin(((dg << kLoBits) | l) + src.bofs, src.cmul, src.bsh);
         }
         __syncthreads();
+        SEG_STAMP(2)
         if (s_last) {
             // every claim of segment l has been performed: publish base(., l')
             // for the next segment and the empty ones after it
@@ -852,6 +875,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
 #endif
         __syncthreads();
         const uint32_t un = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        SEG_STAMP(3)
         uint32_t ln = l, validn = valid;
         uint64_t tbn = tb;
         if (un < units) locate(un, ln, tbn, validn);
@@ -868,6 +892,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
         }
         __syncthreads();
+        SEG_STAMP(4)
         if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
@@ -879,6 +904,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
         }
         __syncthreads();
+        SEG_STAMP(5)
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             k[j] = kn[j];
@@ -890,6 +916,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         valid = validn;
         par ^= 1u;
     }
+#if SA_SEG_PROF
+    if (dg == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("k_split_seg wg %u clk: rank %llu claim %llu base %llu ticket+load %llu scatter %llu write %llu\n",
+               blockIdx.x, (unsigned long long)pacc[0], (unsigned long long)pacc[1], (unsigned long long)pacc[2],
+               (unsigned long long)pacc[3], (unsigned long long)pacc[4], (unsigned long long)pacc[5]);
+#endif
+#undef SEG_STAMP
 }
 
 // bucket b = (h << kLoBits) | l starts at base(h, l) in the second pass's
