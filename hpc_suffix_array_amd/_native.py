@@ -72,6 +72,7 @@ class SaStats(ctypes.Structure):
         ("kern_launches", ctypes.c_uint64 * SA_K_COUNT),
         ("kern_bytes", ctypes.c_uint64 * SA_K_COUNT),
         ("round1_segments", ctypes.c_int32),
+        ("round1_layout", ctypes.c_int32),
     ]
 
     def to_dict(self) -> dict:
@@ -93,6 +94,7 @@ class SaStats(ctypes.Structure):
             "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed"}.get(self.round1, "lsd"),
             "largest_window": self.largest_window,
             "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow"}.get(self.round1_segments, "exact"),
+            "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2)},
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

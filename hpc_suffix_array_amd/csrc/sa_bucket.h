@@ -105,9 +105,20 @@ struct SrcBucketKeys {
     uint32_t bofs;
     __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return vals[e]; }
+    static constexpr bool kPk8 = false;
     __device__ __forceinline__ uint32_t digit(uint64_t k, uint32_t shift, uint32_t mask) const {
         return ((bucket_of(k, rb, cmul, bsh) - bofs) >> shift) & mask;
     }
+};
+
+// radix source of the second bucket pass over the first pass's packed items
+// (k_split_text<.., PK8>): the digit is the item's top hb bits (shift 64 -
+// hb), and the item below them is already the bucket-relative output word
+struct SrcPk8 {
+    const uint64_t* __restrict__ items;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const { return items[e]; }
+    __device__ __forceinline__ uint32_t val(uint64_t) const { return 0u; }
+    static constexpr bool kPk8 = true;
 };
 
 // NW consecutive bytes of an LDS byte array (viewed as words) starting at
@@ -272,15 +283,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 uint64_t r = 0;
                 for (uint32_t q = 0; q < b.s; ++q) Dk = POW2 ? ((Dk << lg) | s_dc[l + q]) : Dk * sig + s_dc[l + q];
                 for (uint32_t q = b.s; q < K; ++q) r = POW2 ? ((r << lg) | s_dc[l + q]) : r * sig + s_dc[l + q];
-                const uint64_t L = n - (tb + l);
-                uint64_t low;
-                if (L >= K) {
-                    low = b.s + r * (b.R + 1) + b.R;
-                } else {
-                    const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
-                    low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
-                }
-                lkeys[run + t] = ((uint64_t)Dk << b.rb) | low;
+                lkeys[run + t] = ((uint64_t)Dk << b.rb) | bucket_low(b, r, n - (tb + l));
                 lpos[run + t] = (uint32_t)(tb + l);
             }
             run += tot;

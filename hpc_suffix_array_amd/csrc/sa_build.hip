@@ -134,7 +134,7 @@ struct sa_context {
     uint32_t* words = nullptr;     // [0..2] = D, m, G; [3] = check error flags
     uint32_t* alpha = nullptr;     // 256 byte counts
     uint16_t* code = nullptr;      // 256 byte -> dense code 1..sigma
-    uint32_t* host_words = nullptr;  // pinned (4096 words): 64 words, 256 counts, 128 words of codes at 320,
+    uint32_t* host_words = nullptr;  // pinned (4096 words): 64 words, 256 counts, 128 words of codes at 320, the text tail (64 B) at 2048,
                                      // per-rank counts of the range-partitioned build at 1024
     hipEvent_t ev[sa::kEvPool];
     int ev_ready = 0;
@@ -631,6 +631,10 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_ALPHABET, n);
     SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 8 * 4, hipMemcpyDeviceToHost, s));
+    // the text's last bytes: the compact key layout's check (short_suffix_ties)
+    const uint32_t tail_n = (uint32_t)std::min<uint64_t>(n, (uint64_t)kMaxK);
+    uint8_t* h_tail = reinterpret_cast<uint8_t*>(c->host_words + 2048);
+    SA_HIP(hipMemcpyAsync(h_tail, d_text + (n - tail_n), tail_n, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
@@ -646,7 +650,10 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // global passes + per-window LDS sort) when the text allows it, else the
     // LSD sort of the packed key
     BucketPlan bp;
-    bool bucketed = plan_bucketed(sigma, n, K, opts ? opts->round1 : SA_ROUND1_AUTO, c->radix, &bp);
+    const int r1 = opts ? opts->round1 : SA_ROUND1_AUTO;
+    bool bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, !std::getenv("SA_NO_CMP"));
+    if (bucketed && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
+        bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, false);
     bool fused = false;
     uint64_t seg1[3] = {0, 0, 0};
     if (bucketed) {

@@ -83,16 +83,34 @@ struct SrcText {
 };
 
 // Key layout of the bucketed first round (sa_bucket.h): key1 = D << rb | low
-// with D the dense s-symbol prefix and low the dense next R symbols times
-// (R + 1) plus the number of them before the end (or L - 1 for a suffix of
-// length L < s).
+// with D the dense s-symbol prefix and, for a suffix of length L >= s, low =
+// s + the dense next R symbols (0 past the end) times (R + 1) plus the number
+// of them before the end (L - 1 for a suffix of length L < s).
+// Compact variant (cmp = 1): low = 2 r + [L >= K] for every suffix (D and r
+// with digit 0 past the end) -- one bit instead of log2(R + 1) for the end
+// and no offset for the suffixes shorter than s, so low fills its rb bits
+// (the local sort's sub-buckets stay uniform).  Exact when no two of the
+// text's last K - 1 suffixes share (D, r), which the host checks on the
+// text's tail before choosing it (short_suffix_ties, sa_round1.h): a short
+// suffix then differs from every other short one in (D, r), and from the
+// longer suffixes continuing it with the smallest symbol -- equal (D, r), it
+// is their prefix -- in the bit.
 struct BucketSpec {
     uint64_t pow_s1;   // sigma^(s-1)
     uint64_t powR1;    // sigma^(R-1)
     uint64_t cmul;     // floor(2^48 / sigma^s): bucket = (D * cmul) >> bsh
     uint32_t sigma, s, R, rb;
     uint32_t bb, bsh;  // bucket bits (16..18), bsh = 48 - bb
+    uint32_t cmp;      // 1: compact low
 };
+
+// low of a suffix of length L with next-R-symbols value r (see BucketSpec)
+__host__ __device__ __forceinline__ uint64_t bucket_low(const BucketSpec& b, uint64_t r, uint64_t L) {
+    if (b.cmp) return 2 * r + (L >= b.s + b.R ? 1u : 0u);
+    if (L < b.s) return L - 1;
+    const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
+    return b.s + r * (b.R + 1) + tl;
+}
 
 // byte -> dense digit (code - 1, absent bytes 0) from the global code table
 struct CodeMap {
@@ -154,15 +172,7 @@ __device__ __forceinline__ uint64_t key1_words(const uint8_t* __restrict__ text,
     }
     *D_out = (uint32_t)D;
     if (!FULL) return 0;
-    const uint64_t L = n - j;
-    uint64_t low;
-    if (L < b.s) {
-        low = L - 1;
-    } else {
-        const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
-        low = b.s + r * (b.R + 1) + tl;
-    }
-    return (D << b.rb) | low;
+    return (D << b.rb) | bucket_low(b, r, n - j);
 }
 
 // Lower bound of x among the sorted key1 of SA positions [lo, hi) when the

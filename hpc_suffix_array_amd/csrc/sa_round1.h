@@ -27,6 +27,11 @@
 #ifndef SA_ITEMS_B
 #define SA_ITEMS_B 10
 #endif
+// pairs per lane of the second pass over packed items (SrcPk8: no spills;
+// 8 / 10 / 12: 5.50 / 5.17 / 4.90 ms at 2^30 DNA, profiles/r02_ai_ab_pk8.txt)
+#ifndef SA_ITEMS_PK
+#define SA_ITEMS_PK 12
+#endif
 // local sort: 1 = size-classed sub-bucket networks (k_bucket_sort_cls), 0 =
 // 16-input network per sub-bucket (k_bucket_sort).  Measured at 2^30 DNA on
 // one box: 8.5 ms (class lists + per-thread re-count of the groups; 12.7 ms
@@ -59,8 +64,10 @@ struct BucketPlan {
 // world: GPUs the bucket range is split over (sa_dist.h); one GPU sorts at
 // most 2^18 buckets (the second pass's 10 digit bits), a rank of a wider
 // build 2^bb / world of them.
+// cmp: the compact low of BucketSpec (only when short_suffix_ties is false
+// for the text)
 static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p,
-                          int world = 1) {
+                          int world = 1, bool cmp = false) {
     if (round1 == SA_ROUND1_LSD || radix != 0 || sigma < 2 || n < 2) return false;
     if (round1 == SA_ROUND1_AUTO && n < kBucketMinN) return false;
     // bucket bits: windows of about n / 2^bb suffixes must fit the
@@ -95,7 +102,7 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     for (uint32_t R = K - s; R >= 1; --R) {
         unsigned __int128 pr = 1;   // sigma^R
         for (uint32_t t = 0; t < R; ++t) pr *= sigma;
-        unsigned __int128 lowmax = s + (pr - 1) * (R + 1) + R;
+        unsigned __int128 lowmax = cmp ? 2 * pr - 1 : s + (pr - 1) * (R + 1) + R;
         uint32_t rb = 0;
         while (lowmax) {
             ++rb;
@@ -111,11 +118,50 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
         p->bs.s = s;
         p->bs.R = R;
         p->bs.rb = rb;
+        p->bs.cmp = cmp ? 1u : 0u;
         p->ib = ib;
         p->K = s + R;
         return true;
     }
     return false;
+}
+
+// The compact layout's precondition fails: two of the text's last K - 1
+// suffixes share (D, r) with digit 0 past the end (the text ends in a run of
+// its smallest symbol, e.g. ...AA for DNA: "A" and "AA" pad alike).  tail:
+// the text's last t = min(n, kMaxK) >= K - 1 bytes; code: dense codes.
+static bool short_suffix_ties(const uint8_t* tail, uint64_t n, uint32_t t, const uint16_t* code, uint32_t sigma,
+                              uint32_t s, uint32_t R) {
+    auto dig = [&](uint8_t x) -> uint32_t { return code[x] ? code[x] - 1u : 0u; };
+    const uint32_t K = s + R;
+    uint64_t Ds[kMaxK];
+    unsigned __int128 rs[kMaxK];
+    uint32_t cnt = 0;
+    for (uint32_t L = 1; L < K && L <= n && L <= t; ++L) {
+        const uint8_t* x = tail + (t - L);
+        uint64_t D = 0;
+        unsigned __int128 r = 0;
+        for (uint32_t q = 0; q < s; ++q) D = D * sigma + (q < L ? dig(x[q]) : 0u);
+        for (uint32_t q = s; q < K; ++q) r = r * sigma + (q < L ? dig(x[q]) : 0u);
+        for (uint32_t o = 0; o < cnt; ++o)
+            if (Ds[o] == D && rs[o] == r) return true;
+        Ds[cnt] = D;
+        rs[cnt] = r;
+        ++cnt;
+    }
+    return false;
+}
+
+// The first bucket pass may write one packed 64-bit item per suffix
+// (k_split_text<.., PK8>, SrcPk8): one GPU, the whole bucket range, a
+// power-of-two alphabet, and the second pass's digit, key1 below its bucket
+// and the index fitting 64 bits
+static bool plan_pk8(const BucketPlan& bp, uint32_t hb) {
+    const uint32_t sg = bp.bs.sigma;
+    if (sg < 2 || (sg & (sg - 1)) != 0 || std::getenv("SA_NO_PK8")) return false;
+    const uint32_t lg = (uint32_t)__builtin_ctz(sg);
+    if (lg * bp.bs.s < bp.bs.bb) return false;
+    return hb + (lg * bp.bs.s - bp.bs.bb) + bp.bs.rb + bp.ib <= 64;
 }
 
 // The buckets [blo, bhi) this build sorts (local bucket = bucket - blo): all
@@ -227,6 +273,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
     const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
+    const bool pk8 = !listed && blo == 0 && bhi == (1u << bp.bs.bb) && plan_pk8(bp, hb);
+    if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0);
     // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
     // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
     // low, [kLoRadix, +2^hb) high
@@ -249,11 +297,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const uint64_t tiles = (n + tile - 1) / tile;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
-#define SA_TEXT_PASS(P)                                                                                       \
-    hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,       \
+#define SA_TEXT_PASS(P, PK)                                                                                   \
+    hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P, PK>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,   \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
-                       padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr)
+                       padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib)
         if (listed) {
             constexpr int kItemsL = SA_ITEMS_B;
             const uint64_t tl = (uint64_t)kSpBlock * kItemsL;
@@ -261,15 +309,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
                                (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
+        } else if (pk8) {
+            SA_TEXT_PASS(true, true);
         } else if (pow2) {
-            SA_TEXT_PASS(true);
+            SA_TEXT_PASS(true, false);
         } else {
-            SA_TEXT_PASS(false);
+            SA_TEXT_PASS(false, false);
         }
 #undef SA_TEXT_PASS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, listed ? 24 * m : n + 12 * m);
+    add_bytes(st, SA_K_SCATTER_FIRST, listed ? 24 * m : n + (pk8 ? 8 : 12) * m);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
@@ -281,26 +331,31 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         // 12288-pair units cut at the first pass's digit boundaries, places
         // claimed per (low digit, high digit) by atomic cursors (sa_split.h)
-        constexpr int kItemsB = SA_ITEMS_B;
+        constexpr int kItemsB = SA_ITEMS_B, kItemsPk = SA_ITEMS_PK;
         const SrcBucketKeys sb{c->keys[0], c->vals_alt, bp.bs.rb, bp.bs.bsh, bp.bs.cmul, blo};
+        const SrcPk8 sp{c->keys[0]};
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
         SA_HIP(hipMemsetAsync(c->segw, 0, segw_words(1u << hb) * 4, s));   // <= 3 MiB
-        const uint64_t units = (m + kSpBlock * kItemsB - 1) / (kSpBlock * kItemsB) + kSegs;
+        const uint64_t ut = (uint64_t)kSpBlock * (pk8 ? kItemsPk : kItemsB);
+        const uint64_t units = (m + ut - 1) / ut + kSegs;
         const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)c->cus));
         switch (hb) {
+#define SA_SEG_LAUNCH(S, B, SRC, SH, IT)                                                                      \
+    hipLaunchKernelGGL((k_split_seg<S, B, IT>), dim3(grid), dim3(kSpBlock), 0, s, SRC, m, SH,                  \
+                       (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,          \
+                       c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr)
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
-        hipLaunchKernelGGL((k_split_seg<SrcBucketKeys, B, kItemsB>), dim3(grid), dim3(kSpBlock), 0, s, sb, m, kLoBits, \
-                           (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,      \
-                           c->words + 4, padded ? (const uint32_t*)cursor : nullptr,                                 \
-                           padded ? (const uint32_t*)dlo : nullptr);                                                 \
+        if (pk8) SA_SEG_LAUNCH(SrcPk8, B, sp, 64u - B, kItemsPk);                                             \
+        else SA_SEG_LAUNCH(SrcBucketKeys, B, sb, kLoBits, kItemsB);                                           \
         break;
             SA_SEG_PASS(7)
             SA_SEG_PASS(8)
             SA_SEG_PASS(9)
             SA_SEG_PASS(10)
 #undef SA_SEG_PASS
+#undef SA_SEG_LAUNCH
             default: return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
         }
         // bucket starts and smallest D values (the local sort rebuilds key1
@@ -320,7 +375,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_BSTARTS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_KEYS, 20 * m);
+    add_bytes(st, SA_K_SCATTER_KEYS, (pk8 ? 16 : 20) * m);
     SA_HIP(hipGetLastError());
     // windows of whole buckets; ws lives in vals_alt (free again; nw + 1 <= m)
     const uint64_t nw = (m + kWinStride - 1) / kWinStride;
@@ -431,8 +486,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         SA_HIP(hipGetLastError());
         *fused = true;
     }
-    SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R, bp.bs.rb,
-             c->host_words[7], c->host_words[10], c->host_words[5]);
+    SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u cmp=%u pk8=%d windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R,
+             bp.bs.rb, bp.bs.cmp, pk8 ? 1 : 0, c->host_words[7], c->host_words[10], c->host_words[5]);
     *done = true;
     return SA_OK;
 }

@@ -34,6 +34,12 @@
 // 12 % at 2^30 DNA).  Batching the per-item LDS reads of the scatter and
 // write loops (one wait instead of one per item) raised VGPR spills 4 -> 17
 // and made both passes slower (5.9 -> 7.2 ms, 5.5 -> 6.3 ms): reverted.
+// Letting the second pass's stores stay in flight into the next unit's
+// ranking (unconditional stores + an explicit wait after the prologue's
+// loads, so the loop-top wait counts only loads; the early ticket's atomic
+// kept off the compiler's atomic optimizer) was slower too (5.91 -> 6.0-6.3
+// ms, profiles/r02_ah_ab_seg_nodrain_reverted.txt): the pass is not waiting
+// on its store acknowledgements.
 #ifndef SA_SEG_PROF
 #define SA_SEG_PROF 0
 #endif
@@ -320,7 +326,13 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // Bucket range (range-partitioned build, sa_dist.h): only positions whose
 // bucket lies in [blo, bhi) are kept, digits of the local bucket bk - blo;
 // m = the number kept (the output's length).  One GPU: [0, 2^bb), m = n.
-template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false>
+// PK8 (POW2, one GPU, the whole bucket range): each pair leaves as ONE 64-bit
+// item -- the second pass's digit (the bucket's high hb bits) on top, then
+// key1 below its bucket (key1 - Dmin(bucket) << rb: the bits of D under the
+// bucket and low) and the position in the low ib bits, so the pass writes 8
+// bytes per suffix instead of 12 (key1 + position) and the second pass reads
+// 8 (SrcPk8).  Needs hb + (lg sigma^s - bb + rb) + ib <= 64 (plan_pk8).
+template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -329,7 +341,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor,
                                                          uint64_t m, uint32_t blo, uint32_t bhi,
                                                          const uint32_t* __restrict__ seg_end = nullptr,
-                                                         uint32_t* __restrict__ ovf = nullptr) {
+                                                         uint32_t* __restrict__ ovf = nullptr, uint32_t pk_hb = 0,
+                                                         uint32_t pk_ib = 0) {
+    static_assert(!PK8 || POW2, "packed items need a power-of-two alphabet (Dmin(bucket) by a shift)");
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int TILE = BLOCK * ITEMS;
@@ -338,7 +352,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     constexpr int WPT = (NW + BLOCK - 1) / BLOCK; // per lane
     static_assert(ITEMS % 4 == 0 && kHalo % 4 == 0 && TILE <= 65535, "word staging, 16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
-    __shared__ uint16_t s_idx[TILE];
+    __shared__ uint16_t s_idx[TILE];                    // tile offset; PK8: the pair's digit
     __shared__ uint32_t s_dcw[NW + 8];                  // dense digits, 4 per word (0 past the end; + slack)
     __shared__ uint8_t s_map[256];
     __shared__ uint32_t s_cnt[RADIX];
@@ -427,6 +441,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
             const uint64_t rmask = POW2 ? ((1ull << (lg * b.R)) - 1ull) : 0ull;
             const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;   // bucket = D >> (lg s - bb)
+            // interior low = r mulR + addR (BucketSpec: compact or not)
+            const uint64_t mulR = b.cmp ? 2u : b.R + 1u, addR = b.cmp ? 1u : b.s + b.R;
             if constexpr (POW2) {
                 for (uint32_t q = 0; q < b.s; ++q) D = (D << lg) | s_dc[l0 + q];
                 for (uint32_t q = 0; q < b.R; ++q) r = (r << lg) | s_dc[l0 + b.s + q];
@@ -453,14 +469,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                         r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
                     }
                 }
-                uint64_t low;
-                if (interior) {
-                    low = b.s + r * (b.R + 1) + b.R;
-                } else {
-                    const uint64_t L = n - (tb + l0 + j);   // wraps past the end: never ranked
-                    const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;
-                    low = L < b.s ? L - 1 : b.s + r * (b.R + 1) + tl;
-                }
+                // (past the end L wraps: never ranked)
+                const uint64_t low = interior ? r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 const uint32_t lb = bk - blo;
@@ -502,13 +512,26 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         load(tn < tiles ? tn : tiles - 1);
 #endif
+        // PK8: the item is built here, not in the key loop (its extra live
+        // values there spilled 19 VGPRs): the second pass's digit (the
+        // bucket's high bits; one GPU: local = global bucket), key1 below its
+        // bucket, the position
+        const uint32_t kbsh = b.rb + (PK8 ? (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb : 0u);
+        const uint64_t remmask = PK8 ? (1ull << kbsh) - 1ull : 0ull;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                s_keys[pos] = k[j];
-                s_idx[pos] = (uint16_t)(ITEMS * dg + j);
+                if constexpr (PK8) {
+                    const uint32_t hi = (uint32_t)(k[j] >> kbsh) >> kLoBits;
+                    s_keys[pos] = ((uint64_t)hi << (64u - pk_hb)) | ((k[j] & remmask) << pk_ib) |
+                                  (tb + ITEMS * dg + j);
+                    s_idx[pos] = (uint16_t)d;
+                } else {
+                    s_keys[pos] = k[j];
+                    s_idx[pos] = (uint16_t)(ITEMS * dg + j);
+                }
             }
         }
         __syncthreads();
@@ -518,14 +541,19 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t q = j * BLOCK + dg;
             if (q < kept) {
                 const uint64_t key = s_keys[q];
-                // POW2: the bucket is a bit field of key1 (no 64-bit multiply)
-                const uint32_t bq = POW2 ? (uint32_t)(key >> (b.rb + (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb))
-                                         : (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh);
-                const uint32_t dd = (bq - blo) & (RADIX - 1);
+                uint32_t dd;
+                if constexpr (PK8) {
+                    dd = s_idx[q];
+                } else {
+                    // POW2: the bucket is a bit field of key1 (no 64-bit multiply)
+                    const uint32_t bq = POW2 ? (uint32_t)(key >> (b.rb + (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb))
+                                             : (uint32_t)(((key >> b.rb) * b.cmul) >> b.bsh);
+                    dd = (bq - blo) & (RADIX - 1);
+                }
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
                 if (seg_end ? g < s_gend[dd] : g < m) {
                     out_keys[g] = key;
-                    out_vals[g] = (uint32_t)(tb + s_idx[q]);
+                    if constexpr (!PK8) out_vals[g] = (uint32_t)(tb + s_idx[q]);
                 } else {
                     over = true;
                 }
@@ -773,7 +801,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             const uint32_t le = wave * WTILE + j * kWave + lane;
             const uint64_t e = tb + (le < last ? le : last);
             kk[j] = src.key(e);
-            vv[j] = src.val(e);
+            vv[j] = Src::kPk8 ? 0u : src.val(e);
         }
     };
     uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
@@ -852,7 +880,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             }
             s_gofs[dg] = bh + s_claim[dg];
             s_claim[dg] = bh;
-            s_dmin[dg] = bucket_dmin(((dg << kLoBits) | l) + src.bofs, src.cmul, src.bsh);
+            if constexpr (!Src::kPk8) s_dmin[dg] = bucket_dmin(((dg << kLoBits) | l) + src.bofs, src.cmul, src.bsh);
         }
         __syncthreads();
         SEG_STAMP(2)
@@ -887,7 +915,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                s_keys[pos] = ((k[j] - ((uint64_t)s_dmin[d] << src.rb)) << ib) | v[j];
+                if constexpr (Src::kPk8)   // the item below its digit (shift = 64 - hb)
+                    s_keys[pos] = k[j] & ((1ull << shift) - 1ull);
+                else
+                    s_keys[pos] = ((k[j] - ((uint64_t)s_dmin[d] << src.rb)) << ib) | v[j];
                 s_dig[pos] = (uint16_t)d;
             }
         }

@@ -533,3 +533,49 @@ def test_round1_padded_segments_skewed(gpu, oracle):
     got, st = build_suffix_array(rep, return_stats=True)
     assert st["round1"] == "bucketed" and st["round1_segments"] in ("padded", "padded-overflow"), st
     assert check_suffix_array(rep, got)
+
+
+@pytest.mark.parametrize("layout", ["default", "no_pk8", "no_cmp"])
+def test_round1_layouts(gpu, oracle, golden, layout, monkeypatch):
+    """Key layouts of the bucketed first round (sa_kernels.h BucketSpec,
+    sa_split.h k_split_text<.., PK8>): the compact low (cmp) with packed
+    8-byte first-pass items (pk8, power-of-two alphabets with the bits to
+    spare), the compact low alone, and the original layout -- same SA."""
+    from hpc_suffix_array_amd import build_suffix_array
+    if layout == "no_pk8":
+        monkeypatch.setenv("SA_NO_PK8", "1")
+    if layout == "no_cmp":
+        monkeypatch.setenv("SA_NO_CMP", "1")
+    for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21), ("alnum", 1_500_007), ("binary", 1 << 20)):
+        t = oracle.gen_text(kind, n, seed=n + 1)
+        t[-1] = t.max()   # no tail run of the smallest symbol (test_compact_layout_text_tails)
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        assert st["round1"] == "bucketed", (kind, st)
+        lay = st["round1_layout"]
+        assert lay["compact"] == (layout != "no_cmp"), (kind, lay)
+        if layout == "no_pk8" or kind == "alnum":   # alnum: sigma 62, not a power of two
+            assert not lay["pk8"], (kind, lay)
+        assert (got == oracle.sa_c(t)).all(), (kind, layout)
+    if layout == "default":   # config 2 through the packed items (1 GiB: the bench)
+        k = golden["known"]["dna_64MiB"]
+        t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
+        got, st = build_suffix_array(t, return_stats=True)
+        assert st["round1_layout"] == {"compact": True, "pk8": True}, st["round1_layout"]
+        assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
+
+
+@pytest.mark.parametrize("tail", [b"A" * 40, b"CAA", b"ACGTACGTTTGCA" * 3, b"T" * 40, b"GATTACA"])
+def test_compact_layout_text_tails(gpu, oracle, tail):
+    """The compact key1 low is exact only when no two of the text's last
+    K - 1 suffixes share (D, r) (sa_round1.h short_suffix_ties): a text
+    ending in a run of its smallest symbol breaks that and takes the original
+    layout;
+    other tails keep the compact one.  Same SA as the oracle either way."""
+    from hpc_suffix_array_amd import build_suffix_array
+    n = 1 << 21
+    t = np.concatenate([oracle.gen_text("dna", n - len(tail), seed=len(tail)), np.frombuffer(tail, np.uint8)])
+    got, st = build_suffix_array(t, return_stats=True)
+    assert st["round1"] == "bucketed"
+    smallest_run = tail.endswith(b"AA")   # "A" and "AA" pad alike
+    assert st["round1_layout"]["compact"] == (not smallest_run), (tail, st["round1_layout"])
+    assert (got == oracle.sa_c(t)).all()
