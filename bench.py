@@ -55,11 +55,11 @@ ALPHABETS = {
 
 # bench kernel kind -> the HIP kernel it times (sa_build.hip Timer kinds)
 KERNEL_NAMES = {
-    "scatter_keys": "k_split_seg<SrcBucketKeys,9,10> (second bucket pass: units cut at the first pass's digit "
-                    "segments, places by per-(low, high digit) cursors, no look-back) | k_onesweep<SrcKeys,1024,4> "
-                    "(LSD first round)",
-    "scatter_first": "k_split_text<12> (first bucket pass: key1 from the text, scatter by atomic cursors) | "
-                     "k_onesweep<SrcKeysIota,1024,4> (LSD first round)",
+    "scatter_keys": "k_split_seg<SrcPk8,9,12> (second bucket pass over packed 8-byte items; SrcBucketKeys,9,10 "
+                    "over key1 + position when they do not fit: units cut at the first pass's digit segments, places "
+                    "by per-(low, high digit) cursors, no look-back) | k_onesweep<SrcKeys,1024,4> (LSD first round)",
+    "scatter_first": "k_split_text<12,1024,POW2,PK8> (first bucket pass: key1 from the text, packed 8-byte items "
+                     "scattered by atomic cursors) | k_onesweep<SrcKeysIota,1024,4> (LSD first round)",
     "local_sort": "k_bucket_sort<512,18> (per-window LDS sort: counting scatter + register sorting networks, "
                   "largest sub-bucket first; SA + every 16th key1 written)",
     "pack": "k_bucket_hist (first-pass digit totals) | k_pack_text (LSD first round keys)",

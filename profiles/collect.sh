@@ -13,10 +13,9 @@ out=gpurun_out/prof_$tag
 mkdir -p "$out"
 export TMPDIR=/tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/trace" -o trace -- \
-    python3 bench.py --no-cpu-baseline --json-out "$out/bench.json" "${args[@]}" > "$out/trace.log" 2>&1
+    python3 bench.py --no-cpu-baseline --no-reference-schedule --json-out "$out/bench.json" "${args[@]}" > "$out/trace.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$out/fetch" -o fetch -- \
-    python3 bench.py --no-cpu-baseline --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/fetch.log" 2>&1
+    python3 bench.py --no-cpu-baseline --no-reference-schedule --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/fetch.log" 2>&1
 timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$out/write" -o write -- \
-    python3 bench.py --no-cpu-baseline --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/write.log" 2>&1
+    python3 bench.py --no-cpu-baseline --no-reference-schedule --no-profile "${args[@]}" --steps 1 --warmup 0 > "$out/write.log" 2>&1
 python3 profiles/summarize.py "$tag" "$out" "${args[@]}"
-cp profiles/"$tag"_summary.json profiles/"$tag"_kernel_stats.csv "$out"/ 2>/dev/null || true
