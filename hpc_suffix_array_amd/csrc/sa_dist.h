@@ -318,13 +318,20 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((present[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
+    // the text's tail (every rank holds the text: all take the same layout)
+    const uint32_t tail_n = (uint32_t)std::min<uint64_t>(n, (uint64_t)kMaxK);
+    uint8_t* h_tail = reinterpret_cast<uint8_t*>(c->host_words + 2048);
+    SA_HIP(hipMemcpyAsync(h_tail, d_text + (n - tail_n), tail_n, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     d->sigma = sigma;
     const uint32_t K = choose_chars(sigma, n, 0);
     info->sigma = (int32_t)sigma;
     BucketPlan bp;
     c->radix = 0;
-    if (!plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world)) {
+    bool planned = plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world, !std::getenv("SA_NO_CMP"));
+    if (planned && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
+        planned = plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world, false);
+    if (!planned) {
         info->status = SA_DIST_UNSUPPORTED;   // one symbol / a key layout that does not fit
         return SA_OK;
     }

@@ -153,9 +153,9 @@ static bool short_suffix_ties(const uint8_t* tail, uint64_t n, uint32_t t, const
 }
 
 // The first bucket pass may write one packed 64-bit item per suffix
-// (k_split_text<.., PK8>, SrcPk8): one GPU, the whole bucket range, a
-// power-of-two alphabet, and the second pass's digit, key1 below its bucket
-// and the index fitting 64 bits
+// (k_split_text / k_split_list <.., PK8>, SrcPk8): a power-of-two alphabet,
+// and the second pass's digit (of the local bucket), key1 below its bucket and
+// the index fitting 64 bits
 static bool plan_pk8(const BucketPlan& bp, uint32_t hb) {
     const uint32_t sg = bp.bs.sigma;
     if (sg < 2 || (sg & (sg - 1)) != 0 || std::getenv("SA_NO_PK8")) return false;
@@ -273,7 +273,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
     const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
-    const bool pk8 = !listed && blo == 0 && bhi == (1u << bp.bs.bb) && plan_pk8(bp, hb);
+    const bool pk8 = plan_pk8(bp, hb);
     if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0);
     // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
     // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
@@ -306,9 +306,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             constexpr int kItemsL = SA_ITEMS_B;
             const uint64_t tl = (uint64_t)kSpBlock * kItemsL;
             const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((m + tl - 1) / tl, (uint64_t)c->cus));
-            hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
-                               (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
-                               os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor);
+            if (pk8)
+                hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock, true>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
+                                   (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
+                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, hb, bp.ib);
+            else
+                hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock, false>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
+                                   (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
+                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u);
         } else if (pk8) {
             SA_TEXT_PASS(true, true);
         } else if (pow2) {
@@ -319,7 +324,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_TEXT_PASS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, listed ? 24 * m : n + (pk8 ? 8 : 12) * m);
+    add_bytes(st, SA_K_SCATTER_FIRST, listed ? (pk8 ? 20 : 24) * m : n + (pk8 ? 8 : 12) * m);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);

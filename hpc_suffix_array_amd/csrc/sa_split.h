@@ -326,8 +326,8 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // Bucket range (range-partitioned build, sa_dist.h): only positions whose
 // bucket lies in [blo, bhi) are kept, digits of the local bucket bk - blo;
 // m = the number kept (the output's length).  One GPU: [0, 2^bb), m = n.
-// PK8 (POW2, one GPU, the whole bucket range): each pair leaves as ONE 64-bit
-// item -- the second pass's digit (the bucket's high hb bits) on top, then
+// PK8 (POW2): each pair leaves as ONE 64-bit
+// item -- the second pass's digit (the local bucket's high hb bits) on top, then
 // key1 below its bucket (key1 - Dmin(bucket) << rb: the bits of D under the
 // bucket and low) and the position in the low ib bits, so the pass writes 8
 // bytes per suffix instead of 12 (key1 + position) and the second pass reads
@@ -524,7 +524,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
                 if constexpr (PK8) {
-                    const uint32_t hi = (uint32_t)(k[j] >> kbsh) >> kLoBits;
+                    const uint32_t hi = ((uint32_t)(k[j] >> kbsh) - blo) >> kLoBits;   // local bucket
                     s_keys[pos] = ((uint64_t)hi << (64u - pk_hb)) | ((k[j] & remmask) << pk_ib) |
                                   (tb + ITEMS * dg + j);
                     s_idx[pos] = (uint16_t)d;
@@ -577,20 +577,22 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
 // claims and the scatter by the low kLoBits of the local bucket are those of
 // k_split_text.
 // ---------------------------------------------------------------------------
-template <int ITEMS, int BLOCK = kSpBlock>
+// PK8: packed 8-byte items as k_split_text<.., PK8> writes them
+template <int ITEMS, int BLOCK = kSpBlock, bool PK8 = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b, const uint64_t* __restrict__ lkeys,
                                                          const uint32_t* __restrict__ lpos, uint64_t m, uint32_t blo,
                                                          const uint32_t* __restrict__ digit_base,
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
                                                          uint32_t* __restrict__ out_vals,
-                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor) {
+                                                         uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor,
+                                                         uint32_t pk_hb = 0, uint32_t pk_ib = 0) {
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(TILE <= 65535, "16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];
-    __shared__ uint32_t s_pos[TILE];
+    __shared__ uint32_t s_pos[TILE];   // PK8: the pair's digit
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
     __shared__ uint32_t s_gofs[RADIX];
@@ -657,13 +659,21 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
         load(tn < tiles ? tn : tiles - 1, kn, vn);
+        const uint32_t kbsh = b.rb + (PK8 ? (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb : 0u);
+        const uint64_t remmask = PK8 ? (1ull << kbsh) - 1ull : 0ull;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t q = s_start[d] + (dr[j] & 0xFFFFu);
-                s_keys[q] = k[j];
-                s_pos[q] = v[j];
+                if constexpr (PK8) {
+                    const uint32_t hi = ((uint32_t)(k[j] >> kbsh) - blo) >> kLoBits;
+                    s_keys[q] = ((uint64_t)hi << (64u - pk_hb)) | ((k[j] & remmask) << pk_ib) | v[j];
+                    s_pos[q] = d;
+                } else {
+                    s_keys[q] = k[j];
+                    s_pos[q] = v[j];
+                }
             }
         }
         __syncthreads();
@@ -672,11 +682,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
             const uint32_t q = j * BLOCK + dg;
             if (q < valid) {
                 const uint64_t key = s_keys[q];
-                const uint32_t dd = (bucket_of(key, b.rb, b.cmul, b.bsh) - blo) & (RADIX - 1);
+                const uint32_t dd =
+                    PK8 ? s_pos[q] : (bucket_of(key, b.rb, b.cmul, b.bsh) - blo) & (RADIX - 1);
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
                 if (g < m) {
                     out_keys[g] = key;
-                    out_vals[g] = s_pos[q];
+                    if constexpr (!PK8) out_vals[g] = s_pos[q];
                 }
             }
         }
