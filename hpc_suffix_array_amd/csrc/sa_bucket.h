@@ -58,6 +58,12 @@ constexpr int kBsBlock = 512;
 #endif
 // 1: each thread sorts its sub-buckets largest first, 8-input networks where
 // no lane of the wave has more than 8 (A/B)
+#ifndef SA_LS_UG_TMP
+#define SA_LS_UG_TMP 1
+#endif
+#ifndef SA_LS_CLASSES
+#define SA_LS_CLASSES 1
+#endif
 #ifndef SA_LS_ORDER
 #define SA_LS_ORDER 1
 #endif
@@ -1027,6 +1033,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     __shared__ uint64_t s_w[CAP];
     __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
     __shared__ uint32_t s_tmp[WAVES];
+    __shared__ uint32_t s_tmp2[WAVES];
     __shared__ uint64_t s_red[2][WAVES];
     __shared__ uint32_t s_bk[2][32];
     constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
@@ -1175,10 +1182,24 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             const uint32_t sb = sb0 + ((order >> (2 * i)) & 3u);
             const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
             const bool wide = __ballot(cnt > 8u) != 0ull;   // uniform
+#if SA_LS_CLASSES
+            // network sizes 4 / 8 / 12 / 16 by the wave's largest sub-bucket
+            // of this rank (the largest of four is > 8 in almost every wave
+            // but > 12 in about a fifth; the smallest is <= 4 in a third)
+            const bool wide4 = __ballot(cnt > 4u) != 0ull, wide12 = __ballot(cnt > 12u) != 0ull;
+#endif
             if (cnt == 0) continue;
             const uint32_t nu0 = nu;
+#if SA_LS_CLASSES
+            if (!wide4 && low_bits <= 28) sort_sub<4>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else if (!wide12 && low_bits <= 28) sort_sub<12>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else
+#else
             if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
-            else if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
+            else
+#endif
+            if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
             if (nu != nu0) umask |= 1u << (sb - sb0);
         }
@@ -1201,13 +1222,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // nu, ng < 2^16 (a window holds <= kBsCap suffixes): one scan of
             // both; heads = singletons + U groups = m - U + G
             const uint32_t iug = wave_inclusive_sum(nu | (ng << 16));
+#if SA_LS_UG_TMP
+            // its own LDS words: no barrier for the reads of the count scan's s_tmp
+            uint32_t* const s_ug = s_tmp2;
+#else
+            uint32_t* const s_ug = s_tmp;
             __syncthreads();   // s_red / s_tmp reads of the scan above are done
-            if (lane == kWave - 1) s_tmp[wave] = iug;
+#endif
+            if (lane == kWave - 1) s_ug[wave] = iug;
             __syncthreads();
             uint32_t oug = 0, tug = 0;
 #pragma unroll
             for (int x = 0; x < WAVES; ++x) {
-                const uint32_t xug = s_tmp[x];
+                const uint32_t xug = s_ug[x];
                 oug += (x < (int)wave) ? xug : 0u;
                 tug += xug;
             }
