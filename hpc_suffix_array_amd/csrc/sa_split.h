@@ -43,6 +43,14 @@
 #ifndef SA_SEG_PROF
 #define SA_SEG_PROF 0
 #endif
+#ifndef SA_TEXT_PROF
+#define SA_TEXT_PROF 0
+#endif
+// the first pass's claims (atomic cursors) are waited for after the LDS
+// staging instead of before it (phase clocks: claims 15 % of the pass)
+#ifndef SA_LATE_CLAIM1
+#define SA_LATE_CLAIM1 1
+#endif
 #ifndef SA_EARLY_TICKET1
 #define SA_EARLY_TICKET1 2
 #endif
@@ -395,12 +403,26 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         const uint64_t tb = tt * TILE;
 #pragma unroll
         for (int i = 0; i < WPT; ++i) {
+            // words past NW (unused) re-read word NW - 1: no zero written
+            // into a register a load may still be filling
             const uint32_t w = dg + i * BLOCK;
-            raw[i] = w < (uint32_t)NW ? load4(tb + 4ull * w) : 0u;
+            raw[i] = load4(tb + 4ull * (w < (uint32_t)NW ? w : (uint32_t)NW - 1u));
         }
     };
     if (t < tiles) load(t);
     uint32_t par = 0;
+#if SA_TEXT_PROF
+    // diagnostic build (-DSA_TEXT_PROF=1): clock64 spans of thread 0 per phase
+    uint64_t pacc[5] = {0, 0, 0, 0, 0}, plast = clock64();
+#define TEXT_STAMP(k)                               \
+    if (dg == 0) {                                  \
+        const uint64_t now_ = clock64();            \
+        pacc[k] += now_ - plast;                    \
+        plast = now_;                               \
+    }
+#else
+#define TEXT_STAMP(k)
+#endif
     while (t < tiles) {
         const uint64_t tb = t * TILE;
         const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
@@ -424,6 +446,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
 #endif
         __syncthreads();
+        TEXT_STAMP(0)
 #if SA_EARLY_TICKET1 == 1
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         load(tn < tiles ? tn : tiles - 1);
@@ -481,14 +504,25 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             }
         }
         __syncthreads();
+        TEXT_STAMP(1)
         uint32_t tile_cnt = 0;
+        // SA_LATE_CLAIM1: the claim, read after the LDS staging (no zero
+        // initialisation: a register write there is a write-after-write on
+        // the previous tile's pending claim, and the compiler drained every
+        // memory operation for it)
+        uint32_t clm, dbase;
         if (dg < (uint32_t)RADIX) {
             tile_cnt = s_cnt[dg];
             s_cnt[dg] = 0;
             // the pass need not be stable, so a tile's place in each digit
             // is claimed from a cursor (one atomic round trip, whatever the
             // other tiles do) instead of a look-back
+#if SA_LATE_CLAIM1
+            dbase = digit_base[dg];
+            clm = tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u;
+#else
             s_gofs[dg] = digit_base[dg] + (tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u);
+#endif
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
@@ -509,6 +543,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
 #endif
         __syncthreads();
+        TEXT_STAMP(2)
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         load(tn < tiles ? tn : tiles - 1);
 #endif
@@ -534,7 +569,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 }
             }
         }
+#if SA_LATE_CLAIM1
+        // the claims' round trips overlapped the staging (only the writes
+        // need the tile's places)
+        if (dg < (uint32_t)RADIX) s_gofs[dg] = dbase + clm;
+#endif
         __syncthreads();
+        TEXT_STAMP(3)
         const uint32_t kept = s_kept;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
@@ -560,12 +601,20 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             }
         }
         __syncthreads();
+        TEXT_STAMP(4)
         t = tn;
         par ^= 1u;
     }
     for (uint32_t i = dg; i < 1024u; i += BLOCK)
         if (s_hhi[i]) atomicAdd(&ghist_hi[i], s_hhi[i]);
     if (over && ovf) atomicOr(ovf, 1u);
+#if SA_TEXT_PROF
+    if (dg == 0 && (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2))
+        printf("k_split_text wg %u clk: stage %llu keys %llu claims %llu scatter %llu write %llu\n", blockIdx.x,
+               (unsigned long long)pacc[0], (unsigned long long)pacc[1], (unsigned long long)pacc[2],
+               (unsigned long long)pacc[3], (unsigned long long)pacc[4]);
+#endif
+#undef TEXT_STAMP
 }
 
 // ---------------------------------------------------------------------------
