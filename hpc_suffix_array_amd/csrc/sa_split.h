@@ -40,6 +40,10 @@
 // kept off the compiler's atomic optimizer) was slower too (5.91 -> 6.0-6.3
 // ms, profiles/r02_ah_ab_seg_nodrain_reverted.txt): the pass is not waiting
 // on its store acknowledgements.
+// Claims issued before the LDS staging and waited for after it, then the
+// segment count and base wait (the order of the first pass's late claims):
+// 4.915 -> 4.95 ms (profiles/r02_am_ab_seg_late_claims_reverted.txt; the
+// publish branch before the writes made the compiler wait for every store).
 #ifndef SA_SEG_PROF
 #define SA_SEG_PROF 0
 #endif
