@@ -50,7 +50,10 @@ namespace sa {
 // <= 128 VGPRs, so two workgroups share a CU and one's loads and stores
 // overlap the other's sorting (1024 x 9 ran one per CU: 11.1 -> 8.3 ms at
 // 2^30 in microbench_bucket)
-constexpr int kBsBlock = 512;
+#ifndef SA_BS_BLOCK
+#define SA_BS_BLOCK 512
+#endif
+constexpr int kBsBlock = SA_BS_BLOCK;
 // 1: single-bucket windows load without rebuilding key1, group counts of a
 // sorted sub-bucket from an equal-neighbour bit mask (0: the v31 code, A/B)
 #ifndef SA_LS_FAST
@@ -58,6 +61,9 @@ constexpr int kBsBlock = 512;
 #endif
 // 1: each thread sorts its sub-buckets largest first, 8-input networks where
 // no lane of the wave has more than 8 (A/B)
+#ifndef SA_LS_FIXED_SPAN
+#define SA_LS_FIXED_SPAN 1
+#endif
 #ifndef SA_LS_UG_TMP
 #define SA_LS_UG_TMP 1
 #endif
@@ -545,6 +551,7 @@ __global__ __launch_bounds__(kLoRadix) void k_pad_starts(const uint32_t* __restr
 constexpr int kSubBits = SA_SUB_BITS;
 constexpr int kSubBuckets = 1 << kSubBits;
 constexpr uint32_t kMaxSub = 64;
+constexpr int kRetryWord = 13;   // words[]: fixed-span windows for the measured-span launch
 
 // where the second pass's bucket-relative items (k_split_seg) sit: window j
 // holds buckets [wb[j], wb[j + 1]); bucket b starts at bstart[b] and its
@@ -554,6 +561,9 @@ struct BucketRel {
     const uint32_t* __restrict__ bstart;
     const uint32_t* __restrict__ bdmin;
     uint32_t rb;
+    // SA_LS_FIXED_SPAN: bit width of the largest bucket-relative key of one
+    // bucket (0: measure each window's span)
+    uint32_t bits1 = 0;
 };
 
 // window j's items -> registers as w = (key1 - min) << ib | idx, with key1 =
@@ -564,7 +574,8 @@ template <int BLOCK, int ITEMS>
 __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, const BucketRel& br, uint32_t j,
                                             uint64_t a, uint32_t m, uint32_t ib, uint64_t (&w)[ITEMS], uint64_t& mn,
                                             uint32_t& bits, uint64_t (*s_red)[BLOCK / kWave],
-                                            uint32_t (*s_bk)[32], uint32_t* __restrict__ err) {
+                                            uint32_t (*s_bk)[32], uint32_t* __restrict__ err, bool* fixed = nullptr) {
+    if (fixed) *fixed = false;
     constexpr int WAVES = BLOCK / kWave;
     constexpr int WT = kWave * ITEMS;
     const uint32_t wave = wave_id(), lane = lane_id();
@@ -604,6 +615,27 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
     uint64_t mx = 0;
     mn = ~0ull;
 #if SA_LS_FAST
+#if SA_LS_FIXED_SPAN
+    if (nbk == 1 && br.bits1) {
+        // one bucket whose keys fill the plan's span (the compact layout):
+        // the items are w already, the sub-buckets split the whole span --
+        // no min / max reduction, no barrier
+        const uint32_t l0 = wave * WT + lane;
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            const uint32_t le = l0 + i * kWave;
+            w[i] = w_in[a + (le < m ? le : m - 1)];
+        }
+        bits = br.bits1;
+        mn = (uint64_t)dmin0 << br.rb;
+        if (fixed) *fixed = true;
+        // the caller's zeroing of the sub-bucket counters must be done before
+        // any wave counts (the min / max path's barrier did this; the loads
+        // stay in flight across it)
+        __syncthreads();
+        return true;
+    }
+#endif
     if (nbk == 1) {
         // one bucket (the common case from 2^29 suffixes): the items are
         // (key1 - Dmin) << ib | idx already, so w = item - (min's key part
@@ -1026,7 +1058,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
                                                        uint32_t ib, uint64_t* __restrict__ keys_out,
                                                        uint32_t* __restrict__ sa_out, uint32_t* __restrict__ skew,
-                                                       SegOut so) {
+                                                       SegOut so, uint32_t* __restrict__ retry = nullptr,
+                                                       uint32_t list_word = 7) {
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     constexpr int WT = kWave * ITEMS;
@@ -1042,7 +1075,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     uint32_t* err = words + 6;
-    const uint32_t nlist = words[7];
+    const uint32_t nlist = words[list_word];
     auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
     static_assert(WAVES * ITEMS * 8 <= kSubBuckets * 2, "per-row segment values fit in s_cnt");
     uint64_t th = 0, tu = 0, tg = 0;
@@ -1067,12 +1100,13 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         uint64_t w[ITEMS];
         uint64_t mn;
         uint32_t bits;
-        if (!load_window<BLOCK, ITEMS>(keys_in, br, j, a, m, ib, w, mn, bits, s_red, s_bk, err)) {
+        bool fixed;
+        if (!load_window<BLOCK, ITEMS>(keys_in, br, j, a, m, ib, w, mn, bits, s_red, s_bk, err, &fixed)) {
             __syncthreads();
             continue;
         }
         stamp(0);
-        const uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
+        uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
         if constexpr ((kVariant & 1) != 0) {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i)
@@ -1133,8 +1167,13 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         }
         __syncthreads();
         stamp(2);
-        if (big > kMaxSub) {   // uniform: clustered keys, leave the window to the LSD kernel
-            if (threadIdx.x == 0) skew[atomicAdd(&words[10], 1u)] = j;
+        if (big > kMaxSub) {   // uniform: clustered keys
+            // a fixed-span window goes to the retry launch (its measured span
+            // may spread the keys), else to the LSD kernel
+            if (threadIdx.x == 0) {
+                if (fixed && retry) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
+                else skew[atomicAdd(&words[10], 1u)] = j;
+            }
             __syncthreads();
             continue;
         }

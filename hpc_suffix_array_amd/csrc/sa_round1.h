@@ -417,7 +417,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* skew = list + nw;
     uint32_t* cnt_u = skew + nw;
     uint32_t* cnt_g = cnt_u + nw + 1;
-    const BucketRel br{cnt_g + nw + 1, c->segw + kBstartOff, c->segw + kBstartOff + kBstartWords, bp.bs.rb};
+    BucketRel br{cnt_g + nw + 1, c->segw + kBstartOff, c->segw + kBstartOff + kBstartWords, bp.bs.rb};
+    // the local sort's sub-buckets split a one-bucket window's whole key span
+    // (D values per bucket x 2^rb) when the compact layout fills it
+    if (bp.bs.cmp) {
+        const uint64_t ps = bp.bs.pow_s1 * bp.bs.sigma, per = (ps + (1ull << bp.bs.bb) - 1) >> bp.bs.bb;
+        br.bits1 = bit_width(per - 1) + bp.bs.rb;
+        // tests: a span wider than the keys' (they cluster in the low
+        // sub-buckets), so every window takes the measured-span recount
+        if (const char* e = std::getenv("SA_TEST_SPAN_EXTRA"))
+            br.bits1 = std::min<uint32_t>(br.bits1 + (uint32_t)std::atoi(e), 64u - bp.ib);
+    }
     SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
     uint32_t* const rank_arr = br_.rank ? br_.rank : c->rank;
     uint32_t* const member = br_.member ? br_.member : c->member;
@@ -426,6 +436,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // rank look-ups; a round that turns out dense re-runs the sort with every
     // key1 below (segments() reads them all)
     const SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g, kKeySample};
+    // fixed-span windows whose keys cluster, for a second launch with the
+    // measured span (after the windows' first buckets: 7 nw + 4 <= capacity)
+    uint32_t* const retry = cnt_g + 2 * nw + 2;
+    BucketRel br_measured = br;
+    br_measured.bits1 = 0;
     auto local_sort = [&](const SegOut& o) {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
 #if SA_LOCAL_SORT_CLS
@@ -433,9 +448,16 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
                            c->keys[0], d_sa, skew, o);
 #else
+        // (no SA_HIP here: its error return would make the lambda non-void)
+        (void)hipMemsetAsync(c->words + kRetryWord, 0, 4, s);
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                            (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
-                           c->keys[0], d_sa, skew, o);
+                           c->keys[0], d_sa, skew, o, br.bits1 ? retry : (uint32_t*)nullptr, 7u);
+        if (br.bits1)   // rare: a small grid loops over the retried windows
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(std::min<uint32_t>(g, 1024)), dim3(kBsBlock),
+                               0, s, (const uint64_t*)c->keys_u, br_measured, (const uint32_t*)ws,
+                               (const uint32_t*)retry, c->words, bp.ib, c->keys[0], d_sa, skew, o, (uint32_t*)nullptr,
+                               (uint32_t)kRetryWord);
 #endif
         // skewed windows are rare: a small grid loops over them (one
         // workgroup per listed window spent 0.1 ms on empty workgroups)

@@ -40,6 +40,9 @@
 // kept off the compiler's atomic optimizer) was slower too (5.91 -> 6.0-6.3
 // ms, profiles/r02_ah_ab_seg_nodrain_reverted.txt): the pass is not waiting
 // on its store acknowledgements.
+// Reading every pair's LDS slot before the staging writes (no read-wait-write
+// chain per pair) was slower in the first pass (4.19 -> 4.28 ms) and equal in
+// the second (profiles/r02_ao_ab_batched_slots_reverted.txt).
 // Claims issued before the LDS staging and waited for after it, then the
 // segment count and base wait (the order of the first pass's late claims):
 // 4.915 -> 4.95 ms (profiles/r02_am_ab_seg_late_claims_reverted.txt; the

@@ -579,3 +579,22 @@ def test_compact_layout_text_tails(gpu, oracle, tail):
     smallest_run = tail.endswith(b"AA")   # "A" and "AA" pad alike
     assert st["round1_layout"]["compact"] == (not smallest_run), (tail, st["round1_layout"])
     assert (got == oracle.sa_c(t)).all()
+
+
+@pytest.mark.parametrize("extra", [0, 6])
+def test_local_sort_fixed_span(gpu, oracle, extra, monkeypatch):
+    """One-bucket windows of the compact layout split the bucket's whole key
+    span into sub-buckets without measuring it (sa_bucket.h load_window,
+    SA_LS_FIXED_SPAN); a window whose keys cluster (forced here by a span 2^6
+    too wide: every key in the lowest sub-buckets) is listed for a second
+    launch that measures its span (sa_round1.h, retry list) instead of going
+    to the LSD kernel."""
+    from hpc_suffix_array_amd import build_suffix_array
+    if extra:
+        monkeypatch.setenv("SA_TEST_SPAN_EXTRA", str(extra))
+    for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21)):
+        t = oracle.gen_text(kind, n, seed=n + 5)
+        t[-1] = t.max()
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        assert st["round1"] == "bucketed" and st["round1_layout"]["compact"], (kind, st)
+        assert (got == oracle.sa_c(t)).all(), (kind, extra)
