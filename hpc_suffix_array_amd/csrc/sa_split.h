@@ -40,6 +40,10 @@
 // kept off the compiler's atomic optimizer) was slower too (5.91 -> 6.0-6.3
 // ms, profiles/r02_ah_ab_seg_nodrain_reverted.txt): the pass is not waiting
 // on its store acknowledgements.
+// First-pass writes unconditional in count (a slot past the tile's pairs
+// re-writing the last pair) so that the next tile's staging would not wait
+// for them: 4.09 -> 4.08 ms, within noise (profiles/r02_ar_ab_text_staging.txt;
+// the loop-top wait stays vmcnt(0) for the claims' branches anyway), dropped.
 // Reading every pair's LDS slot before the staging writes (no read-wait-write
 // chain per pair) was slower in the first pass (4.19 -> 4.28 ms) and equal in
 // the second (profiles/r02_ao_ab_batched_slots_reverted.txt).
@@ -433,16 +437,24 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     while (t < tiles) {
         const uint64_t tb = t * TILE;
         const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
-        // dense digits (0 past the end)
+        // dense digits (0 past the end); a tile whose staged words lie inside
+        // the text maps its four bytes with four independent LDS reads (the
+        // per-byte bounds test made them a chain of branches and waits)
+        const bool whole = tb + 4ull * NW <= n;   // uniform
 #pragma unroll
         for (int i = 0; i < WPT; ++i) {
             const uint32_t w = dg + i * BLOCK;
             if (w < (uint32_t)NW) {
                 uint32_t o = 0;
+                if (whole) {
+                    o = (uint32_t)s_map[raw[i] & 0xFFu] | ((uint32_t)s_map[(raw[i] >> 8) & 0xFFu] << 8) |
+                        ((uint32_t)s_map[(raw[i] >> 16) & 0xFFu] << 16) | ((uint32_t)s_map[raw[i] >> 24] << 24);
+                } else {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const uint64_t pos = tb + 4ull * w + q;
-                    o |= (pos < n ? (uint32_t)s_map[(raw[i] >> (8 * q)) & 0xFFu] : 0u) << (8 * q);
+                    for (int q = 0; q < 4; ++q) {
+                        const uint64_t pos = tb + 4ull * w + q;
+                        o |= (pos < n ? (uint32_t)s_map[(raw[i] >> (8 * q)) & 0xFFu] : 0u) << (8 * q);
+                    }
                 }
                 s_dcw[w] = o;
             }
