@@ -86,3 +86,18 @@ def test_unsigned_semantics(oracle):
     assert list(oracle.sa_c(t)) == [1, 0]
     t = np.frombuffer(b"a\x00b\x00", np.uint8)
     assert list(oracle.sa_c(t)) == list(oracle.sa_numpy(t))
+
+
+def test_oracle_under_sanitizers():
+    """The C restatement built with AddressSanitizer + UBSan (host code only,
+    oracle/Makefile `asan`) over the edge cases of SURVEY.md section 5: empty,
+    one symbol, degenerate and periodic runs, bytes 0x00 / 0xFF, ragged
+    sizes -- every SA O(n)-checked, LCP and LRS computed."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-C", os.path.join(root, "oracle"), "asan"], check=True)
+    r = subprocess.run([os.path.join(root, "oracle", "build", "asan_check")], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    assert "FAIL" not in r.stdout and "ERROR" not in r.stderr
