@@ -563,6 +563,10 @@ static uint32_t choose_chars(uint32_t sigma, uint64_t n, int32_t req) {
 // unsorted-set rounds try the per-group register sort when the average
 // group holds at most kUsAvg suffixes; its oversize flag lives in words[12]
 constexpr uint64_t kUsAvg = 4;
+// per-group register sort over keys materialised one lane per suffix first
+#ifndef SA_US_TWO_PHASE
+#define SA_US_TWO_PHASE 1
+#endif
 constexpr int kUsFlagWord = 12;
 
 template <class Pos>
@@ -735,6 +739,19 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             SA_HIP(hipMemsetAsync(c->words + kUsFlagWord, 0, 4, s));
             const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
             tm.begin(SA_K_SORT_U);
+#if SA_US_TWO_PHASE
+            // the keys first, one lane per suffix, then each group's lane sorts
+            // them in place (ukb0 is read and written by that lane only)
+            const uint32_t gk = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 65536);
+            if (sparse)
+                hipLaunchKernelGGL(k_usort_keys<SrcU<true>>, dim3(gk), dim3(kBlock), 0, s,
+                                   SrcU<true>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, m, ukb0);
+            else
+                hipLaunchKernelGGL(k_usort_keys<SrcU<false>>, dim3(gk), dim3(kBlock), 0, s,
+                                   SrcU<false>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, m, ukb0);
+            hipLaunchKernelGGL(k_usort_small<SrcKeys>, dim3(grid), dim3(kBlock), 0, s,
+                               SrcKeys{ukb0, c->u_idx[ui]}, c->u_g[ui], m, ukb0, c->vals_u, c->words + kUsFlagWord);
+#else
             if (sparse)
                 hipLaunchKernelGGL(k_usort_small<SrcU<true>>, dim3(grid), dim3(kBlock), 0, s,
                                    SrcU<true>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, c->u_g[ui], m, ukb0, c->vals_u,
@@ -743,6 +760,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
                 hipLaunchKernelGGL(k_usort_small<SrcU<false>>, dim3(grid), dim3(kBlock), 0, s,
                                    SrcU<false>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, c->u_g[ui], m, ukb0, c->vals_u,
                                    c->words + kUsFlagWord);
+#endif
             tm.end();
             SA_HIP(hipGetLastError());
             SA_HIP(hipMemcpyAsync(c->host_words + kUsFlagWord, c->words + kUsFlagWord, 4, hipMemcpyDeviceToHost, s));

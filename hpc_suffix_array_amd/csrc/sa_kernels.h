@@ -362,6 +362,15 @@ __global__ __launch_bounds__(kBlock) void k_usort_small(Src src, const uint32_t*
     }
 }
 
+// The keys of an unsorted-set round, one lane per suffix (each a sparse rank
+// look-up: a chain of dependent loads), for k_usort_small to read: the
+// group's first lane no longer walks its members' look-ups one after another.
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_usort_keys(Src src, uint64_t m, uint64_t* __restrict__ out_keys) {
+    for (uint64_t s = (uint64_t)blockIdx.x * kBlock + threadIdx.x; s < m; s += (uint64_t)gridDim.x * kBlock)
+        out_keys[s] = src.key(s);
+}
+
 // Later passes: the previous pass's output.
 struct SrcKeys {
     const uint64_t* __restrict__ keys;
