@@ -44,6 +44,9 @@
 // re-writing the last pair) so that the next tile's staging would not wait
 // for them: 4.09 -> 4.08 ms, within noise (profiles/r02_ar_ab_text_staging.txt;
 // the loop-top wait stays vmcnt(0) for the claims' branches anyway), dropped.
+// Packed items staged whole in the second pass (digit from the item's top
+// bits, no 16-bit digit array): 4.646 -> 4.650 ms, and 14 pairs per lane with
+// the LDS so saved spill (5.16 ms): profiles/r02_au_ab_pk_digit_in_item.txt.
 // Reading every pair's LDS slot before the staging writes (no read-wait-write
 // chain per pair) was slower in the first pass (4.19 -> 4.28 ms) and equal in
 // the second (profiles/r02_ao_ab_batched_slots_reverted.txt).
