@@ -47,6 +47,10 @@
 // Packed items staged whole in the second pass (digit from the item's top
 // bits, no 16-bit digit array): 4.646 -> 4.650 ms, and 14 pairs per lane with
 // the LDS so saved spill (5.16 ms): profiles/r02_au_ab_pk_digit_in_item.txt.
+// The first pass's early ticket kept off the atomic optimizer and held in a
+// register until the claims (no wait for it, nor drain of wave 0, before the
+// staging barrier) was slower: 4.09 -> 4.50 ms
+// (profiles/r02_ax_ab_text_ticket_deferred.txt).
 // Reading every pair's LDS slot before the staging writes (no read-wait-write
 // chain per pair) was slower in the first pass (4.19 -> 4.28 ms) and equal in
 // the second (profiles/r02_ao_ab_batched_slots_reverted.txt).
