@@ -61,6 +61,9 @@ constexpr int kBsBlock = SA_BS_BLOCK;
 #endif
 // 1: each thread sorts its sub-buckets largest first, 8-input networks where
 // no lane of the wave has more than 8 (A/B)
+#ifndef SA_LS_STORE_NOWAIT
+#define SA_LS_STORE_NOWAIT 1
+#endif
 #ifndef SA_LS_FIXED_SPAN
 #define SA_LS_FIXED_SPAN 1
 #endif
@@ -1322,7 +1325,12 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 }
             }
         }
+#if !SA_LS_STORE_NOWAIT
         __syncthreads();
+#endif
+        // (SA_LS_STORE_NOWAIT: the U/G scan's barrier already follows every
+        // thread's sort; the unsorted-set writes and the store only read s_w,
+        // so the store need not wait for the few threads walking groups)
         stamp(5);
         store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
