@@ -24,6 +24,12 @@
 #ifndef SA_ITEMS_A
 #define SA_ITEMS_A 12
 #endif
+#ifndef SA_TEXT_BLOCK
+#define SA_TEXT_BLOCK 512
+#endif
+#ifndef SA_SEG_BLOCK
+#define SA_SEG_BLOCK 1024
+#endif
 #ifndef SA_ITEMS_B
 #define SA_ITEMS_B 10
 #endif
@@ -293,12 +299,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         // 12288-position tiles (8192: 5.7 ms, measured on the same box)
         constexpr int kItemsA = SA_ITEMS_A;
-        const uint64_t tile = (uint64_t)kSpBlock * kItemsA;
+        constexpr int kTextBlock = SA_TEXT_BLOCK;   // workgroups of 1024 / kTextBlock per CU
+        const uint64_t tile = (uint64_t)kTextBlock * kItemsA;
         const uint64_t tiles = (n + tile - 1) / tile;
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)c->cus));
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>(tiles, (uint64_t)c->cus * (kSpBlock / kTextBlock)));
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
 #define SA_TEXT_PASS(P, PK)                                                                                   \
-    hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, P, PK>), dim3(grid), dim3(kSpBlock), 0, s, d_text, n,   \
+    hipLaunchKernelGGL((k_split_text<kItemsA, kTextBlock, P, PK>), dim3(grid), dim3(kTextBlock), 0, s, d_text, n, \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib)
@@ -342,12 +350,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
         SA_HIP(hipMemsetAsync(c->segw, 0, segw_words(1u << hb) * 4, s));   // <= 3 MiB
-        const uint64_t ut = (uint64_t)kSpBlock * (pk8 ? kItemsPk : kItemsB);
+        // workgroups of kSegBlock threads (1024 / kSegBlock per CU) for radices up to 512
+        constexpr int kSegBlock = SA_SEG_BLOCK;
+        const int sblk = hb <= 9 ? kSegBlock : kSpBlock;
+        const uint64_t ut = (uint64_t)sblk * (pk8 ? kItemsPk : kItemsB);
         const uint64_t units = (m + ut - 1) / ut + kSegs;
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)c->cus));
+        const uint32_t grid = (uint32_t)std::max<uint64_t>(
+            1, std::min<uint64_t>(units, (uint64_t)c->cus * (kSpBlock / sblk)));
         switch (hb) {
 #define SA_SEG_LAUNCH(S, B, SRC, SH, IT)                                                                      \
-    hipLaunchKernelGGL((k_split_seg<S, B, IT>), dim3(grid), dim3(kSpBlock), 0, s, SRC, m, SH,                  \
+    hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock)>), dim3(grid),                    \
+                       dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                                  \
                        (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,          \
                        c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr)
 #define SA_SEG_PASS(B)                                                                                        \

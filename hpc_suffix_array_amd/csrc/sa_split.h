@@ -346,7 +346,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // a K - 1 byte halo, as 32-bit words) is loaded while the current one is
 // staged and written.
 // ---------------------------------------------------------------------------
-// (BLOCK 512, two workgroups per CU, measured slower: 5.5 -> 6.3 ms)
+// Launched as BLOCK 512 x 12 items, two workgroups per CU (SA_TEXT_BLOCK):
+// one workgroup's scatter overlaps the other's staging and barriers, 4.09 ->
+// 3.62 ms at 1 GiB DNA over one 1024 x 12 workgroup per CU (an early version
+// measured the opposite, 5.5 -> 6.3 ms; 256 x 12: 6.6 ms, 512 x 8: 5.0 ms)
 // POW2: sigma a power of two -- D and the remainder roll by shifts and masks
 // and the bucket is a bit field of D (no multiplications)
 // Bucket range (range-partitioned build, sa_dist.h): only positions whose
@@ -805,7 +808,8 @@ constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; 
 constexpr uint64_t kBstartOff = segw_words(1024);
 constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 
-// (BLOCK 512 x 10 items, two workgroups per CU, measured slower: 7.2 -> 9.1 ms)
+// (BLOCK 512 x 10 items, two workgroups per CU, measured slower: 7.2 -> 9.1 ms;
+// again with PK8 items, 512 x 12 (SA_SEG_BLOCK=512): 4.64 -> 6.27 ms)
 template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint64_t n, uint32_t shift,
                                                         const uint32_t* __restrict__ lo_base,
