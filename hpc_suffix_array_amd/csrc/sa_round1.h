@@ -299,14 +299,18 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     {
         // 12288-position tiles (8192: 5.7 ms, measured on the same box)
         constexpr int kItemsA = SA_ITEMS_A;
-        constexpr int kTextBlock = SA_TEXT_BLOCK;   // workgroups of 1024 / kTextBlock per CU
-        const uint64_t tile = (uint64_t)kTextBlock * kItemsA;
-        const uint64_t tiles = (n + tile - 1) / tile;
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(
-            1, std::min<uint64_t>(tiles, (uint64_t)c->cus * (kSpBlock / kTextBlock)));
+        // power-of-two alphabets: two 512-thread workgroups per CU (4.09 -> 3.62 ms
+        // at 1 GiB DNA); others one 1024-thread workgroup (ascii127 5.09 ms vs 6.15
+        // at 512, alnum 5.13 vs 4.90: profiles/r02_bc_ab_text_block_kinds.txt)
+        constexpr int kTextBlock = SA_TEXT_BLOCK;
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
-#define SA_TEXT_PASS(P, PK)                                                                                   \
-    hipLaunchKernelGGL((k_split_text<kItemsA, kTextBlock, P, PK>), dim3(grid), dim3(kTextBlock), 0, s, d_text, n, \
+        auto text_grid = [&](int block) {
+            const uint64_t tile = (uint64_t)block * kItemsA;
+            return (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>((n + tile - 1) / tile, (uint64_t)c->cus * (kSpBlock / block)));
+        };
+#define SA_TEXT_PASS(P, PK, BLK)                                                                              \
+    hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n,  \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib)
@@ -323,11 +327,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u);
         } else if (pk8) {
-            SA_TEXT_PASS(true, true);
+            SA_TEXT_PASS(true, true, kTextBlock);
         } else if (pow2) {
-            SA_TEXT_PASS(true, false);
+            SA_TEXT_PASS(true, false, kTextBlock);
         } else {
-            SA_TEXT_PASS(false, false);
+            SA_TEXT_PASS(false, false, kSpBlock);
         }
 #undef SA_TEXT_PASS
     }
