@@ -27,6 +27,9 @@
 #ifndef SA_TEXT_BLOCK
 #define SA_TEXT_BLOCK 512
 #endif
+#ifndef SA_LIST_BLOCK
+#define SA_LIST_BLOCK 1024
+#endif
 #ifndef SA_SEG_BLOCK
 #define SA_SEG_BLOCK 1024
 #endif
@@ -315,15 +318,16 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib)
         if (listed) {
-            constexpr int kItemsL = SA_ITEMS_B;
-            const uint64_t tl = (uint64_t)kSpBlock * kItemsL;
-            const uint32_t gl = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((m + tl - 1) / tl, (uint64_t)c->cus));
+            constexpr int kItemsL = SA_ITEMS_B, kListBlock = SA_LIST_BLOCK;
+            const uint64_t tl = (uint64_t)kListBlock * kItemsL;
+            const uint32_t gl = (uint32_t)std::max<uint64_t>(
+                1, std::min<uint64_t>((m + tl - 1) / tl, (uint64_t)c->cus * (kSpBlock / kListBlock)));
             if (pk8)
-                hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock, true>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
+                hipLaunchKernelGGL((k_split_list<kItemsL, kListBlock, true>), dim3(gl), dim3(kListBlock), 0, s, bp.bs,
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, hb, bp.ib);
             else
-                hipLaunchKernelGGL((k_split_list<kItemsL, kSpBlock, false>), dim3(gl), dim3(kSpBlock), 0, s, bp.bs,
+                hipLaunchKernelGGL((k_split_list<kItemsL, kListBlock, false>), dim3(gl), dim3(kListBlock), 0, s, bp.bs,
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u);
         } else if (pk8) {
