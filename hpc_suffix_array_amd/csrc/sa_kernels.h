@@ -754,6 +754,10 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
 // Presence is all the dense codes need; it is kept in 8 registers per lane
 // (no LDS atomics, so a 4-symbol text costs no bank conflicts), OR-reduced
 // over the wave, one atomicOr per word per wave.
+// SA_ALPHA_FAST: 16-byte chunks inside one 32-symbol block take one LDS
+// atomic instead of 16 -- measured equal at 1 GiB DNA (0.274-0.289 ms either
+// way, profiles/r02_bd_ab_alpha_fast.txt): the kernel is not bound by its LDS
+// atomics, so the simpler path stays the default
 #ifndef SA_ALPHA_FAST
 #define SA_ALPHA_FAST 0
 #endif
