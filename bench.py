@@ -42,6 +42,8 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+from hpc_suffix_array_amd._native import source_hash   # noqa: E402  (no GPU, no torch)
+SRC_HASH = source_hash()
 METRIC = "suffixes sorted/sec + ms/doubling-round, 1 GiB input at 1/2/4/8 MI355X"   # BASELINE.json metric
 
 ALPHABETS = {
@@ -131,20 +133,45 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
                       f"host cpus {os.cpu_count()}"}
 
 
-def pmc_summary() -> dict | None:
-    """The latest committed rocprofv3 summary (profiles/<tag>_summary.json,
-    written by profiles/collect.sh + summarize.py), or None."""
-    def version(path):   # r01_v21_summary.json -> (1, 21): numeric, not lexical, order
-        nums = re.findall(r"\d+", os.path.basename(path))
-        return tuple(int(x) for x in nums)
-    paths = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_summary.json")), key=version)
-    if not paths:
+def tag_order(tag: str) -> tuple:
+    """Sort key of a profile tag: round, then the version within the round.
+    Round 1 used v<number> (r01_v9 < r01_v30), later rounds letter tags in
+    bijective base 26 (r02_o < r02_z < r02_aa < r02_bb): length, then text."""
+    m = re.match(r"r(\d+)_(.+)$", tag)
+    if not m:
+        return (-1, 0, 0, tag)
+    rnd, rest = int(m.group(1)), m.group(2)
+    v = re.fullmatch(r"v(\d+)", rest)
+    if v:
+        return (rnd, 0, int(v.group(1)), "")
+    return (rnd, 1, len(rest), rest)
+
+
+def pmc_summary(n: int, kind: str, src_hash: str | None, profiles_dir: str | None = None) -> dict | None:
+    """The rocprofv3 summary (profiles/<tag>_summary.json, written by
+    profiles/collect.sh + summarize.py) of this workload: among the summaries
+    of the same n and kind, the one stamped with the current sources' hash
+    (latest tag if several); else the latest one, marked "stale" (its
+    traffic measured older code).  None when no summary has this workload."""
+    d = profiles_dir or os.path.join(ROOT, "profiles")
+    cands = []
+    for p in glob.glob(os.path.join(d, "*_summary.json")):
+        try:
+            with open(p) as f:
+                s = json.load(f)
+        except (OSError, ValueError):
+            continue
+        args = list(s.get("args") or [])
+        extra = [x for i, x in enumerate(args) if x not in ("--n", "--kind") and (i == 0 or args[i - 1] not in ("--n", "--kind"))]
+        if s.get("n") == n and s.get("kind") == kind and not extra:
+            tag = s.get("tag") or os.path.basename(p)[: -len("_summary.json")]
+            cands.append((tag_order(tag), tag, s))
+    if not cands:
         return None
-    try:
-        with open(paths[-1]) as f:
-            return json.load(f)
-    except (OSError, ValueError):
-        return None
+    cands.sort(key=lambda x: x[0])
+    same = [c for c in cands if src_hash and c[2].get("src_hash") == src_hash]
+    _, tag, s = (same or cands)[-1]
+    return dict(s, tag=tag, stale=not same)
 
 
 def make_text(b, n, kind, seed, dev, sptr):
@@ -229,13 +256,15 @@ def run_single(a, torch, dev, world, rank, barrier):
             avg_s = kern[dom]["ms"] / kern[dom]["launches"] / 1e3
             per_launch = kern[dom]["bytes"] / kern[dom]["launches"]
             ach = per_launch / avg_s / 1e9
-            traffic = None
-            pmc = pmc_summary()
-            if pmc and pmc.get("n") == n and pmc.get("kind") == a.kind:
+            traffic = traffic_src = None
+            pmc = pmc_summary(n, a.kind, SRC_HASH)
+            if pmc:
                 skind = {"scatter_first": "scatter_first" if bucketed else "scatter_iota"}.get(dom, dom)
                 traffic = pmc.get("traffic_bytes_per_launch", {}).get(skind)
+                traffic_src = {"summary": f"profiles/{pmc['tag']}_summary.json", "src_hash": pmc.get("src_hash"),
+                               "stale": pmc["stale"]}
             roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic,
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": KERNEL_NAMES.get(dom, dom) + (" [bucketed round 1]" if bucketed else ""),
                         "kind": dom, "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
     extra = {
@@ -373,6 +402,7 @@ def main():
         "scaling": "weak" if (world > 1 and not distributed) else "strong",
         "vs_baseline": None,
         "dtype": "u32",
+        "src_hash": SRC_HASH,
         "data": f"synthetic: seeded splitmix64 {a.kind} text generated in HBM (SURVEY.md 8(d)), seed {a.seed}"
                 + ("" if distributed or world == 1 else "+rank"),
         "config": {"workload": f"{a.kind} n={a.n} ({a.n / (1 << 30):.3g} GiB)"

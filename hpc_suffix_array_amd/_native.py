@@ -35,7 +35,7 @@ EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", 
                "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
                "sa_gather_u64_device", "sa_running_max_i64_device",
-               "sa_dist_begin", "sa_dist_cuts", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
+               "sa_dist_begin", "sa_dist_cuts", "sa_dist_plan_cuts", "sa_dist_release", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
                "sa_dist_answer", "sa_dist_refine",
                "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
 
@@ -124,6 +124,21 @@ class SuffixArrayStruct(ctypes.Structure):
 _lib = None
 
 
+def source_hash() -> str:
+    """SHA-256 (first 16 hex digits) of the sources libsa_hip.so is built
+    from: bench.py stamps it on its line and profiles/summarize.py on each
+    rocprof summary, so a summary is matched to the code it measured."""
+    import glob
+    import hashlib
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(CSRC, "sa_*")) + [os.path.join(CSRC, "Makefile")]
+                   + glob.glob(os.path.join(PKG_DIR, "..", "include", "*.h")))
+    for p in files:
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read())
+    return h.hexdigest()[:16]
+
+
 def build_library(force: bool = False) -> str:
     """Compile libsa_hip.so for gfx950 in-tree (hipcc cross-compiles without a GPU)."""
     if force or not os.path.exists(LIB_PATH):
@@ -173,12 +188,15 @@ def lib() -> ctypes.CDLL:
     DI = ctypes.POINTER(SaDistInfo)
     L.sa_dist_begin.argtypes = [vp, vp, u64, i32, i32, ctypes.POINTER(ctypes.c_uint32), vp, vp, DI]
     L.sa_dist_cuts.argtypes = [vp, ctypes.POINTER(u64), DI]
+    L.sa_dist_plan_cuts.argtypes = [i32, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint32),
+                                    ctypes.POINTER(u64)]
+    L.sa_dist_release.argtypes = [vp]
     L.sa_dist_round1.argtypes = [vp, vp, vp, DI, ctypes.POINTER(SaStats)]
     L.sa_dist_req_count.argtypes = [vp, u64, ctypes.POINTER(u64), vp, DI]
     L.sa_dist_req_fill.argtypes = [vp, u64, vp, vp]
     L.sa_dist_answer.argtypes = [vp, vp, u64, vp, vp]
     L.sa_dist_refine.argtypes = [vp, u64, vp, vp, vp, DI]
-    for f in (L.sa_dist_begin, L.sa_dist_cuts, L.sa_dist_round1, L.sa_dist_req_count, L.sa_dist_req_fill,
+    for f in (L.sa_dist_begin, L.sa_dist_cuts, L.sa_dist_plan_cuts, L.sa_dist_release, L.sa_dist_round1, L.sa_dist_req_count, L.sa_dist_req_fill,
               L.sa_dist_answer, L.sa_dist_refine):
         f.restype = i32
     L.sa_generate_text_device.argtypes = [vp, u64, u64, ctypes.c_char_p, ctypes.c_uint32, vp]

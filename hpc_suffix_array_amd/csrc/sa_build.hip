@@ -1597,6 +1597,26 @@ int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info) 
     return dist_cuts(ctx, h_coarse, info);
 }
 
+int sa_dist_release(sa_context* ctx) {
+    if (!ctx) return set_err(SA_E_INVALID, "NULL argument");
+    SA_HIP(hipSetDevice(ctx->device));
+    SA_HIP(hipDeviceSynchronize());
+    free_dist(ctx);
+    return SA_OK;
+}
+
+int sa_dist_plan_cuts(int world, uint64_t n, int bucket_bits, const uint64_t* h_coarse, uint32_t* cuts_out,
+                      uint64_t* m_max) {
+    if (world < 1 || world > kDistMaxWorld || !h_coarse || !cuts_out || !m_max)
+        return set_err(SA_E_INVALID, "bad argument");
+    if (bucket_bits < (int)kCoarseBits || bucket_bits > 32) return set_err(SA_E_INVALID, "bucket_bits out of range");
+    std::vector<uint64_t> pre(kCoarse + 1, 0);
+    for (uint32_t i = 0; i < kCoarse; ++i) pre[i + 1] = pre[i] + h_coarse[i];
+    if (pre[kCoarse] != n) return set_err(SA_E_INVALID, "coarse histogram does not sum to n");
+    return plan_cuts(world, n, (uint32_t)bucket_bits - kCoarseBits, pre.data(), cuts_out, m_max) ? SA_DIST_OK
+                                                                                                  : SA_DIST_UNBALANCED;
+}
+
 int sa_dist_round1(sa_context* ctx, uint32_t* d_sa_local, void* stream, sa_dist_info* info, sa_stats* stats) {
     if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
     if (!ctx->dist) return set_err(SA_E_INVALID, "sa_dist_round1 before sa_dist_begin");

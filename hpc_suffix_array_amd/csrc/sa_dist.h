@@ -360,6 +360,47 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     return SA_OK;
 }
 
+// The cut plan (host only): W contiguous ranges of coarse buckets from the
+// prefix sums pre[0 .. kCoarse] of the global coarse histogram.  Cut q is the
+// coarse boundary nearest q n / W, clamped so that every range holds at most
+// cap = 2^18 >> cs coarse buckets (the second pass's local buckets) -- also
+// the ranges still to come: cut[q] >= kCoarse - (W - q) cap.  Returns whether
+// the plan is usable: every range within the cap and the largest within 1.5x
+// of the mean (+ 65536); *mmax = the largest range's suffix count.
+static bool plan_cuts(int W, uint64_t n, uint32_t cs, const uint64_t* pre, uint32_t* cut, uint64_t* mmax) {
+    const uint64_t cap = (1ull << 18) >> cs;
+    cut[0] = 0;
+    cut[W] = kCoarse;
+    for (int q = 1; q < W; ++q) {
+        const uint64_t t = n * (uint64_t)q / W;
+        uint32_t lo = cut[q - 1], hi = kCoarse;   // first i >= cut[q - 1] with pre[i] >= t
+        while (lo < hi) {
+            const uint32_t mid = (lo + hi) / 2;
+            if (pre[mid] >= t) hi = mid;
+            else lo = mid + 1;
+        }
+        // the boundary just before it when that one is nearer to t
+        if (lo > cut[q - 1] && t - pre[lo - 1] < pre[lo] - t) --lo;
+        const uint64_t hi_cap = (uint64_t)cut[q - 1] + cap;
+        const uint64_t rest = (uint64_t)(W - q) * cap;
+        const uint64_t lo_cap = rest >= kCoarse ? 0 : kCoarse - rest;
+        uint64_t x = lo;
+        if (x > hi_cap) x = hi_cap;
+        if (x < lo_cap) x = lo_cap;
+        if (x < cut[q - 1]) x = cut[q - 1];
+        if (x > kCoarse) x = kCoarse;
+        cut[q] = (uint32_t)x;
+    }
+    bool ok = true;
+    uint64_t mx = 0;
+    for (int q = 0; q < W; ++q) {
+        mx = std::max(mx, pre[cut[q + 1]] - pre[cut[q]]);
+        if ((uint64_t)(cut[q + 1] - cut[q]) > cap) ok = false;
+    }
+    *mmax = mx;
+    return ok && mx <= (n / W) + (n / W) / 2 + 65536;
+}
+
 // h_coarse: the global coarse histogram (sum over ranks; NULL at world 1)
 static int dist_cuts(sa_context* c, const uint64_t* h_coarse, sa_dist_info* info) {
     DistState* d = c->dist;
@@ -377,32 +418,15 @@ static int dist_cuts(sa_context* c, const uint64_t* h_coarse, sa_dist_info* info
             return set_err(SA_E_INTERNAL, "coarse histogram sums to %llu, not n = %llu",
                            (unsigned long long)pre[kCoarse], (unsigned long long)n);
     }
-    // cut q = the first coarse boundary whose prefix reaches q n / W
-    d->cut.assign(W + 1, 0);
-    d->cut[W] = kCoarse;
-    for (int q = 1; q < W; ++q) {
-        const uint64_t t = n * (uint64_t)q / W;
-        uint32_t lo = d->cut[q - 1], hi = kCoarse;   // first i >= lo with pre[i] >= t
-        while (lo < hi) {
-            const uint32_t mid = (lo + hi) / 2;
-            if (pre[mid] >= t) hi = mid;
-            else lo = mid + 1;
-        }
-        d->cut[q] = lo;
-    }
     const uint32_t cs = dist_cshift(*d);
+    d->cut.assign(W + 1, 0);
     uint64_t mmax = 0;
-    for (int q = 0; q < W; ++q) mmax = std::max(mmax, pre[d->cut[q + 1]] - pre[d->cut[q]]);
+    const bool ok = plan_cuts(W, n, cs, pre.data(), d->cut.data(), &mmax);
     const int r = d->rank;
     d->blo = d->cut[r] << cs;
     d->bhi = d->cut[r + 1] << cs;
     d->m = pre[d->cut[r + 1]] - pre[d->cut[r]];
     d->sa_off = pre[d->cut[r]];
-    // balance: the largest range within 1.5x of the mean; each rank's bucket
-    // range within the second pass's 2^18 local buckets
-    bool ok = mmax <= (n / W) + (n / W) / 2 + 65536;
-    for (int q = 0; q < W; ++q)
-        if (((uint64_t)(d->cut[q + 1] - d->cut[q]) << cs) > (1ull << 18)) ok = false;
     info->m = d->m;
     info->sa_off = d->sa_off;
     info->m_max = mmax;

@@ -234,8 +234,13 @@ class HipRangeOps:
         return self._info()
 
     def fallback_ops(self) -> "HipOps":
+        """The sample-sort driver's operations on this rank's own context:
+        the range build's per-rank buffers (n-entry rank array, member map,
+        request buffers) are released first and the workspace is shared, so
+        the fallback does not double the HBM footprint."""
+        N.check(self.L.sa_dist_release(self.b.ctx), "sa_dist_release")
         if not hasattr(self, "_fb"):
-            self._fb = HipOps(0, self.dev.index)
+            self._fb = HipOps(0, self.dev.index, builder=self.b)
         return self._fb
 
 
@@ -276,6 +281,25 @@ class DistributedSA:
                 out[a] = round(out.get(a, 0.0) + ea.elapsed_time(eb), 4)
         return out
 
+    def _phase(self, name: str, dev, fn, *args):
+        """Run one native phase and agree on its outcome: a libsa_hip error on
+        one rank (NOMEM, a request outside the range, ...) makes EVERY rank
+        raise here, instead of leaving the others blocked in the next
+        collective until its timeout (one all_reduce MAX per phase, G > 1)."""
+        err, res = None, None
+        try:
+            res = fn(*args)
+        except N.SAError as e:
+            err = e
+        if self.G > 1:
+            t = torch.tensor([1 if err is not None else 0], dtype=I64, device=dev)
+            _all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
+            if int(t.item()) and err is None:
+                raise N.SAError(f"sa_dist {name}: failed on another rank")
+        if err is not None:
+            raise err
+        return res
+
     def _min_all(self, x: int, dev) -> int:
         if self.G == 1:
             return int(x)
@@ -302,7 +326,7 @@ class DistributedSA:
             return self._fallback(text, n, "n < 2")
         _trace("begin")
         self._mark("begin", dev)
-        info, coarse = self.ops.begin(text, n, G, r, present)
+        info, coarse = self._phase("begin", dev, self.ops.begin, text, n, G, r, present)
         self.stats.update(sigma=info["sigma"], K=info["K"], bucket_bits=info["bucket_bits"])
         if info["status"] != N.DIST_OK:   # identical on every rank (global alphabet and n)
             return self._fallback(text, n, "unsupported alphabet / size")
@@ -311,14 +335,14 @@ class DistributedSA:
             _all_reduce(coarse, group=self.group)
             ch = coarse.cpu()
         _trace("cuts")
-        info = self.ops.cuts(ch)
+        info = self._phase("cuts", dev, self.ops.cuts, ch)
         _trace("cut", info)
         self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
         if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
             return self._fallback(text, n, "unbalanced bucket ranges")
         sa_local = self.ops.empty(info["m"], I32)
         self._mark("round1", dev)
-        info = self.ops.round1(sa_local)
+        info = self._phase("round1", dev, self.ops.round1, sa_local)
         _trace("round1", info)
         if self._min_all(info["round1_ok"], dev) == 0:
             return self._fallback(text, n, "a bucket window exceeds the LDS tile")
@@ -328,7 +352,7 @@ class DistributedSA:
         h = self.stats["K"]
         while True:
             self._mark("requests", dev)
-            counts, info = self.ops.req_count(h, G)
+            counts, info = self._phase("req_count", dev, self.ops.req_count, h, G)
             _trace("req_count", h, counts)
             mat = _all_gather_rows(torch.tensor([info["unsorted"]] + counts, dtype=I64, device=dev), self.group)
             total_u = sum(row[0] for row in mat)
@@ -342,16 +366,16 @@ class DistributedSA:
             # every rank holds the whole count matrix: the slice count of both
             # exchanges needs no extra collective
             slices = max([0] + [(x + XCHUNK - 1) // XCHUNK for row in mat for x in row[1:]])
-            req = self.ops.req_fill(h, sum(counts))
+            req = self._phase("req_fill", dev, self.ops.req_fill, h, sum(counts))
             self._mark("exchange", dev)
             (got,), _ = alltoallv([req], counts, recv_counts, self.group, slices)
             _trace("requests in", got.numel())
             self._mark("answer", dev)
-            ans = self.ops.answer(got)
+            ans = self._phase("answer", dev, self.ops.answer, got)
             self._mark("exchange", dev)
             (back,), _ = alltoallv([ans], recv_counts, counts, self.group, slices)
             self._mark("refine", dev)
-            self.ops.refine(h, back, sa_local)
+            self._phase("refine", dev, self.ops.refine, h, back, sa_local)
             _trace("refined", h)
             self.stats["rounds"] += 1
             h *= 2
@@ -466,10 +490,10 @@ def choose_chars(sigma: int, n: int, limit_bits: int = 63) -> Tuple[int, int]:
 class HipOps:
     """Local per-rank operations on the GPU through libsa_hip's C ABI."""
 
-    def __init__(self, max_n: int, device: int):
+    def __init__(self, max_n: int, device: int, builder=None):
         from .builder import DeviceBuilder
         self.dev = torch.device("cuda", device)
-        self.b = DeviceBuilder(max_n, device=device)
+        self.b = builder if builder is not None else DeviceBuilder(max_n, device=device)
         self.L = N.lib()
 
     def _stream(self):

@@ -220,6 +220,17 @@ int sa_dist_begin(sa_context* ctx, const uint8_t* d_text, uint64_t n, int world,
                   const uint32_t present[8], uint64_t* d_coarse, void* stream, sa_dist_info* info);
 /* h_coarse: the all-reduced coarse histogram on the host (NULL at world 1) */
 int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info);
+/* Frees the range-partitioned build's per-rank buffers of ctx (rank and
+ * member arrays, request buffers); the context stays usable (a fallback
+ * driver reuses its workspace).  Synchronises the device first. */
+int sa_dist_release(sa_context* ctx);
+/* The cut plan sa_dist_cuts applies (host only, no device): world + 1 cuts
+ * into the 4096 coarse buckets of h_coarse (summing to n) at bucket width
+ * bucket_bits; every range holds at most 2^18 buckets.  Returns SA_DIST_OK or
+ * SA_DIST_UNBALANCED (largest range m_max above 1.5x the mean), < 0 on bad
+ * arguments. */
+int sa_dist_plan_cuts(int world, uint64_t n, int bucket_bits, const uint64_t* h_coarse, uint32_t* cuts_out,
+                      uint64_t* m_max);
 /* d_sa_local: info->m uint32 (global text positions, SA order) */
 int sa_dist_round1(sa_context* ctx, uint32_t* d_sa_local, void* stream, sa_dist_info* info, sa_stats* stats);
 /* counts_out: world uint64 -- requests this rank sends to each rank */

@@ -104,6 +104,23 @@ def main():
                 full = [x for x in tot if x >= 0.25 * max(tot)]
                 big[k] = sum(full) / len(full)
         pmc[name] = big
+    # SQ pass (collect.sh, one --pmc run of 8 SQ counters): per kind, the
+    # full-size launches' average of each counter (whole chip, per dispatch)
+    sq = defaultdict(dict)
+    c = find(os.path.join(out, "sq"), "counter_collection.csv")
+    if c:
+        acc = defaultdict(lambda: defaultdict(lambda: defaultdict(float)))
+        with open(c) as f:
+            for row in csv.DictReader(f):
+                k = kind_of(row.get("Kernel_Name", ""))
+                if k:
+                    d = row.get("Dispatch_Id") or row.get("Correlation_Id")
+                    acc[k][row["Counter_Name"]][d] += float(row["Counter_Value"])
+        for k, cv in acc.items():
+            for cname, per_d in cv.items():
+                vals = list(per_d.values())
+                full = [x for x in vals if x >= 0.25 * max(vals)] if max(vals) > 0 else vals
+                sq[k][cname] = sum(full) / len(full)
     fetch, write = pmc["FETCH_SIZE"], pmc["WRITE_SIZE"]
     # calibration: k_alphabet reads exactly n text bytes (16 B per lane)
     read_factor = None
@@ -122,14 +139,22 @@ def main():
         if k in fetch and k in write:
             rf = read_factor if read_factor else 2.0
             e["traffic_bytes_corrected"] = fetch[k] * rf + write[k]
+        if sq.get(k):
+            e["sq"] = dict(sorted(sq[k].items()))
+            if sq[k].get("SQ_INSTS_LDS"):
+                e["sq"]["conflict_cycles_per_lds_inst"] = sq[k].get("SQ_LDS_BANK_CONFLICT", 0.0) / sq[k]["SQ_INSTS_LDS"]
         kernels[k] = e
     bench = None
     bj = os.path.join(out, "bench.json")
     if os.path.exists(bj):
         with open(bj) as f:
             bench = json.loads(f.read())
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from hpc_suffix_array_amd._native import source_hash
     summary = {
         "tag": tag, "n": n, "kind": kind, "args": args,
+        # the sources these counters measured (bench.py matches on it)
+        "src_hash": (bench or {}).get("src_hash") or source_hash(),
         "read_calibration": {"kernel": "alphabet (full-n launch)", "known_read_bytes": n,
                              "factor": read_factor},
         "kernels": kernels,

@@ -108,6 +108,57 @@ def test_sample_sort_gloo(oracle, world):
     _run(oracle, world, driver="sample")
 
 
+def _plan(sa_lib, world, bb, hist):
+    import ctypes
+    h = np.ascontiguousarray(hist, dtype=np.uint64)
+    cuts = np.zeros(world + 1, np.uint32)
+    mmax = ctypes.c_uint64()
+    rc = sa_lib.lib().sa_dist_plan_cuts(world, int(h.sum()), bb, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                        cuts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(mmax))
+    return rc, cuts, int(mmax.value)
+
+
+def test_dist_cut_plan(sa_lib):
+    """sa_dist_plan_cuts (host only): at 19-bit buckets a range holds at most
+    2048 coarse buckets (2^18 local buckets).  A balanced text whose midpoint
+    falls just past coarse bucket 2048 at W = 2 (the 2^31+17 config-4 shape)
+    must be clamped to 2048 | 2048, not planned 2049 | 2047 and reported
+    unbalanced."""
+    hist = np.full(4096, 1000, np.uint64)
+    hist[0], hist[2048] = 0, 2000           # prefix at 2048 just below n / 2
+    rc, cuts, mmax = _plan(sa_lib, 2, 19, hist)
+    assert rc == 0 and list(cuts) == [0, 2048, 4096] and mmax == 2049000
+    # uniform at every world size: equal ranges, contiguous, within the cap
+    for world in (1, 2, 3, 4, 8):
+        for bb in (16, 17, 18, 19):
+            rc, cuts, mmax = _plan(sa_lib, world, bb, np.full(4096, 7, np.uint64))
+            cap = (1 << 18) >> (bb - 12)
+            if world * cap < 4096:   # the ranges cannot cover the buckets (plan_bucketed never asks)
+                assert rc == 2
+                continue
+            assert rc == 0, (world, bb)
+            assert cuts[0] == 0 and cuts[-1] == 4096 and (np.diff(cuts.astype(np.int64)) >= 0).all()
+            assert (np.diff(cuts.astype(np.int64)) <= cap).all()
+            assert mmax <= 7 * (4096 // world + 1)
+    # the nearer boundary: prefix 4999 vs 5001 around n / 2 = 5000 (W = 2)
+    hist = np.zeros(4096, np.uint64)
+    hist[:10] = [1000, 1000, 1000, 1000, 999, 1001, 1000, 1000, 1000, 1000]
+    rc, cuts, mmax = _plan(sa_lib, 2, 16, hist)
+    assert rc == 0 and cuts[1] == 5 and mmax == 5001
+    # one coarse bucket holding most suffixes cannot balance
+    hist = np.ones(4096, np.uint64)
+    hist[7] = 10_000_000
+    rc, cuts, _ = _plan(sa_lib, 4, 16, hist)
+    assert rc == 2
+    # a histogram that does not sum to n is an argument error
+    import ctypes
+    h = np.ones(4096, np.uint64)
+    cuts = np.zeros(3, np.uint32)
+    m = ctypes.c_uint64()
+    assert sa_lib.lib().sa_dist_plan_cuts(2, 5, 16, h.ctypes.data_as(ctypes.POINTER(ctypes.c_uint64)),
+                                          cuts.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), ctypes.byref(m)) < 0
+
+
 def test_choose_chars_keeps_int64_keys():
     from hpc_suffix_array_amd.distributed import choose_chars
     for sigma in (1, 2, 3, 4, 26, 62, 127, 255, 256):

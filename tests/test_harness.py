@@ -90,6 +90,61 @@ def test_cli_and_shim_on_gpu(gpu, oracle, tmp_path):
     assert list(df.columns) == B.CSV_COLUMNS and len(df) == 3
 
 
+@pytest.mark.gpu
+def test_config1_random_1mb_through_the_harness(gpu, oracle, tmp_path):
+    """configs[0]: scripts/benchmark_sequential.py on the generated 1 MiB
+    random file (test_data/large/random_1MB.txt of generate_large_datasets.py)
+    through the shim and the CLI, LRS and SA pinned by SURVEY.md 8(c)."""
+    import benchmark_sequential as B
+    import generate_large_datasets as G
+    from hpc_suffix_array_amd import SuffixArray
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tools")], check=True)
+    G.main(["--sizes", "1", "--out", str(tmp_path)])
+    f = str(tmp_path / "large" / "random_1MB.txt")
+    for cli in (False, True):
+        r = B.run_benchmark(f, use_cli=cli)
+        assert r["success"], r["error"]
+        assert (r["lrs_string"], r["lrs_length"]) == ("E31tuV", 6)
+        assert r["suffix_array_length"] == 1 << 20 and "Valid suffix array: YES" in r["output"]
+    out = tmp_path / "res.csv"
+    assert B.main(["--files", f, "--out", str(out)]) == 0
+    with SuffixArray(open(f, "rb").read()) as s:   # the drop-in symbols the shim calls
+        s.build()
+        assert oracle.sha256(s.sa.astype(np.int32)) == \
+            "327c4c99ad49e1ae66133ef0558e0ef6b91174715ba6c02dc5f50deeec63fa56"
+
+
+def test_bench_picks_the_profile_of_the_current_sources(tmp_path):
+    """bench.py's roofline.traffic comes from the rocprof summary of this
+    workload stamped with the current sources' hash; tags order by round and
+    version (r02_bb after r02_o, r01_v30 after r01_v9), never lexically."""
+    import json
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.tag_order("r02_bb") > bench.tag_order("r02_o") > bench.tag_order("r02_a")
+    assert bench.tag_order("r01_v30") > bench.tag_order("r01_v9")
+    assert bench.tag_order("r03_a") > bench.tag_order("r02_bb")
+
+    def put(tag, **kw):
+        s = dict(tag=tag, n=1 << 30, kind="dna", args=[], traffic_bytes_per_launch={"local_sort": 1.0})
+        s.update(kw)
+        (tmp_path / f"{tag}_summary.json").write_text(json.dumps(s))
+    put("r02_o", src_hash="old")
+    put("r02_bb", src_hash="head")
+    put("r02_bc", src_hash="old2")
+    put("r02_bd", src_hash="head", args=["--round1", "lsd"])   # another configuration: never used
+    put("r02_be", src_hash="head", n=1 << 26)
+    s = bench.pmc_summary(1 << 30, "dna", "head", str(tmp_path))
+    assert s["tag"] == "r02_bb" and not s["stale"]
+    s = bench.pmc_summary(1 << 30, "dna", "new", str(tmp_path))
+    assert s["tag"] == "r02_bc" and s["stale"]
+    assert bench.pmc_summary(1 << 30, "dna", "head", str(tmp_path)) is not None
+    assert bench.pmc_summary(1 << 29, "dna", "head", str(tmp_path)) is None
+    # the committed profiles: the latest default-workload summary is picked
+    s = bench.pmc_summary(1 << 30, "dna", bench.SRC_HASH)
+    assert s is not None and s["tag"] != "r02_o"
+
+
 def test_scaling_harness_columns_and_commands():
     """scripts/benchmark_scaling.py: the mpi_results.csv columns of the
     reference's sweep (benchmark_mpi.py:180-210) from bench.py JSON lines, and
