@@ -147,8 +147,7 @@ int main(int argc, char** argv) {
                                (const uint32_t*)base, states, tick, epoch, k1, v1, err);
         };
     };
-    report("onesweep_1024x4", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 4, 0>, 1024, 4096), reps));
-    report("onesweep_1024x4_nolookback", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 4, 1>, 1024, 4096), reps));
+    report("onesweep_1024x4", T.ms(onesweep(k_onesweep<SrcKeys, 1024, 4>, 1024, 4096), reps));
     // the onesweep output is the reference the chunked variants are compared with
     uint64_t* kref;
     uint32_t* vref;

@@ -1,7 +1,7 @@
 // microbench_bucket.hip -- the bucketed first round's local sort in
 // isolation: n synthetic key1-like keys already in bucket order (bucket =
 // top 16 bits, rising with the position; low bits random), the window
-// kernels of sa_bucket.h, then k_bucket_sort variants against a streaming
+// kernels of sa_bucket.h, then k_bucket_sort against a streaming
 // copy of the same 12 bytes per suffix in and out.  Not part of libsa_hip.
 //   build: make -C hpc_suffix_array_amd/csrc microbench_bucket
 //   run:   hpc_suffix_array_amd/csrc/build/microbench_bucket [log2 n] [reps]
@@ -15,6 +15,21 @@
 #include "sa_bucket.h"
 
 using namespace sa;
+
+// per-phase clock64() spans of each workgroup's thread 0 (k_bucket_sort's
+// Probe hook), summed into words[32 ..] as 7 u64
+struct ClockProbe {
+    uint64_t acc[7] = {0, 0, 0, 0, 0, 0, 0}, last = 0;
+    __device__ __forceinline__ void mark(int k) {
+        const uint64_t now = clock64();
+        if (k >= 0) acc[k] += now - last;
+        last = now;
+    }
+    __device__ __forceinline__ void flush(uint32_t* words) {
+        if (threadIdx.x == 0)
+            for (int k = 0; k < 7; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(words + 32) + k, acc[k]);
+    }
+};
 
 #define CK(x)                                                                                 \
     do {                                                                                      \
@@ -126,47 +141,24 @@ int main(int argc, char** argv) {
     timeit("copy 12 B in + out (old item size)", [&] {
         hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
     });
-    for (uint32_t g : {512u}) {
+    for (uint32_t g : {512u, hw[7]}) {
         char nm[64];
         std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
         timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, SegOut{});
         });
         std::snprintf(nm, sizeof nm, "bucket_sort + segments grid %u", g);
         timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(g), dim3(kBsBlock), 0, 0,
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, so);
-        });
-        std::snprintf(nm, sizeof nm, "bucket_sort no-sort grid %u", g);
-        timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 1>), dim3(g), dim3(kBsBlock), 0, 0,
-                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
-                               words, ib, okeys, ovals, skew, SegOut{});
-        });
-    }
-    for (uint32_t g : {512u, hw[7]}) {
-        char nm[64];
-        std::snprintf(nm, sizeof nm, "bucket_sort_cls + seg grid %u", g);
-        timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort_cls<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
-                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys,
-                               ovals, skew, so);
-        });
-    }
-    for (uint32_t g : {512u, 1024u, hw[7]}) {
-        char nm[64];
-        std::snprintf(nm, sizeof nm, "bucket_sort 512x18 + seg grid %u", g);
-        timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<512, 18, 0>), dim3(g), dim3(512), 0, 0, (const uint64_t*)items, br,
-                               (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
         });
     }
     {   // per-phase clock64 spans of one workgroup's thread 0, per window
         CK(hipMemset(words + 32, 0, 64));
-        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 2>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
+        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, ClockProbe>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
                            br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
         CK(hipDeviceSynchronize());
         unsigned long long t[7];
@@ -181,7 +173,7 @@ int main(int argc, char** argv) {
     std::printf("flags=%u skewed=%u heads=%u unsorted=%u groups=%u (accumulated over runs)\n", hw[6], hw[10], hw[0], hw[1], hw[2]);
     // check: output sorted within each window, keys monotone overall
     std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
-    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, 0>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
                        br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
     CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
     size_t bad = 0;

@@ -54,28 +54,6 @@ namespace sa {
 #define SA_BS_BLOCK 512
 #endif
 constexpr int kBsBlock = SA_BS_BLOCK;
-// 1: single-bucket windows load without rebuilding key1, group counts of a
-// sorted sub-bucket from an equal-neighbour bit mask (0: the v31 code, A/B)
-#ifndef SA_LS_FAST
-#define SA_LS_FAST 1
-#endif
-// 1: each thread sorts its sub-buckets largest first, 8-input networks where
-// no lane of the wave has more than 8 (A/B)
-#ifndef SA_LS_STORE_NOWAIT
-#define SA_LS_STORE_NOWAIT 1
-#endif
-#ifndef SA_LS_FIXED_SPAN
-#define SA_LS_FIXED_SPAN 1
-#endif
-#ifndef SA_LS_UG_TMP
-#define SA_LS_UG_TMP 1
-#endif
-#ifndef SA_LS_CLASSES
-#define SA_LS_CLASSES 1
-#endif
-#ifndef SA_LS_ORDER
-#define SA_LS_ORDER 1
-#endif
 #ifndef SA_BS_ITEMS
 #define SA_BS_ITEMS 18
 #endif
@@ -564,7 +542,7 @@ struct BucketRel {
     const uint32_t* __restrict__ bstart;
     const uint32_t* __restrict__ bdmin;
     uint32_t rb;
-    // SA_LS_FIXED_SPAN: bit width of the largest bucket-relative key of one
+    // bit width of the largest bucket-relative key of one
     // bucket (0: measure each window's span)
     uint32_t bits1 = 0;
 };
@@ -617,8 +595,6 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
     };
     uint64_t mx = 0;
     mn = ~0ull;
-#if SA_LS_FAST
-#if SA_LS_FIXED_SPAN
     if (nbk == 1 && br.bits1) {
         // one bucket whose keys fill the plan's span (the compact layout):
         // the items are w already, the sub-buckets split the whole span --
@@ -638,7 +614,6 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
         __syncthreads();
         return true;
     }
-#endif
     if (nbk == 1) {
         // one bucket (the common case from 2^29 suffixes): the items are
         // (key1 - Dmin) << ib | idx already, so w = item - (min's key part
@@ -676,7 +651,6 @@ __device__ __forceinline__ bool load_window(const uint64_t* __restrict__ w_in, c
         mn = ((uint64_t)dmin0 << br.rb) + mrel;
         return true;
     }
-#endif
     uint32_t v[ITEMS];
     // unpredicated loads (slots past m re-read the last suffix: no per-item
     // exec masks, which cost SGPRs and spills at 128 VGPRs); later phases
@@ -1052,10 +1026,16 @@ __device__ __forceinline__ void sort_sub_lds(uint64_t* __restrict__ s_w, uint32_
     }
 }
 
-// kVariant (microbenchmarks only; 0 in the product): 1 skips the sort (the
-// loaded window is written back in input order); 2 accumulates per-phase
-// clock64() spans of thread 0 into words[16..23] (words must hold 24 u64)
-template <int BLOCK, int ITEMS, int kVariant = 0>
+// Instrumentation hook of k_bucket_sort: mark(k) at the end of phase k (0
+// load, 1 histogram, 2 scan, 3 scatter, 4 sub-bucket sort, 5 U scan, 6 store;
+// -1 = window start), flush(words) once per workgroup.  The library uses
+// NoProbe (compiled away); microbench_bucket.hip passes a clock64() probe.
+struct NoProbe {
+    __device__ __forceinline__ void mark(int) {}
+    __device__ __forceinline__ void flush(uint32_t*) {}
+};
+
+template <int BLOCK, int ITEMS, class Probe = NoProbe>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in, BucketRel br,
                                                        const uint32_t* __restrict__ ws,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
@@ -1082,16 +1062,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
     static_assert(WAVES * ITEMS * 8 <= kSubBuckets * 2, "per-row segment values fit in s_cnt");
     uint64_t th = 0, tu = 0, tg = 0;
-    uint64_t tacc[7] = {0, 0, 0, 0, 0, 0, 0}, tlast = 0;
-    auto stamp = [&](int k) {
-        if constexpr ((kVariant & 2) != 0) {
-            const uint64_t now = clock64();
-            if (k >= 0) tacc[k] += now - tlast;
-            tlast = now;
-        }
-    };
+    Probe probe;
     for (uint32_t q = blockIdx.x; q < nlist; q += gridDim.x) {
-        stamp(-1);
+        probe.mark(-1);
         const uint32_t j = list[q];
         const uint64_t a = ws[j];
         const uint32_t m = (uint32_t)(ws[j + 1] - a);
@@ -1108,17 +1081,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             __syncthreads();
             continue;
         }
-        stamp(0);
+        probe.mark(0);
         uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
-        if constexpr ((kVariant & 1) != 0) {
-#pragma unroll
-            for (int i = 0; i < ITEMS; ++i)
-                if (wave * WT + i * kWave + lane < m) s_w[wave * WT + i * kWave + lane] = w[i];
-            __syncthreads();
-            store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
-            __syncthreads();
-            continue;
-        }
         // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
 #pragma unroll
         for (int i = 0; i < ITEMS; ++i) {
@@ -1128,7 +1092,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             }
         }
         __syncthreads();
-        stamp(1);
+        probe.mark(1);
         // exclusive scan of the counts (2 WPT per thread, 16 bits each) and
         // their maximum
         uint32_t big = 0;
@@ -1169,7 +1133,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             }
         }
         __syncthreads();
-        stamp(2);
+        probe.mark(2);
         if (big > kMaxSub) {   // uniform: clustered keys
             // a fixed-span window goes to the retry launch (its measured span
             // may spread the keys), else to the LSD kernel
@@ -1190,7 +1154,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             }
         }
         __syncthreads();
-        stamp(3);
+        probe.mark(3);
         // ... then each thread sorts its 2 WPT consecutive sub-buckets: up to
         // kNet suffixes in registers (Batcher network), larger ones by
         // insertion in LDS.  Equal keys share a sub-bucket, so the sorted
@@ -1201,7 +1165,6 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         const uint32_t sb0 = 2 * WPT * dg;
         const uint32_t low_bits = bits > (uint32_t)kSubBits ? bits - kSubBits : bits;
         const uint32_t low_mask = low_bits >= 32 ? ~0u : ((1u << low_bits) - 1u);
-#if SA_LS_ORDER
         // the thread's four sub-buckets largest first: one of Poisson(~4.5)
         // sizes in 64 lanes exceeds 8 in most waves, but the second largest
         // of four rarely does, so iterations 2-4 mostly run the 8-input
@@ -1224,39 +1187,21 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             const uint32_t sb = sb0 + ((order >> (2 * i)) & 3u);
             const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
             const bool wide = __ballot(cnt > 8u) != 0ull;   // uniform
-#if SA_LS_CLASSES
             // network sizes 4 / 8 / 12 / 16 by the wave's largest sub-bucket
             // of this rank (the largest of four is > 8 in almost every wave
             // but > 12 in about a fifth; the smallest is <= 4 in a third)
             const bool wide4 = __ballot(cnt > 4u) != 0ull, wide12 = __ballot(cnt > 12u) != 0ull;
-#endif
             if (cnt == 0) continue;
             const uint32_t nu0 = nu;
-#if SA_LS_CLASSES
             if (!wide4 && low_bits <= 28) sort_sub<4>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else if (!wide12 && low_bits <= 28) sort_sub<12>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else
-#else
-            if (!wide && low_bits <= 28) sort_sub<8>(s_w, lo, cnt, ib, low_mask, nu, ng);
-            else
-#endif
             if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
             else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
             if (nu != nu0) umask |= 1u << (sb - sb0);
         }
-#else
-#pragma unroll 1
-        for (uint32_t sb = sb0; sb < sb0 + 2 * WPT; ++sb) {
-            const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
-            if (cnt == 0) continue;
-            const uint32_t nu0 = nu;
-            if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub<kNet>(s_w, lo, cnt, ib, low_mask, nu, ng);
-            else sort_sub_lds(s_w, lo, hi, ib, nu, ng);
-            if (nu != nu0) umask |= 1u << (sb - sb0);
-        }
-#endif
-        stamp(4);
+        probe.mark(4);
         // exclusive U / U-group offsets of this thread's sub-buckets in the
         // window, and the window totals
         uint32_t bu, bg, th_w, tu_w, tg_w;
@@ -1264,13 +1209,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // nu, ng < 2^16 (a window holds <= kBsCap suffixes): one scan of
             // both; heads = singletons + U groups = m - U + G
             const uint32_t iug = wave_inclusive_sum(nu | (ng << 16));
-#if SA_LS_UG_TMP
             // its own LDS words: no barrier for the reads of the count scan's s_tmp
             uint32_t* const s_ug = s_tmp2;
-#else
-            uint32_t* const s_ug = s_tmp;
-            __syncthreads();   // s_red / s_tmp reads of the scan above are done
-#endif
             if (lane == kWave - 1) s_ug[wave] = iug;
             __syncthreads();
             uint32_t oug = 0, tug = 0;
@@ -1325,329 +1265,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 }
             }
         }
-#if !SA_LS_STORE_NOWAIT
-        __syncthreads();
-#endif
-        // (SA_LS_STORE_NOWAIT: the U/G scan's barrier already follows every
+        // (the U/G scan's barrier already follows every
         // thread's sort; the unsorted-set writes and the store only read s_w,
         // so the store need not wait for the few threads walking groups)
-        stamp(5);
+        probe.mark(5);
         store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
         __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
-        stamp(6);
+        probe.mark(6);
     }
-    if constexpr ((kVariant & 2) != 0) {
-        if (threadIdx.x == 0)
-            for (int k = 0; k < 7; ++k) atomicAdd(reinterpret_cast<unsigned long long*>(words + 32) + k, tacc[k]);
-    }
-    flush_totals(words, th, tu, tg);
-}
-
-// ---------------------------------------------------------------------------
-// k_bucket_sort_cls: the same local sort with the sub-buckets sorted by SIZE
-// CLASS.  After the counting scatter a window's 2048 sub-buckets hold ~4
-// suffixes each (random text: 63 % at most 4, 4 % over 8); the per-thread
-// 16-input networks of k_bucket_sort spent 63 compare-exchanges on each.
-// Here the sub-buckets are listed by class (2, 3-4, 5-8, 9-16, larger) in the
-// free tail of the LDS tile and every class is sorted with its own network
-// size, one sub-bucket per thread, so a wave runs one network shape.  Heads
-// and the unsorted set then come from row ballots over the sorted tile
-// (window_segments, as the skewed-window kernel), not from per-thread
-// counting in the network phase.  Windows too full for the lists (m > CAP -
-// 512) sort their sub-buckets per thread with the 16-input network.
-// ---------------------------------------------------------------------------
-template <int N>
-__device__ __forceinline__ void sort_sub32(uint64_t* __restrict__ s_w, uint32_t lo, uint32_t cnt, uint32_t ib,
-                                           uint32_t low_mask) {
-    // u32 sort keys: the key bits below the sub-bucket's (exact: equal <=>
-    // same group) over the slot in the sub-bucket (4 bits: cnt <= 16)
-    uint32_t v[N];
-#pragma unroll
-    for (int t = 0; t < N; ++t)
-        v[t] = (uint32_t)t < cnt ? (((uint32_t)(s_w[lo + t] >> ib) & low_mask) << 4) | (uint32_t)t : ~0u;
-    sort_net32<N>(v);
-    uint64_t x[N];
-#pragma unroll
-    for (int t = 0; t < N; ++t) x[t] = (uint32_t)t < cnt ? s_w[lo + (v[t] & 15u)] : 0ull;
-#pragma unroll
-    for (int t = 0; t < N; ++t)
-        if ((uint32_t)t < cnt) s_w[lo + t] = x[t];
-}
-
-__device__ __forceinline__ void sort_sub_insertion(uint64_t* __restrict__ s_w, uint32_t lo, uint32_t hi) {
-    for (uint32_t k = lo + 1; k < hi; ++k) {
-        const uint64_t x = s_w[k];
-        uint32_t y = k;
-        while (y > lo && s_w[y - 1] > x) {
-            s_w[y] = s_w[y - 1];
-            --y;
-        }
-        s_w[y] = x;
-    }
-}
-
-template <int BLOCK, int ITEMS>
-__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort_cls(const uint64_t* __restrict__ keys_in, BucketRel br,
-                                                           const uint32_t* __restrict__ ws,
-                                                           const uint32_t* __restrict__ list,
-                                                           uint32_t* __restrict__ words, uint32_t ib,
-                                                           uint64_t* __restrict__ keys_out,
-                                                           uint32_t* __restrict__ sa_out, uint32_t* __restrict__ skew,
-                                                           SegOut so) {
-    constexpr int WAVES = BLOCK / kWave;
-    constexpr int CAP = BLOCK * ITEMS;
-    constexpr int WT = kWave * ITEMS;
-    constexpr int kClasses = 5;                       // 2, 3-4, 5-8, 9-16, larger
-    constexpr int kListSlots = kSubBuckets / 4;       // u64 slots of the u16 list (512)
-    __shared__ uint64_t s_w[CAP];
-    __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; later per-row scratch
-    __shared__ uint32_t s_tmp[WAVES];
-    __shared__ uint64_t s_red[2][WAVES];
-    __shared__ uint32_t s_bk[2][32];
-    __shared__ uint32_t s_cls[2 * kClasses];      // class totals, then bases
-    constexpr int WPT = kSubBuckets / 2 / BLOCK;
-    static_assert(WPT >= 1 && WPT * 2 * BLOCK == kSubBuckets, "whole counter words per thread");
-    static_assert(WAVES * ITEMS * 8 <= kSubBuckets * 2, "per-row segment values fit in s_cnt");
-
-    const uint32_t wave = wave_id(), lane = lane_id();
-    const uint32_t dg = threadIdx.x;
-    uint32_t* err = words + 6;
-    const uint32_t nlist = words[7];
-    auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
-    uint64_t th = 0, tu = 0, tg = 0;
-    for (uint32_t q = blockIdx.x; q < nlist; q += gridDim.x) {
-        const uint32_t j = list[q];
-        const uint64_t a = ws[j];
-        const uint32_t m = (uint32_t)(ws[j + 1] - a);
-        if (m > (uint32_t)CAP) {
-            if (threadIdx.x == 0) atomicOr(err, 1u);
-            continue;
-        }
-        for (int i = threadIdx.x; i < kSubBuckets / 2; i += BLOCK) s_cnt[i] = 0;
-        if (threadIdx.x < 2 * kClasses) s_cls[threadIdx.x] = 0;
-        uint64_t w[ITEMS];
-        uint64_t mn;
-        uint32_t bits;
-        if (!load_window<BLOCK, ITEMS>(keys_in, br, j, a, m, ib, w, mn, bits, s_red, s_bk, err)) {
-            __syncthreads();
-            continue;
-        }
-        const uint32_t dsh = ib + (bits > (uint32_t)kSubBits ? bits - kSubBits : 0u);
-        // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            if (wave * WT + i * kWave + lane < m) {
-                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
-            }
-        }
-        __syncthreads();
-        // exclusive scan of the counts and their maximum
-        uint32_t big = 0;
-        uint32_t c[2 * WPT];
-        {
-            uint32_t sum = 0, cm = 0;
-#pragma unroll
-            for (int x = 0; x < WPT; ++x) {
-                const uint32_t pw = s_cnt[WPT * dg + x];
-                c[2 * x] = pw & 0xFFFFu;
-                c[2 * x + 1] = pw >> 16;
-            }
-#pragma unroll
-            for (int x = 0; x < 2 * WPT; ++x) {
-                sum += c[x];
-                cm = c[x] > cm ? c[x] : cm;
-            }
-            const uint32_t inc = wave_inclusive_sum(sum);
-#pragma unroll
-            for (int o = kWave / 2; o > 0; o >>= 1) {
-                const uint32_t y = __shfl_xor(cm, o, kWave);
-                cm = y > cm ? y : cm;
-            }
-            if (lane == kWave - 1) s_tmp[wave] = inc;
-            if (lane == 0) s_red[0][wave] = cm;
-            __syncthreads();
-            uint32_t off = 0;
-#pragma unroll
-            for (int x = 0; x < WAVES; ++x) {
-                off += (x < (int)wave) ? s_tmp[x] : 0u;
-                big = (uint32_t)s_red[0][x] > big ? (uint32_t)s_red[0][x] : big;
-            }
-            uint32_t b = off + inc - sum;
-#pragma unroll
-            for (int x = 0; x < WPT; ++x) {
-                const uint32_t b0 = b, b1 = b + c[2 * x];
-                s_cnt[WPT * dg + x] = b0 | (b1 << 16);
-                b = b1 + c[2 * x + 1];
-            }
-        }
-        __syncthreads();
-        if (big > kMaxSub) {   // uniform: clustered keys, leave the window to the LSD kernel
-            if (threadIdx.x == 0) skew[atomicAdd(&words[10], 1u)] = j;
-            __syncthreads();
-            continue;
-        }
-        // 2. scatter into sub-buckets (any order inside one)
-#pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            if (wave * WT + i * kWave + lane < m) {
-                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
-                s_w[(old >> (16 * (sb & 1))) & 0xFFFFu] = w[i];
-            }
-        }
-        // (s_cnt now holds the sub-bucket ends)
-        const uint32_t low_bits = bits > (uint32_t)kSubBits ? bits - kSubBits : bits;
-        const uint32_t low_mask = low_bits >= 32 ? ~0u : ((1u << low_bits) - 1u);
-        const uint32_t sb0 = 2 * WPT * dg;
-        const bool lists = m + kListSlots <= (uint32_t)CAP && low_bits <= 28;   // uniform
-        if (lists) {
-            // 3a. class of each of this thread's sub-buckets; per-wave class
-            // counts (ballots), one LDS atomic per class per wave
-            int cls[2 * WPT];
-#pragma unroll
-            for (int x = 0; x < 2 * WPT; ++x)
-                cls[x] = c[x] <= 1 ? -1 : c[x] <= 2 ? 0 : c[x] <= 4 ? 1 : c[x] <= 8 ? 2 : c[x] <= 16 ? 3 : 4;
-            uint32_t rnk[2 * WPT];
-            uint32_t wbase[kClasses];
-#pragma unroll
-            for (int k = 0; k < kClasses; ++k) {
-                uint32_t run = 0;
-#pragma unroll
-                for (int x = 0; x < 2 * WPT; ++x) {
-                    const uint64_t bal = __ballot(cls[x] == k);
-                    if (cls[x] == k) rnk[x] = run + (uint32_t)__popcll(bal & lanemask_lt());
-                    run += (uint32_t)__popcll(bal);
-                }
-                wbase[k] = 0;
-                if (lane == 0 && run) wbase[k] = atomicAdd(&s_cls[k], run);
-                wbase[k] = (uint32_t)__shfl((int)wbase[k], 0, kWave);
-            }
-            __syncthreads();   // class totals complete (and the scatter above)
-            uint32_t cbase[kClasses], ctot[kClasses];
-            {
-                uint32_t acc = 0;
-#pragma unroll
-                for (int k = kClasses - 1; k >= 0; --k) {   // largest class first in the list
-                    ctot[k] = s_cls[k];
-                    cbase[k] = acc;
-                    acc += ctot[k];
-                }
-            }
-            uint16_t* lst = reinterpret_cast<uint16_t*>(s_w + (CAP - kListSlots));
-#pragma unroll
-            for (int x = 0; x < 2 * WPT; ++x)
-                if (cls[x] >= 0) lst[cbase[cls[x]] + wbase[cls[x]] + rnk[x]] = (uint16_t)(sb0 + x);
-            __syncthreads();
-            // 3b. each class with its network size, one sub-bucket per thread
-#pragma unroll
-            for (int k = kClasses - 1; k >= 0; --k) {
-                for (uint32_t i = dg; i < ctot[k]; i += BLOCK) {
-                    const uint32_t sb = lst[cbase[k] + i];
-                    const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
-                    if (k == 0) sort_sub32<2>(s_w, lo, cnt, ib, low_mask);
-                    else if (k == 1) sort_sub32<4>(s_w, lo, cnt, ib, low_mask);
-                    else if (k == 2) sort_sub32<8>(s_w, lo, cnt, ib, low_mask);
-                    else if (k == 3) sort_sub32<16>(s_w, lo, cnt, ib, low_mask);
-                    else sort_sub_insertion(s_w, lo, hi);
-                }
-            }
-        } else {
-            __syncthreads();
-#pragma unroll 1
-            for (uint32_t sb = sb0; sb < sb0 + 2 * WPT; ++sb) {
-                const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
-                if (cnt <= 1) continue;
-                if (cnt <= (uint32_t)kNet && low_bits <= 28) sort_sub32<kNet>(s_w, lo, cnt, ib, low_mask);
-                else sort_sub_insertion(s_w, lo, hi);
-            }
-        }
-        __syncthreads();
-        // 4. each thread counts the heads, unsorted members (groups of two or
-        // more) and unsorted heads of its own sub-buckets, in SA order
-        uint32_t nh = 0, nu = 0, ng = 0;
-        {
-            const uint32_t lo0 = sb0 ? end_of(sb0 - 1) : 0u, hi0 = end_of(sb0 + 2 * WPT - 1);
-            uint64_t pr = ~0ull, cur = lo0 < hi0 ? (s_w[lo0] >> ib) : 0ull;
-            uint32_t sbe = end_of(sb0);   // end of the sub-bucket holding k (groups never cross one)
-            uint32_t sbi = sb0;
-            for (uint32_t k = lo0; k < hi0; ++k) {
-                if (k >= sbe) {
-                    while (k >= sbe) sbe = end_of(++sbi);
-                    pr = ~0ull;
-                    cur = s_w[k] >> ib;
-                }
-                const uint64_t nx = k + 1 < sbe ? (s_w[k + 1] >> ib) : ~0ull;
-                const bool eqp = pr == cur, eqn = nx == cur;
-                nh += eqp ? 0u : 1u;
-                nu += (eqp || eqn) ? 1u : 0u;
-                ng += (!eqp && eqn) ? 1u : 0u;
-                pr = cur;
-                cur = nx;
-            }
-        }
-        // exclusive U / U-group offsets of this thread's sub-buckets in the
-        // window, and the window totals (as k_bucket_sort)
-        uint32_t bu, bg, th_w, tu_w, tg_w;
-        {
-            const uint32_t iu = wave_inclusive_sum(nu), ig = wave_inclusive_sum(ng), ih = wave_inclusive_sum(nh);
-            if (lane == kWave - 1) {
-                s_tmp[wave] = iu;
-                s_red[0][wave] = (uint64_t)ig | ((uint64_t)ih << 32);
-            }
-            __syncthreads();
-            uint32_t ou = 0, og = 0;
-            th_w = tu_w = tg_w = 0;
-#pragma unroll
-            for (int x = 0; x < WAVES; ++x) {
-                const uint32_t xu = s_tmp[x], xg = (uint32_t)s_red[0][x], xh = (uint32_t)(s_red[0][x] >> 32);
-                if (x < (int)wave) {
-                    ou += xu;
-                    og += xg;
-                }
-                tu_w += xu;
-                tg_w += xg;
-                th_w += xh;
-            }
-            bu = ou + iu - nu;
-            bg = og + ig - ng;
-        }
-        if (so.rank) {
-            if (threadIdx.x == 0) {
-                so.cnt_u[j] = tu_w;
-                so.cnt_g[j] = tg_w;
-                th += th_w;
-                tu += tu_w;
-                tg += tg_w;
-            }
-            if (nu) {   // the unsorted members (rare): rank, member bit, (p, x, group)
-                const uint64_t imask = (ib >= 64) ? ~0ull : ((1ull << ib) - 1ull);
-                const uint32_t lo0 = sb0 ? end_of(sb0 - 1) : 0u, hi0 = end_of(sb0 + 2 * WPT - 1);
-                uint32_t head = lo0, ku = bu, kg = bg;
-                uint64_t pr = ~0ull;
-                for (uint32_t k = lo0; k < hi0; ++k) {
-                    const uint64_t x = s_w[k], r = x >> ib;
-                    const uint64_t nx = k + 1 < hi0 ? (s_w[k + 1] >> ib) : ~0ull;
-                    const bool eqp = k > lo0 && pr == r, eqn = k + 1 < hi0 && nx == r;
-                    if (!eqp) head = k;
-                    if (!eqp && eqn) ++kg;
-                    if (eqp || eqn) {
-                        const uint32_t xi = (uint32_t)(x & imask);
-                        so.rank[xi] = (uint32_t)(so.rank_off + a + head + 1u);
-                        atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
-                        so.tmp_pos[a + ku] = (uint32_t)(a + k);
-                        so.tmp_idx[a + ku] = xi;
-                        so.tmp_g[a + ku] = kg - 1u;
-                        ++ku;
-                    }
-                    pr = r;
-                }
-            }
-        }
-        __syncthreads();
-        store_window<BLOCK, ITEMS>(s_w, a, m, ib, mn, keys_out, sa_out, so.ksh);
-        __syncthreads();   // s_w / s_cnt / s_red reuse by the next window
-    }
+    probe.flush(words);
     flush_totals(words, th, tu, tg);
 }
 

@@ -352,7 +352,7 @@ static void onesweep_pass(sa_context* c, const Src& src, uint64_t n, uint32_t sh
     // 1024 x 4: 16 waves per tile, 2 workgroups (32 waves) per CU -- the
     // fastest shape in microbench.hip (r01: 10.4 ms per 2^30-pair pass)
     static_assert(kOsBlock * kOsItems == kTile, "tile states are sized for kTile");
-    hipLaunchKernelGGL((k_onesweep<Src, kOsBlock, kOsItems, 0, RBITS>), dim3((uint32_t)tiles), dim3(kOsBlock), 0, s, src,
+    hipLaunchKernelGGL((k_onesweep<Src, kOsBlock, kOsItems, RBITS>), dim3((uint32_t)tiles), dim3(kOsBlock), 0, s, src,
                        n, shift, nbits, base, c->states, ticket, epoch, out_keys, out_vals, c->words + 4);
 }
 

@@ -754,13 +754,9 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
 // Presence is all the dense codes need; it is kept in 8 registers per lane
 // (no LDS atomics, so a 4-symbol text costs no bank conflicts), OR-reduced
 // over the wave, one atomicOr per word per wave.
-// SA_ALPHA_FAST: 16-byte chunks inside one 32-symbol block take one LDS
-// atomic instead of 16 -- measured equal at 1 GiB DNA (0.274-0.289 ms either
-// way, profiles/r02_bd_ab_alpha_fast.txt): the kernel is not bound by its LDS
-// atomics, so the simpler path stays the default
-#ifndef SA_ALPHA_FAST
-#define SA_ALPHA_FAST 0
-#endif
+// (one LDS atomic per 16-byte chunk inside one 32-symbol block instead of 16
+// measured equal at 1 GiB DNA, profiles/r02_bd_ab_alpha_fast.txt: the kernel
+// is not bound by its LDS atomics)
 __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__ text, uint64_t n,
                                                      uint32_t* __restrict__ present) {
     // a private 256-bit mask per lane in LDS, set by one atomic OR per byte
@@ -776,21 +772,6 @@ __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__
         if (i + 16 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
             const uint4 v = *reinterpret_cast<const uint4*>(text + i);
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
-#if SA_ALPHA_FAST
-            // all 16 bytes in one 32-symbol block of the byte range (DNA,
-            // upper-case text): their bits OR'd in registers, one LDS atomic
-            const uint32_t h = (w4[0] & 0xE0u) * 0x01010101u;
-            if (((w4[0] & 0xE0E0E0E0u) == h) & ((w4[1] & 0xE0E0E0E0u) == h) &
-                ((w4[2] & 0xE0E0E0E0u) == h) & ((w4[3] & 0xE0E0E0E0u) == h)) {
-                uint32_t bits = 0;
-#pragma unroll
-                for (int q = 0; q < 4; ++q)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) bits |= 1u << ((w4[q] >> (8 * b)) & 31u);
-                atomicOr(&m[(w4[0] >> 5) & 7u], bits);
-                continue;
-            }
-#endif
 #pragma unroll
             for (int q = 0; q < 4; ++q)
 #pragma unroll

@@ -121,12 +121,9 @@ __global__ __launch_bounds__(kBlock) void k_digit_base(const uint32_t* __restric
     base[p * kRadix + threadIdx.x] = block_exclusive_sum(ghist[p * kRadix + threadIdx.x], s_tmp, nullptr);
 }
 
-// kVariant (microbenchmarks only; 0 in the product): bit 0 skips the look-back
-// (tile offsets faked), bit 1 skips the ranking (identity layout), bit 2
-// skips the LDS staging (writes straight from registers).
 // RBITS: digit width (8, or 9 for the bucketed first round's high pass);
 // digit_base and states are laid out with 1 << RBITS entries per tile.
-template <class Src, int BLOCK, int ITEMS, int kVariant = 0, int RBITS = 8>
+template <class Src, int BLOCK, int ITEMS, int RBITS = 8>
 __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
                                                     const uint32_t* __restrict__ digit_base,
                                                     uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
@@ -151,14 +148,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     const uint32_t mask = (1u << nbits) - 1u;
     if (threadIdx.x == 0) {
         uint32_t tk = atomicAdd(ticket, 1u);
-        if constexpr ((kVariant & 8) != 0) {
-            // microbenchmark only: consecutive tiles on one XCD (blocks are
-            // dealt round-robin over the 8 XCDs); unsafe with the look-back
-            const uint32_t tiles = (uint32_t)((n + TILE - 1) / TILE);
-            const uint32_t g = tk / 64, j = tk % 64;
-            const uint32_t cand = g * 64 + (j % 8) * 8 + j / 8;
-            tk = cand < tiles ? cand : tk;
-        }
         s_tile = tk;
     }
     for (int i = threadIdx.x; i < WAVES * RADIX; i += BLOCK) (&s_wcnt[0][0])[i] = 0;
@@ -180,7 +169,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     }
     uint32_t r[ITEMS];
     uint16_t* wc = s_wcnt[wave];
-    if constexpr ((kVariant & 2) == 0) {
+    {
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const bool ok = d[j] < (uint32_t)RADIX;
@@ -196,9 +185,6 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
             r[j] = cnt + below;
             if (ok && below == 0) wc[d[j]] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
         }
-    } else {
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) r[j] = j * kWave + lane;
     }
     __syncthreads();
 
@@ -228,9 +214,7 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
     // look back (one thread per digit)
     if (dg < (uint32_t)RADIX) {
         uint64_t excl = 0;
-        if constexpr ((kVariant & 1) != 0) {
-            excl = t * (uint64_t)(TILE / RADIX);
-        } else if (t > 0) {
+        if (t > 0) {
             // read kLook predecessors per step (independent loads: one
             // fabric round trip per kLook tiles instead of per tile)
             constexpr int kLook = 4;
@@ -273,25 +257,10 @@ __global__ __launch_bounds__(BLOCK) void k_onesweep(Src src, uint64_t n, uint32_
         s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
     }
     __syncthreads();
-    if constexpr ((kVariant & 4) != 0) {
-        // no LDS staging: scatter straight from registers
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            if (d[j] < (uint32_t)RADIX) {
-                const uint64_t g = (uint64_t)s_gofs[d[j]] + s_wcnt[wave][d[j]] + r[j];
-                if (g < n) {
-                    out_keys[g] = k[j];
-                    out_vals[g] = v[j];
-                }
-            }
-        }
-        return;
-    }
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         if (d[j] < (uint32_t)RADIX) {
-            const uint32_t pos = (kVariant & 2) ? (uint32_t)(wave * WTILE) + r[j]
-                                                : s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
+            const uint32_t pos = s_start[d[j]] + s_wcnt[wave][d[j]] + r[j];
             s_keys[pos] = k[j];
             s_vals[pos] = v[j];
         }

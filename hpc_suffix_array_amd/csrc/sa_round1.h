@@ -41,11 +41,6 @@
 #ifndef SA_ITEMS_PK
 #define SA_ITEMS_PK 12
 #endif
-// local sort: 1 = size-classed sub-bucket networks (k_bucket_sort_cls), 0 =
-// 16-input network per sub-bucket (k_bucket_sort).  Measured at 2^30 DNA on
-// one box: 8.5 ms (class lists + per-thread re-count of the groups; 12.7 ms
-// with row-ballot segments) against 7.3 ms -- the list building and the
-// re-count cost more than the smaller networks save; kept for A/B runs.
 // the sorted key1 of every 2^kKeySample-th SA position is kept for the rank
 // look-ups of later rounds (lower_bound_sampled)
 #ifndef SA_KEY_SAMPLE
@@ -59,9 +54,6 @@ constexpr uint64_t kPadMinN = 1ull << 26;
 constexpr uint64_t kPadMaxN = 1ull << 31;
 constexpr uint32_t kPadStartOff = kLoRadix + 1024;                 // kLoRadix + 1 words
 constexpr uint32_t kPadDenseOff = kPadStartOff + kLoRadix + 64;    // kLoRadix words
-#ifndef SA_LOCAL_SORT_CLS
-#define SA_LOCAL_SORT_CLS 0
-#endif
 
 struct BucketPlan {
     BucketSpec bs{};
@@ -467,11 +459,6 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     br_measured.bits1 = 0;
     auto local_sort = [&](const SegOut& o) {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
-#if SA_LOCAL_SORT_CLS
-        hipLaunchKernelGGL((k_bucket_sort_cls<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
-                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
-                           c->keys[0], d_sa, skew, o);
-#else
         // (no SA_HIP here: its error return would make the lambda non-void)
         (void)hipMemsetAsync(c->words + kRetryWord, 0, 4, s);
         hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
@@ -482,7 +469,6 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                                0, s, (const uint64_t*)c->keys_u, br_measured, (const uint32_t*)ws,
                                (const uint32_t*)retry, c->words, bp.ib, c->keys[0], d_sa, skew, o, (uint32_t*)nullptr,
                                (uint32_t)kRetryWord);
-#endif
         // skewed windows are rare: a small grid loops over them (one
         // workgroup per listed window spent 0.1 ms on empty workgroups)
         const uint32_t gl = std::min<uint32_t>(g, 1024);
