@@ -739,6 +739,11 @@ struct SegOut {
     uint32_t* cnt_u;
     uint32_t* cnt_g;
     uint32_t ksh;   // sorted key1 written for every 2^ksh-th SA position only (store_window)
+    // non-null (range-partitioned build): each unsorted member's rank goes to
+    // tmp_rank at its window-local U index instead of rank[x] -- the compact
+    // rank map's slots are known only once the member bitmap is complete, so
+    // k_u_gather places them
+    uint32_t* tmp_rank = nullptr;
 };
 
 template <int BLOCK, int ITEMS>
@@ -826,7 +831,9 @@ __device__ __forceinline__ void window_segments(const uint64_t* __restrict__ s_w
             const uint32_t ku = bu + (uint32_t)((pre >> 32) & 0xFFFFu) + (uint32_t)__popcll(mu & lt);
             const uint32_t kg = bg + (uint32_t)(pre >> 48) + (uint32_t)__popcll(muh & lem) - 1u;
             const uint32_t x = (uint32_t)(s_w[rb0 + lane] & imask);
-            so.rank[x] = (uint32_t)(so.rank_off + a + hpos + 1u);
+            const uint32_t rv = (uint32_t)(so.rank_off + a + hpos + 1u);
+            if (so.tmp_rank) so.tmp_rank[a + ku] = rv;
+            else so.rank[x] = rv;
             atomicOr(&so.member[x >> 5], 1u << (x & 31));
             so.tmp_pos[a + ku] = (uint32_t)(a + rb0 + lane);
             so.tmp_idx[a + ku] = x;
@@ -915,22 +922,74 @@ __global__ __launch_bounds__(kBlock) void k_wscan_apply(uint32_t* __restrict__ c
 
 // each listed window's U members from tmp (window-local order) to their
 // compacted SA-order slots; one wave per window
+// (so.tmp_rank: each member's rank also to rank[rm.slot(x)], the compact
+// rank map of the range-partitioned build)
 __global__ __launch_bounds__(kBlock) void k_u_gather(const uint32_t* __restrict__ list,
                                                      const uint32_t* __restrict__ words,
                                                      const uint32_t* __restrict__ ws, const uint32_t* __restrict__ ou,
                                                      const uint32_t* __restrict__ og, SegOut so,
                                                      uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
-                                                     uint32_t* __restrict__ u_g) {
+                                                     uint32_t* __restrict__ u_g, RankMap rm = RankMap{}) {
     const uint32_t nlist = words[7];
     const uint32_t lane = lane_id();
     for (uint64_t q = (uint64_t)blockIdx.x * kWaves + wave_id(); q < nlist; q += (uint64_t)gridDim.x * kWaves) {
         const uint32_t j = list[q];
         const uint32_t a = ws[j], o = ou[j], c = ou[j + 1] - o, g0 = og[j];
         for (uint32_t k = lane; k < c; k += kWave) {
+            const uint32_t x = so.tmp_idx[a + k];
             u_pos[o + k] = so.tmp_pos[a + k];
-            u_idx[o + k] = so.tmp_idx[a + k];
+            u_idx[o + k] = x;
             u_g[o + k] = so.tmp_g[a + k] + g0;
+            if (so.tmp_rank) so.rank[rm.slot(x)] = so.tmp_rank[a + k];
         }
+    }
+}
+
+// Exclusive popcount scan of a bitmap of nw words (the compact rank map's
+// prefix, RankMap): k_popc_reduce (per-block popcount sums) -> k_popc_top
+// (their exclusive scan, one workgroup) -> k_popc_apply (each block's words
+// rescanned from its offset).  kWsBlock words per block.
+__global__ __launch_bounds__(kBlock) void k_popc_reduce(const uint32_t* __restrict__ bits, uint64_t nw,
+                                                        uint32_t* __restrict__ part) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kWsBlock + (uint64_t)threadIdx.x * kWsPer;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < kWsPer; ++k) sum += b0 + k < nw ? (uint32_t)__popc(bits[b0 + k]) : 0u;
+    uint32_t tot;
+    block_exclusive_sum(sum, s_tmp, &tot);
+    if (threadIdx.x == 0) part[blockIdx.x] = tot;
+}
+
+__global__ __launch_bounds__(kBlock) void k_popc_top(uint32_t* __restrict__ part, uint32_t blocks) {
+    __shared__ uint32_t s_tmp[kWaves];
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < blocks; b0 += kBlock) {
+        const uint32_t b = b0 + threadIdx.x;
+        const uint32_t v = b < blocks ? part[b] : 0u;
+        uint32_t t;
+        const uint32_t e = block_exclusive_sum(v, s_tmp, &t) + carry;
+        if (b < blocks) part[b] = e;
+        carry += t;
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void k_popc_apply(const uint32_t* __restrict__ bits, uint64_t nw,
+                                                       const uint32_t* __restrict__ part,
+                                                       uint32_t* __restrict__ prefix) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kWsBlock + (uint64_t)threadIdx.x * kWsPer;
+    uint32_t c[kWsPer], sum = 0;
+#pragma unroll
+    for (int k = 0; k < kWsPer; ++k) {
+        c[k] = b0 + k < nw ? (uint32_t)__popc(bits[b0 + k]) : 0u;
+        sum += c[k];
+    }
+    uint32_t run = block_exclusive_sum(sum, s_tmp, nullptr) + part[blockIdx.x];
+#pragma unroll
+    for (int k = 0; k < kWsPer; ++k) {
+        if (b0 + k < nw) prefix[b0 + k] = run;
+        run += c[k];
     }
 }
 
@@ -1253,7 +1312,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                         if (!eqp && eqn) ++kg;
                         if (eqp || eqn) {
                             const uint32_t xi = (uint32_t)(x & imask);
-                            so.rank[xi] = (uint32_t)(so.rank_off + a + head + 1u);
+                            const uint32_t rv = (uint32_t)(so.rank_off + a + head + 1u);
+                            if (so.tmp_rank) so.tmp_rank[a + ku] = rv;
+                            else so.rank[xi] = rv;
                             atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
                             so.tmp_pos[a + ku] = (uint32_t)(a + k);
                             so.tmp_idx[a + ku] = xi;

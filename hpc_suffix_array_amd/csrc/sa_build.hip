@@ -462,16 +462,36 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     int rc = ev.make();
     if (rc) return rc;
     const Chunking ch = plan_chunks(n);
+    // first ranks: dense codes 1..sigma of the bytes present (the order of
+    // manber_myers.c:90's text[i] + 1, so D_j and the round count are the
+    // reference's; the first key spans 2 bit_width(sigma) bits, not 18)
+    uint32_t* h_alpha = c->host_words + 64;
+    uint16_t* h_code = reinterpret_cast<uint16_t*>(c->host_words + 320);
+    SA_HIP(hipMemsetAsync(c->alpha, 0, 8 * 4, s));
+    tm.begin(SA_K_ALPHABET);
+    {
+        const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), SA_ALPHA_GRID);
+        hipLaunchKernelGGL(k_alphabet, dim3(grid), dim3(kBlock), 0, s, d_text, n, c->alpha);
+    }
+    tm.end();
+    add_bytes(st, SA_K_ALPHABET, n);
+    SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 8 * 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    uint32_t sigma = 0;
+    for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
+    SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
     tm.begin(SA_K_INIT);
     {
         const uint64_t grid = std::min<uint64_t>((n + kBlock * 4 - 1) / (kBlock * 4), 4096);
-        hipLaunchKernelGGL(k_init_rank, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n, c->rank);
+        hipLaunchKernelGGL(k_init_rank_dense, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n,
+                           (const uint16_t*)c->code, c->rank);
     }
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_INIT, 5 * n);
+    if (st) st->sigma = (int32_t)sigma;
 
-    uint64_t D = 256;   // manber_myers.c:94
+    uint64_t D = sigma;   // ranks 1..sigma (manber_myers.c:94 sizes its bins for 256)
     for (uint64_t h = 1;; h *= 2) {
         SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t w = bit_width(D);          // ranks are 0..D
@@ -573,9 +593,10 @@ template <class Pos>
 static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
                     bool sparse_ok, bool* sparse_out,
                     uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
-                    uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0) {
-    // rank_arr / rank_off: the range-partitioned build's n-entry rank array and
-    // its SA offset (sa_dist.h); the context's rank array and 0 on one GPU
+                    uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0, RankMap rm = RankMap{}) {
+    // rank_arr / rank_off / rm: the range-partitioned build's compact rank map
+    // and its SA offset (sa_dist.h); the context's rank array, 0 and the
+    // identity map on one GPU
     if (!rank_arr) rank_arr = c->rank;
     uint32_t* c_h = c->counts;
     uint32_t* c_u = c->counts + kMaxChunks;
@@ -605,7 +626,7 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     tm.begin(SA_K_SEG_WRITE);
     hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
                        (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, rank_arr, sa,
-                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1, (uint32_t)rank_off);
+                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1, (uint32_t)rank_off, rm);
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);

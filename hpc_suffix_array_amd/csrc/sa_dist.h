@@ -60,8 +60,9 @@ struct DistState {
     // device
     uint64_t cap_n = 0, cap_m = 0;
     uint16_t* owner_tab = nullptr;   // kCoarse: coarse bucket -> rank
-    uint32_t* grank = nullptr;       // n: rank of this range's unsorted suffixes
-    uint32_t* gmember = nullptr;     // n bits: this range's unsorted suffixes
+    uint32_t* gmember = nullptr;     // n bits: this range's round-1 unsorted suffixes
+    uint32_t* gprefix = nullptr;     // n / 32 words + scan sums: the bitmap's popcount prefix
+    uint32_t* crank = nullptr;       // cap_m: their ranks, in text order (RankMap)
     uint64_t* r1 = nullptr;          // cap_m: rank[x + h] of each unsorted x
     uint32_t* perm = nullptr;        // cap_m: request slot -> unsorted index
     uint32_t* owner = nullptr;       // cap_m: owner of each unsorted x's request
@@ -78,8 +79,9 @@ static void free_dist(sa_context* c) {
     DistState* d = c->dist;
     if (!d) return;
     hipFree(d->owner_tab);
-    hipFree(d->grank);
     hipFree(d->gmember);
+    hipFree(d->gprefix);
+    hipFree(d->crank);
     hipFree(d->r1);
     hipFree(d->perm);
     hipFree(d->owner);
@@ -95,15 +97,20 @@ static DistState* dist_of(sa_context* c) {
 
 static int ensure_dist_n(sa_context* c, uint64_t n) {
     DistState* d = dist_of(c);
-    if (d->grank && d->cap_n >= n) return SA_OK;
-    hipFree(d->grank);
+    if (d->gmember && d->cap_n >= n) return SA_OK;
+    hipFree(d->gprefix);
     hipFree(d->gmember);
-    d->grank = nullptr;
+    d->gprefix = nullptr;
     d->gmember = nullptr;
     d->cap_n = 0;
     if (!d->owner_tab && hipMalloc(&d->owner_tab, kCoarse * 2) != hipSuccess) d->owner_tab = nullptr;
     if (!d->cnt && hipMalloc(&d->cnt, (2 * kDistMaxWorld + 8) * 4) != hipSuccess) d->cnt = nullptr;
-    if (!d->owner_tab || !d->cnt || hipMalloc(&d->grank, align_up(std::max<uint64_t>(n, 1), 64) * 4) != hipSuccess ||
+    // the member bitmap and its popcount prefix (+ the scan's block sums):
+    // 8 bytes per 32 positions, not the 4 per position of an n-entry rank
+    // array -- per-rank memory falls with the world size (RankMap)
+    const uint64_t nwb = (std::max<uint64_t>(n, 1) + 31) / 32;
+    if (!d->owner_tab || !d->cnt ||
+        hipMalloc(&d->gprefix, (nwb + 1 + (nwb + kWsBlock - 1) / kWsBlock + 64) * 4) != hipSuccess ||
         hipMalloc(&d->gmember, align_up(std::max<uint64_t>(n, 1), 1024) / 8) != hipSuccess) {
         (void)hipGetLastError();
         return set_err(SA_E_NOMEM, "range-partitioned build: rank arrays for n=%llu", (unsigned long long)n);
@@ -122,12 +129,13 @@ static int ensure_dist_m(sa_context* c, uint64_t m) {
     hipFree(d->r1);
     hipFree(d->perm);
     hipFree(d->owner);
+    hipFree(d->crank);
     d->r1 = nullptr;
-    d->perm = d->owner = nullptr;
+    d->perm = d->owner = d->crank = nullptr;
     d->cap_m = 0;
     const uint64_t a = align_up(std::max<uint64_t>(m, 1), 64);
     if (hipMalloc(&d->r1, a * 8) != hipSuccess || hipMalloc(&d->perm, a * 4) != hipSuccess ||
-        hipMalloc(&d->owner, a * 4) != hipSuccess) {
+        hipMalloc(&d->owner, a * 4) != hipSuccess || hipMalloc(&d->crank, a * 4) != hipSuccess) {
         (void)hipGetLastError();
         return set_err(SA_E_NOMEM, "range-partitioned build: unsorted-set buffers for m=%llu", (unsigned long long)m);
     }
@@ -216,8 +224,8 @@ __global__ __launch_bounds__(kBlock) void k_dist_fill(const uint32_t* __restrict
 // this range), else the round-1 group head of key1(j) in the range's sorted
 // keys, searched inside j's bucket.  err bit 0: a request outside the range.
 struct DistLookup {
-    const uint32_t* __restrict__ grank;
-    const uint32_t* __restrict__ gmember;
+    const uint32_t* __restrict__ crank;    // the members' ranks (compact, RankMap rm)
+    RankMap rm;
     const uint64_t* __restrict__ keys1;    // this range's sorted key1: every 2^ksh-th of m
     const uint32_t* __restrict__ sa;       // this range's SA (m; key1 of the other slots)
     uint32_t ksh;
@@ -232,7 +240,7 @@ struct DistLookup {
 
 // rank[j] (j < n) by the owner of j's bucket; *bad set on a j outside the range
 __device__ __forceinline__ uint64_t dist_rank_of(const DistLookup& L, const uint8_t* s_map, uint64_t j, bool* bad) {
-    if ((L.gmember[j >> 5] >> (j & 31)) & 1u) return L.grank[j];
+    if ((L.rm.member[j >> 5] >> (j & 31)) & 1u) return L.crank[L.rm.slot((uint32_t)j)];
     uint32_t D;
     const uint64_t x = key1_words<true>(L.text, L.n, s_map, L.bs, j, &D);
     const uint32_t b = (uint32_t)(((uint64_t)D * L.bs.cmul) >> L.bs.bsh) - L.blo;
@@ -474,8 +482,10 @@ static int dist_round1(sa_context* c, const uint8_t* d_text, uint32_t* d_sa, hip
     br.m = d->m;
     br.sa_off = d->sa_off;
     br.always_u = true;
-    br.rank = d->grank;
+    br.rank = d->crank;
     br.member = d->gmember;
+    br.prefix = d->gprefix;
+    br.tmp_rank = d->perm;   // free until the first request round
     bool done = false, fused = false;
     uint64_t seg[3] = {0, 0, 0};
     int rc = round1_bucketed(c, d_text, d->n, d_sa, d->bp, br, s, tm, st, &done, &fused, seg, &d->ksh);
@@ -551,7 +561,7 @@ static int dist_answer(sa_context* c, const uint32_t* d_req, uint64_t nreq, uint
     if (nreq == 0) return SA_OK;
     if (!d_req || !d_ans) return set_err(SA_E_INVALID, "NULL request / answer buffer");
     const uint32_t nbl = d->bhi - d->blo;
-    const DistLookup L{d->grank, d->gmember, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
+    const DistLookup L{d->crank, RankMap{d->gmember, d->gprefix}, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
                        d->n, d->bp.bs, d->blo, nbl, d->sa_off};
     const uint32_t grid = (uint32_t)std::min<uint64_t>((nreq + kBlock - 1) / kBlock, 8192);
     hipLaunchKernelGGL(k_dist_answer, dim3(grid), dim3(kBlock), 0, s, d_req, nreq, L, d_ans, d->cnt + 2 * kDistMaxWorld);
@@ -579,7 +589,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     Timer tm{c, s, false, nullptr};
     const uint64_t m = d->mu, G = d->gu;
     if (d->world == 1) {   // every look-up is local: no request / answer exchange
-        const DistLookup L{d->grank, d->gmember, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
+        const DistLookup L{d->crank, RankMap{d->gmember, d->gprefix}, c->keys[0], d->sa, d->ksh, c->segw + kBstartOff, d->text, (const uint16_t*)c->code,
                            d->n, d->bp.bs, d->blo, d->bhi - d->blo, d->sa_off};
         const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
         hipLaunchKernelGGL(k_dist_r1_local, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[d->uo], m, h, L,
@@ -628,7 +638,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     }
     uint64_t Du = 0, m2 = 0, G2 = 0;
     int rc = segments(c, sorted, c->vals_u, plan_chunks(m), PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm,
-                      nullptr, &Du, &m2, &G2, d->grank, d->sa_off);
+                      nullptr, &Du, &m2, &G2, d->crank, d->sa_off, RankMap{d->gmember, d->gprefix});
     if (rc) return rc;
     if (d->world == 1) {   // the local look-ups' range check (segments() synchronised the stream)
         SA_HIP(hipMemcpy(hc, d->cnt + 2 * kDistMaxWorld, 4, hipMemcpyDeviceToHost));

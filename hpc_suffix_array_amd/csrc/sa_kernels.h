@@ -464,6 +464,33 @@ __global__ __launch_bounds__(kBlock) void k_init_rank(const uint8_t* __restrict_
     }
 }
 
+// The reference schedule's first ranks as DENSE codes (code[byte] = 1..sigma
+// in byte order, 0 = past the end): the same order as text[i] + 1, so every
+// round's D_j and the round count are the reference's, but the first
+// round's key spans 2 bit_width(sigma) bits instead of 18 (DNA: one radix
+// pass of 6 bits instead of three of 8).
+__global__ __launch_bounds__(kBlock) void k_init_rank_dense(const uint8_t* __restrict__ text, uint64_t n,
+                                                            const uint16_t* __restrict__ code,
+                                                            uint32_t* __restrict__ rank) {
+    __shared__ uint16_t s_code[256];
+    s_code[threadIdx.x] = code[threadIdx.x];
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * 4;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 4; i < n; i += stride) {
+        if (i + 4 <= n && (((uintptr_t)(text + i)) & 3) == 0) {
+            const uint32_t v = *reinterpret_cast<const uint32_t*>(text + i);
+            uint4 r;
+            r.x = s_code[v & 0xFFu];
+            r.y = s_code[(v >> 8) & 0xFFu];
+            r.z = s_code[(v >> 16) & 0xFFu];
+            r.w = s_code[v >> 24];
+            *reinterpret_cast<uint4*>(rank + i) = r;
+        } else {
+            for (uint64_t j = i; j < n && j < i + 4; ++j) rank[j] = s_code[text[j]];
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // radix upsweep: per-(digit, chunk) counts.  Per-wave LDS histograms keep the
 // LDS atomics of different waves apart (counting_sort_radix_seq :19-21).
@@ -748,6 +775,7 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
     }
     (void)s_tmp;
 }
+
 
 // ---------------------------------------------------------------------------
 // alphabet presence: bit b of present[b >> 5] is set when byte b occurs.
@@ -1065,8 +1093,23 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(uint32_t* __restrict__ c_he
     }
 }
 
+// Where rank[x] lives: rank[x] itself (prefix == nullptr: the n-entry rank
+// array of one GPU), or the range-partitioned build's compact map -- only
+// the members of this rank's round-1 unsorted set have ranks, in text order:
+// rank[prefix[x >> 5] + popc(member[x >> 5] below bit x & 31)], prefix the
+// exclusive popcount scan of the member bitmap (sa_dist.h).  8 + 4 |U| bytes
+// per suffix range instead of 4 n.
+struct RankMap {
+    const uint32_t* __restrict__ member = nullptr;
+    const uint32_t* __restrict__ prefix = nullptr;
+    __device__ __forceinline__ uint64_t slot(uint32_t x) const {
+        if (!prefix) return x;
+        return (uint64_t)prefix[x >> 5] + (uint32_t)__popc(member[x >> 5] & ((1u << (x & 31u)) - 1u));
+    }
+};
+
 // Per sorted index s (idx = sorted suffix index):
-//   rank[idx]   = pos(head of s's group) + 1
+//   rank[idx]   = pos(head of s's group) + 1  (at rm.slot(idx))
 //   sa[pos(s)]  = idx                               (when sa != nullptr)
 //   unsorted members are compacted, in order, to (u_pos, u_idx, u_g) with
 //   u_g the dense id of their group among unsorted groups.
@@ -1079,7 +1122,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ sa,
                                                       uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
                                                       uint32_t* __restrict__ u_g, uint32_t* __restrict__ member,
-                                                      int dense_rank, uint32_t rank_off) {
+                                                      int dense_rank, uint32_t rank_off, RankMap rm = RankMap{}) {
     __shared__ uint64_t s_m[kWaves][kItems][3];
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
@@ -1146,7 +1189,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                 const uint32_t x = idx[s];
                 const uint32_t p = pos(s);
                 const bool in_u = (mu >> lane) & 1ull;
-                if (dense_rank || in_u) rank[x] = rank_off + (hs == s ? p : pos(hs)) + 1u;
+                if (dense_rank || in_u) rank[rm.slot(x)] = rank_off + (hs == s ? p : pos(hs)) + 1u;
                 if (sa) sa[p] = x;
                 if (member && in_u) atomicOr(&member[x >> 5], 1u << (x & 31));
                 if (in_u) {

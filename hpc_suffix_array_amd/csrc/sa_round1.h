@@ -177,6 +177,12 @@ struct BucketRange {
     bool always_u = false;      // compact the unsorted set whatever its size
     uint32_t* rank = nullptr;   // n-entry rank array / n-bit member map of the
     uint32_t* member = nullptr; // unsorted set (null: the context's)
+    // compact rank map (RankMap; the range-partitioned build): rank holds the
+    // members' ranks in text order, prefix ((n + 31) / 32 words + the scan's
+    // per-block sums) the member bitmap's exclusive popcount scan; tmp_rank
+    // (m words) stages the ranks until the bitmap is complete
+    uint32_t* prefix = nullptr;
+    uint32_t* tmp_rank = nullptr;
 };
 
 static BucketRange full_range(const BucketPlan& bp, uint64_t n) {
@@ -451,7 +457,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // sorted key1 sampled (every 2^kKeySample-th SA position) for the sparse
     // rank look-ups; a round that turns out dense re-runs the sort with every
     // key1 below (segments() reads them all)
-    const SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g, kKeySample};
+    SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g, kKeySample};
+    so.tmp_rank = br_.prefix ? br_.tmp_rank : nullptr;
     // fixed-span windows whose keys cluster, for a second launch with the
     // measured span (after the windows' first buckets: 7 nw + 4 <= capacity)
     uint32_t* const retry = cnt_g + 2 * nw + 2;
@@ -515,9 +522,22 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         hipLaunchKernelGGL(k_wscan_top, dim3(1), dim3(kBlock), 0, s, part, wb);
         hipLaunchKernelGGL(k_wscan_apply, dim3(wb), dim3(kBlock), 0, s, cnt_u, cnt_g, nw, (const uint32_t*)part);
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((c->host_words[7] + kWaves - 1) / kWaves, 4096));
+        RankMap rm;
+        if (br_.prefix) {
+            // the member bitmap is complete: its popcount prefix gives each
+            // member's slot in the compact rank map
+            const uint64_t nwb = (n + 31) / 32;
+            const uint32_t pb = (uint32_t)((nwb + kWsBlock - 1) / kWsBlock);
+            uint32_t* ppart = br_.prefix + nwb + 1;
+            hipLaunchKernelGGL(k_popc_reduce, dim3(pb), dim3(kBlock), 0, s, (const uint32_t*)member, nwb, ppart);
+            hipLaunchKernelGGL(k_popc_top, dim3(1), dim3(kBlock), 0, s, ppart, pb);
+            hipLaunchKernelGGL(k_popc_apply, dim3(pb), dim3(kBlock), 0, s, (const uint32_t*)member, nwb,
+                               (const uint32_t*)ppart, br_.prefix);
+            rm = RankMap{member, br_.prefix};
+        }
         hipLaunchKernelGGL(k_u_gather, dim3(g), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)c->words,
                            (const uint32_t*)ws, (const uint32_t*)cnt_u, (const uint32_t*)cnt_g, so, c->u_pos[0],
-                           c->u_idx[0], c->u_g[0]);
+                           c->u_idx[0], c->u_g[0], rm);
         tm.end();
         add_bytes(st, SA_K_SEG_WRITE, 8 * (2 * nw + 2) + seg[1] * 24);
         SA_HIP(hipGetLastError());

@@ -10,11 +10,14 @@ and size-independent properties (O(n) checker, analytic degenerate SA) at
 larger sizes.
 """
 import ctypes
+import os
+import sys
 
 import numpy as np
 import pytest
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def test_golden_cases_ex(gpu, golden):
@@ -598,3 +601,23 @@ def test_local_sort_fixed_span(gpu, oracle, extra, monkeypatch):
         got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
         assert st["round1"] == "bucketed" and st["round1_layout"]["compact"], (kind, st)
         assert (got == oracle.sa_c(t)).all(), (kind, extra)
+
+
+@pytest.mark.slow
+@pytest.mark.gpu
+def test_config4_partition_at_its_own_shape(gpu):
+    """configs[3] at its own shape, played rank by rank on one GPU: byte256
+    text of n = 2^32 suffixes over G = 8 ranks (19-bit buckets, 32-bit index
+    fields, ~2^29 suffixes per rank).  The cut plan covers n suffixes in
+    contiguous SA ranges, every rank's round 1 sorts its slice on the first K
+    symbols, the slices follow each other in SA order and every text position
+    lands in exactly one slice (scripts/sim_ranks.py --check; the later
+    rounds' look-ups across ranks are the multi-rank tests' and the 8-GPU
+    run's)."""
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import sim_ranks
+    rows = sim_ranks.simulate(1 << 32, "byte256", [8], ranks="all", reps=0, check=True)
+    assert len(rows) == 8 and all(r["checked"] and r["ok"] == 1 for r in rows)
+    assert sum(r["m"] for r in rows) == 1 << 32
+    assert max(r["share"] for r in rows) < 1.2, rows
+    assert rows[0]["bucket_bits"] == 19
