@@ -92,6 +92,10 @@ int main(int argc, char** argv) {
     CK(hipMalloc(&ovals, n * 4));
     const uint64_t nw = (n + kWinStride - 1) / kWinStride;
     CK(hipMalloc(&ws, (4 * nw + 3) * 4));
+    uint32_t* retry;
+    uint4* hdr;
+    CK(hipMalloc(&retry, (nw + 1) * 4));
+    CK(hipMalloc(&hdr, (nw + 1) * 16));
     CK(hipMalloc(&words, 256));
     uint32_t* list = ws + nw + 1;
     uint32_t* skew = list + nw;
@@ -101,6 +105,8 @@ int main(int argc, char** argv) {
     hipLaunchKernelGGL(k_keys, dim3(8192), dim3(256), 0, 0, keys, vals, items, n, rb, rbits, ib);
     hipLaunchKernelGGL(k_tables, dim3(512), dim3(256), 0, 0, n, bstart, bdmin);
     const BucketRel br{wbk, bstart, bdmin, rb};
+    BucketRel brf = br;   // fixed span: the keys fill rb bits of their bucket
+    brf.bits1 = rb;
     // segments outputs (as round1_bucketed lays them out)
     uint32_t *rank, *member, *tmp;
     CK(hipMalloc(&rank, n * 4));
@@ -141,31 +147,52 @@ int main(int argc, char** argv) {
     timeit("copy 12 B in + out (old item size)", [&] {
         hipLaunchKernelGGL(k_copy12, dim3(16384), dim3(256), 0, 0, keys, vals, n, okeys, ovals);
     });
+    int cus = 256;
+    CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
+    // the fixed-span 32-bit kernel over the one-bucket windows (k_window_split)
+    auto fast = [&](const SegOut& o, bool probe) {
+        CK(hipMemset(words + kRetryWord, 0, 12));
+        hipLaunchKernelGGL(k_window_split, dim3(1024), dim3(256), 0, 0, (const uint32_t*)list, (const uint32_t*)ws, brf,
+                           words, hdr, retry, 1u);
+        if (probe)
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, ClockProbe>), dim3(kBsWpc * cus), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)items, (const uint4*)hdr, rb, rb, ib, words, okeys, ovals, retry, o);
+        else
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(kBsWpc * cus), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)items, (const uint4*)hdr, rb, rb, ib, words, okeys, ovals, retry, o);
+    };
+    timeit("bucket_sort (32-bit, prefetch)", [&] { fast(SegOut{}, false); });
+    timeit("bucket_sort (32-bit, prefetch) + segments", [&] { fast(so, false); });
     for (uint32_t g : {512u, hw[7]}) {
         char nm[64];
-        std::snprintf(nm, sizeof nm, "bucket_sort grid %u", g);
+        std::snprintf(nm, sizeof nm, "bucket_sort_wide grid %u", g);
         timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
+            hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, SegOut{});
         });
-        std::snprintf(nm, sizeof nm, "bucket_sort + segments grid %u", g);
+        std::snprintf(nm, sizeof nm, "bucket_sort_wide + segments grid %u", g);
         timeit(nm, [&] {
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
+            hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, 0,
                                (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list,
                                words, ib, okeys, ovals, skew, so);
         });
     }
-    {   // per-phase clock64 spans of one workgroup's thread 0, per window
+    for (int fastk = 0; fastk < 2; ++fastk) {   // per-phase clock64 spans of thread 0, per window
         CK(hipMemset(words + 32, 0, 64));
-        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, ClockProbe>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
-                           br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, so);
+        if (fastk)
+            fast(so, true);
+        else
+            hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems, ClockProbe>), dim3(512), dim3(kBsBlock), 0, 0,
+                               (const uint64_t*)items, br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys,
+                               ovals, skew, so);
         CK(hipDeviceSynchronize());
         unsigned long long t[7];
         CK(hipMemcpy(t, words + 32, 56, hipMemcpyDeviceToHost));
-        const char* nm[7] = {"load+minmax", "histogram", "scan", "scatter", "net-sort", "U+scan", "store+sync"};
+        const char* nm[7] = {"load", "histogram", "scan", "scatter", "net-sort", "U+scan", "store+sync"};
         double tot = 0;
         for (int k = 0; k < 7; ++k) tot += (double)t[k];
+        std::printf("%s phases:\n", fastk ? "bucket_sort (32-bit)" : "bucket_sort_wide");
         for (int k = 0; k < 7; ++k)
             std::printf("  phase %-12s %7.0f clk/window (%4.1f %%)\n", nm[k], (double)t[k] / hw[7], 100.0 * t[k] / tot);
     }
@@ -173,8 +200,7 @@ int main(int argc, char** argv) {
     std::printf("flags=%u skewed=%u heads=%u unsorted=%u groups=%u (accumulated over runs)\n", hw[6], hw[10], hw[0], hw[1], hw[2]);
     // check: output sorted within each window, keys monotone overall
     std::vector<uint64_t> h(std::min<uint64_t>(n, 1 << 24));
-    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(512), dim3(kBsBlock), 0, 0, (const uint64_t*)items,
-                       br, (const uint32_t*)ws, (const uint32_t*)list, words, ib, okeys, ovals, skew, SegOut{});
+    fast(SegOut{}, false);
     CK(hipMemcpy(h.data(), okeys, h.size() * 8, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (size_t i = 1; i < h.size(); ++i) bad += h[i] < h[i - 1];

@@ -60,6 +60,11 @@ constexpr int kBsBlock = SA_BS_BLOCK;
 constexpr int kBsItems = SA_BS_ITEMS;
 constexpr int kBsCap = kBsBlock * kBsItems;  // 9216 suffixes per window
 constexpr uint32_t kWinStride = 1024;        // nominal window spacing W
+// persistent workgroups per CU of the fixed-span local sort (k_bucket_sort)
+#ifndef SA_BS_WPC
+#define SA_BS_WPC 2
+#endif
+constexpr uint32_t kBsWpc = SA_BS_WPC;
 #ifndef SA_BS_GRID
 #define SA_BS_GRID (1u << 22)
 #endif
@@ -1095,7 +1100,7 @@ struct NoProbe {
 };
 
 template <int BLOCK, int ITEMS, class Probe = NoProbe>
-__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in, BucketRel br,
+__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort_wide(const uint64_t* __restrict__ keys_in, BucketRel br,
                                                        const uint32_t* __restrict__ ws,
                                                        const uint32_t* __restrict__ list, uint32_t* __restrict__ words,
                                                        uint32_t ib, uint64_t* __restrict__ keys_out,
@@ -1336,6 +1341,384 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     }
     probe.flush(words);
     flush_totals(words, th, tu, tg);
+}
+
+// ---------------------------------------------------------------------------
+// The fixed-span local sort over 32-bit LDS words.  For one-bucket windows of
+// the compact layout (keys fill br.bits1 bits) the sub-bucket holds the top
+// kSubBits of the key, so the bits below it (<= kLowMax) and the item's load
+// slot (< 2^kSlotBits) fit one u32: the counting scatter writes that word,
+// the sub-buckets are sorted as u32 words (networks without a gather by
+// slot), and the store fetches the index of each sorted slot from a second
+// LDS array (idx by load slot, written coalesced).  The register sort then
+// needs 16 VGPRs instead of 48, which leaves room for the NEXT window's
+// items: a workgroup takes windows from a ticket (dynamic, one ahead) and
+// loads the next window right after scattering the current one into LDS,
+// so the loads are in flight during the sort, the segments and the store.
+// Windows: k_window_split lists the one-bucket windows with their headers
+// (hdr, words[14]); the others, and windows whose keys cluster (a sub-bucket
+// above kMaxSub), go to `retry` for k_bucket_sort_wide (measured span).
+// ---------------------------------------------------------------------------
+// This lane's first item slot of a window (wave-major rows of 64) as a value
+// the compiler cannot hoist out of the window loop: kept live there, the
+// ITEMS slot indices l0 + 64 i and the offsets derived from them took 36
+// VGPRs and made the next window's loads spill
+template <int ITEMS>
+__device__ __forceinline__ uint32_t slot0() {
+    uint32_t t = threadIdx.x;
+    asm volatile("" : "+v"(t));
+    return (t / kWave) * (kWave * ITEMS) + (t & (kWave - 1));
+}
+
+constexpr uint32_t kSlotBits = 14;
+constexpr uint32_t kSlotMask = (1u << kSlotBits) - 1u;
+constexpr uint32_t kLowMax = 32 - kSlotBits;   // key bits below the sub-bucket
+static_assert(kBsCap <= (1 << kSlotBits), "load slots in kSlotBits");
+constexpr int kHdrWord = 14;                   // words[]: one-bucket windows listed by k_window_split
+constexpr int kTicketWord = 15;                // words[]: k_bucket_sort's window ticket
+
+// listed windows -> one-bucket windows with headers {j, a, m, Dmin} (fast:
+// the fixed-span kernel runs) or the retry list (k_bucket_sort_wide)
+__global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restrict__ list,
+                                                         const uint32_t* __restrict__ ws, BucketRel br,
+                                                         uint32_t* __restrict__ words, uint4* __restrict__ hdr,
+                                                         uint32_t* __restrict__ retry, uint32_t fast) {
+    const uint32_t nlist = words[7];
+    const uint32_t lane = lane_id();
+    for (uint64_t q0 = (uint64_t)blockIdx.x * kBlock; q0 < nlist; q0 += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t q = q0 + threadIdx.x;
+        uint32_t j = 0, b0 = 0;
+        bool one = false;
+        const bool ok = q < nlist;
+        if (ok) {
+            j = list[q];
+            b0 = br.wb[j];
+            one = fast && br.wb[j + 1] - b0 == 1u;
+        }
+        const uint64_t m1 = __ballot(ok && one), m2 = __ballot(ok && !one);
+        uint32_t base1 = 0, base2 = 0;
+        if (lane == 0) {
+            if (m1) base1 = atomicAdd(&words[kHdrWord], (uint32_t)__popcll(m1));
+            if (m2) base2 = atomicAdd(&words[kRetryWord], (uint32_t)__popcll(m2));
+        }
+        base1 = (uint32_t)__shfl((int)base1, 0, kWave);
+        base2 = (uint32_t)__shfl((int)base2, 0, kWave);
+        if (ok && one) {
+            const uint32_t a = ws[j];
+            hdr[base1 + (uint32_t)__popcll(m1 & lanemask_lt())] = make_uint4(j, a, ws[j + 1] - a, br.bdmin[b0]);
+        } else if (ok) {
+            retry[base2 + (uint32_t)__popcll(m2 & lanemask_lt())] = j;
+        }
+    }
+}
+
+// Sort one sub-bucket of u32 words s_k[lo, lo + cnt) (cnt <= N) in
+// registers; equal key bits (above the slot) = one group: U members and U
+// groups added to nu / ng
+template <int N>
+__device__ __forceinline__ void sort_sub_words(uint32_t* __restrict__ s_k, uint32_t lo, uint32_t cnt, uint32_t& nu,
+                                               uint32_t& ng) {
+    uint32_t v[N];
+#pragma unroll
+    for (int t = 0; t < N; ++t) v[t] = (uint32_t)t < cnt ? s_k[lo + t] : ~0u;
+    sort_net32<N>(v);
+    uint32_t eqm = 0;
+#pragma unroll
+    for (int t = 0; t + 1 < N; ++t) eqm |= ((v[t] ^ v[t + 1]) <= kSlotMask ? 1u : 0u) << t;
+    eqm &= (1u << (cnt - 1)) - 1u;
+#pragma unroll
+    for (int t = 0; t < N; ++t)
+        if ((uint32_t)t < cnt) s_k[lo + t] = v[t];
+    nu += (uint32_t)__popc(eqm | (eqm << 1));
+    ng += (uint32_t)__popc(eqm & ~(eqm << 1));
+}
+
+// a sub-bucket above kNet words (rare): insertion sort in LDS
+__device__ __forceinline__ void sort_sub_words_lds(uint32_t* __restrict__ s_k, uint32_t lo, uint32_t hi, uint32_t& nu,
+                                                   uint32_t& ng) {
+    for (uint32_t k = lo + 1; k < hi; ++k) {
+        const uint32_t x = s_k[k];
+        uint32_t y = k;
+        while (y > lo && s_k[y - 1] > x) {
+            s_k[y] = s_k[y - 1];
+            --y;
+        }
+        s_k[y] = x;
+    }
+    uint32_t pr = ~0u, cur = s_k[lo] >> kSlotBits;
+    for (uint32_t k = lo; k < hi; ++k) {
+        const uint32_t nx = k + 1 < hi ? (s_k[k + 1] >> kSlotBits) : ~0u;
+        const bool eqp = k > lo && pr == cur, eqn = k + 1 < hi && nx == cur;
+        nu += (eqp || eqn) ? 1u : 0u;
+        ng += (!eqp && eqn) ? 1u : 0u;
+        pr = cur;
+        cur = nx;
+    }
+}
+
+// The window's items into registers (slot le = l0 + 64 i; slots past m
+// re-read the last item, see load_raw)
+template <int ITEMS>
+__device__ __forceinline__ void load_items(const uint64_t* __restrict__ w_in, uint64_t a, uint32_t m,
+                                           uint64_t (&x)[ITEMS]) {
+    const uint32_t l0 = slot0<ITEMS>();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t le = l0 + i * kWave;
+        x[i] = w_in[a + (le < m ? le : m - 1)];
+    }
+}
+
+// bits: the plan's key span (br.bits1), kSubBits < bits <= kSubBits + kLowMax
+template <int BLOCK, int ITEMS, class Probe = NoProbe>
+__global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
+                                                       const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
+                                                       uint32_t ib, uint32_t* __restrict__ words,
+                                                       uint64_t* __restrict__ keys_out, uint32_t* __restrict__ sa_out,
+                                                       uint32_t* __restrict__ retry, SegOut so) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int CAP = BLOCK * ITEMS;
+    static_assert(CAP <= (1 << kSlotBits), "load slots");
+    __shared__ uint32_t s_k[CAP];                 // (key bits below the sub-bucket) << kSlotBits | load slot
+    __shared__ uint32_t s_x[CAP];                 // index of each load slot
+    __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
+    __shared__ uint32_t s_tmp[WAVES];
+    __shared__ uint32_t s_cm[WAVES];
+    __shared__ uint32_t s_ug[WAVES];
+    __shared__ uint32_t s_q[2];
+    __shared__ unsigned long long s_tot[3];   // heads, U, U groups of the workgroup's windows (thread 0)
+    constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
+    static_assert(WPT * 2 == 4 && WPT * 2 * BLOCK == kSubBuckets, "four sub-buckets per thread");
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint32_t nwin = words[kHdrWord];
+    const uint32_t low_bits = bits - kSubBits;
+    const uint32_t dsh = ib + low_bits;
+    const uint32_t lmask = (1u << low_bits) - 1u;
+    const uint64_t imask = (1ull << ib) - 1ull;
+    const uint64_t smask = (1ull << so.ksh) - 1ull;
+    auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
+    Probe probe;
+    if (threadIdx.x == 0) {
+        s_q[0] = atomicAdd(&words[kTicketWord], 1u);
+        s_tot[0] = s_tot[1] = s_tot[2] = 0;
+    }
+    __syncthreads();
+    // window numbers and headers are uniform: scalar registers
+    uint32_t q = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[0]);
+    if (q >= nwin) return;   // uniform
+    uint4 h = hdr[q];
+    uint64_t w[ITEMS];
+    load_items<ITEMS>(keys_in, h.y, h.z, w);
+    uint32_t par = 0;
+    for (;;) {
+        probe.mark(-1);
+        const uint32_t j = h.x, m = h.z;
+        const uint64_t a = h.y;
+        const uint64_t mn = (uint64_t)h.w << rb;
+        if (threadIdx.x == 0) s_q[par ^ 1u] = atomicAdd(&words[kTicketWord], 1u);   // the next window
+        for (int i = threadIdx.x; i < kSubBuckets / 2; i += BLOCK) s_cnt[i] = 0;
+        __syncthreads();
+        const uint32_t qn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[par ^ 1u]);
+        const bool more = qn < nwin;   // uniform
+        // the next window's header (needed at the prefetch point only); past
+        // the last window a dummy one-item window at 0, loaded but never
+        // used -- an unconditional load keeps the current items dead after
+        // the scatter (a conditional one kept them live through the sort)
+        uint4 hn = make_uint4(0u, 0u, 1u, 0u);
+        if (more) hn = hdr[qn];
+        probe.mark(0);
+        const uint32_t l0 = slot0<ITEMS>();
+        // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
+#pragma unroll
+        for (int i = 0; i < ITEMS; ++i) {
+            if (l0 + i * kWave < m) {
+                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+            }
+        }
+        __syncthreads();
+        probe.mark(1);
+        // exclusive scan of the counts and their maximum
+        uint32_t big = 0;
+        {
+            uint32_t c[2 * WPT], sum = 0, cm = 0;
+#pragma unroll
+            for (int x = 0; x < WPT; ++x) {
+                const uint32_t pw = s_cnt[WPT * dg + x];
+                c[2 * x] = pw & 0xFFFFu;
+                c[2 * x + 1] = pw >> 16;
+            }
+#pragma unroll
+            for (int x = 0; x < 2 * WPT; ++x) {
+                sum += c[x];
+                cm = c[x] > cm ? c[x] : cm;
+            }
+            const uint32_t inc = wave_inclusive_sum(sum);
+#pragma unroll
+            for (int o = kWave / 2; o > 0; o >>= 1) {
+                const uint32_t y = __shfl_xor(cm, o, kWave);
+                cm = y > cm ? y : cm;
+            }
+            if (lane == kWave - 1) s_tmp[wave] = inc;
+            if (lane == 0) s_cm[wave] = cm;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int x = 0; x < WAVES; ++x) {
+                off += (x < (int)wave) ? s_tmp[x] : 0u;
+                big = s_cm[x] > big ? s_cm[x] : big;
+            }
+            uint32_t b = off + inc - sum;
+#pragma unroll
+            for (int x = 0; x < WPT; ++x) {
+                const uint32_t b0 = b, b1 = b + c[2 * x];
+                s_cnt[WPT * dg + x] = b0 | (b1 << 16);
+                b = b1 + c[2 * x + 1];
+            }
+        }
+        __syncthreads();
+        probe.mark(2);
+        if (big > kMaxSub) {   // uniform: clustered keys -> the measured-span kernel
+            if (threadIdx.x == 0) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
+            __builtin_amdgcn_sched_barrier(0);
+            load_items<ITEMS>(keys_in, hn.y, hn.z, w);
+            __syncthreads();
+        } else {
+            // 2. scatter the 32-bit words into sub-buckets (any order inside
+            // one); the indices stay by load slot
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t le = l0 + i * kWave;
+                if (le < m) {
+                    const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                    const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                    s_k[(old >> (16 * (sb & 1))) & 0xFFFFu] = (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
+                    s_x[le] = (uint32_t)(w[i] & imask);
+                }
+            }
+            // ... the window is in LDS: the next window's loads go out now (a
+            // scheduling barrier: hoisted above the scatter, they would hold
+            // a second window of registers)
+            __builtin_amdgcn_sched_barrier(0);
+            load_items<ITEMS>(keys_in, hn.y, hn.z, w);
+            __syncthreads();
+            probe.mark(3);
+            // ... then each thread sorts its four consecutive sub-buckets,
+            // largest first, with 4 / 8 / 12 / 16-input networks by the
+            // wave's largest sub-bucket of this rank (larger: insertion)
+            uint32_t nu = 0, ng = 0;
+            uint32_t umask = 0;   // bit k: sub-bucket sb0 + k holds a group
+            const uint32_t sb0 = 2 * WPT * dg;
+            uint32_t order = 0;
+            {
+                uint32_t o[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const uint32_t sb = sb0 + k;
+                    o[k] = ((end_of(sb) - (sb ? end_of(sb - 1) : 0u)) << 2) | (uint32_t)k;
+                }
+                sort_net32<4>(o);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) order |= (o[3 - k] & 3u) << (2 * k);
+            }
+#pragma unroll 1
+            for (uint32_t i = 0; i < 4; ++i) {
+                const uint32_t sb = sb0 + ((order >> (2 * i)) & 3u);
+                const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb), cnt = hi - lo;
+                const bool wide4 = __ballot(cnt > 4u) != 0ull, wide8 = __ballot(cnt > 8u) != 0ull,
+                           wide12 = __ballot(cnt > 12u) != 0ull;   // uniform
+                if (cnt == 0) continue;
+                const uint32_t nu0 = nu;
+                if (!wide4) sort_sub_words<4>(s_k, lo, cnt, nu, ng);
+                else if (!wide8) sort_sub_words<8>(s_k, lo, cnt, nu, ng);
+                else if (!wide12) sort_sub_words<12>(s_k, lo, cnt, nu, ng);
+                else if (cnt <= (uint32_t)kNet) sort_sub_words<kNet>(s_k, lo, cnt, nu, ng);
+                else sort_sub_words_lds(s_k, lo, hi, nu, ng);
+                if (nu != nu0) umask |= 1u << (sb - sb0);
+                // the sorted key1 of this sub-bucket's every-2^ksh-th SA
+                // positions, from the sorted words (a global load here would
+                // make the store phase wait for the next window's loads)
+                for (uint64_t p = ((a + lo + smask) >> so.ksh) << so.ksh; p < a + hi; p += smask + 1)
+                    keys_out[p >> so.ksh] =
+                        mn + (((uint64_t)sb << low_bits) | (s_k[(uint32_t)(p - a)] >> kSlotBits));
+            }
+            probe.mark(4);
+            // 3. U / U-group offsets (one scan of both; heads = m - U + G)
+            uint32_t bu, bg, tu_w, tg_w;
+            {
+                const uint32_t iug = wave_inclusive_sum(nu | (ng << 16));
+                if (lane == kWave - 1) s_ug[wave] = iug;
+                __syncthreads();
+                uint32_t oug = 0, tug = 0;
+#pragma unroll
+                for (int x = 0; x < WAVES; ++x) {
+                    const uint32_t xug = s_ug[x];
+                    oug += (x < (int)wave) ? xug : 0u;
+                    tug += xug;
+                }
+                tu_w = tug & 0xFFFFu;
+                tg_w = tug >> 16;
+                bu = (oug & 0xFFFFu) + (iug & 0xFFFFu) - nu;
+                bg = (oug >> 16) + (iug >> 16) - ng;
+            }
+            if (so.rank) {
+                if (threadIdx.x == 0) {
+                    so.cnt_u[j] = tu_w;
+                    so.cnt_g[j] = tg_w;
+                    s_tot[0] += m - tu_w + tg_w;
+                    s_tot[1] += tu_w;
+                    s_tot[2] += tg_w;
+                }
+                // the unsorted members of this thread's sub-buckets (rare)
+                if (umask) {
+                    uint32_t ku = bu, kg = bg;
+                    for (uint32_t um = umask; um; um &= um - 1u) {
+                        const uint32_t sb = sb0 + (uint32_t)__builtin_ctz(um);
+                        const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
+                        uint32_t head = lo, pr = ~0u;
+                        for (uint32_t k = lo; k < hi; ++k) {
+                            const uint32_t v = s_k[k], r = v >> kSlotBits;
+                            const uint32_t nx = k + 1 < hi ? (s_k[k + 1] >> kSlotBits) : ~0u;
+                            const bool eqp = k > lo && pr == r, eqn = k + 1 < hi && nx == r;
+                            if (!eqp) head = k;
+                            if (!eqp && eqn) ++kg;
+                            if (eqp || eqn) {
+                                const uint32_t xi = s_x[v & kSlotMask];
+                                const uint32_t rv = (uint32_t)(so.rank_off + a + head + 1u);
+                                if (so.tmp_rank) so.tmp_rank[a + ku] = rv;
+                                else so.rank[xi] = rv;
+                                atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
+                                so.tmp_pos[a + ku] = (uint32_t)(a + k);
+                                so.tmp_idx[a + ku] = xi;
+                                so.tmp_g[a + ku] = kg - 1u;
+                                ++ku;
+                            }
+                            pr = r;
+                        }
+                    }
+                }
+            }
+            probe.mark(5);
+            // 4. the SA, coalesced: the index of each sorted word's load slot
+            // (the U / G scan's barrier follows every thread's sort)
+#pragma unroll 2
+            for (int i = 0; i < ITEMS; ++i) {
+                const uint32_t le = l0 + i * kWave;
+                if (le < m) sa_out[a + le] = s_x[s_k[le] & kSlotMask];
+            }
+            __syncthreads();   // s_k / s_x / s_cnt reuse by the next window
+            probe.mark(6);
+        }
+        if (!more) break;
+        q = qn;
+        h = hn;
+        par ^= 1u;
+    }
+    probe.flush(words);
+    __syncthreads();
+    flush_totals(words, s_tot[0], s_tot[1], s_tot[2]);
 }
 
 // The skewed windows: stable LSD passes of 8 bits over the key span, each an

@@ -464,16 +464,32 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* const retry = cnt_g + 2 * nw + 2;
     BucketRel br_measured = br;
     br_measured.bits1 = 0;
+    // the fixed-span 32-bit local sort (k_bucket_sort): the key bits below a
+    // sub-bucket fit beside the load slot, and buckets are large enough that
+    // windows hold one bucket each (n / 2^bb >= 4 window strides)
+    const bool fast32 = br.bits1 > (uint32_t)kSubBits && br.bits1 - kSubBits <= kLowMax &&
+                        (m >> bp.bs.bb) >= 4 * kWinStride && !std::getenv("SA_NO_FAST32");
+    // one-bucket window headers after the retry list (16-byte aligned; 11 nw + 8 <= capacity)
+    uint4* const hdr = reinterpret_cast<uint4*>(((uintptr_t)(retry + nw + 4) + 15) & ~(uintptr_t)15);
     auto local_sort = [&](const SegOut& o) {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
         // (no SA_HIP here: its error return would make the lambda non-void)
-        (void)hipMemsetAsync(c->words + kRetryWord, 0, 4, s);
-        hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
-                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words, bp.ib,
-                           c->keys[0], d_sa, skew, o, br.bits1 ? retry : (uint32_t*)nullptr, 7u);
-        if (br.bits1)   // rare: a small grid loops over the retried windows
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(std::min<uint32_t>(g, 1024)), dim3(kBsBlock),
-                               0, s, (const uint64_t*)c->keys_u, br_measured, (const uint32_t*)ws,
+        (void)hipMemsetAsync(c->words + kRetryWord, 0, 12, s);   // retry count, one-bucket windows, ticket
+        if (fast32) {
+            const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024));
+            hipLaunchKernelGGL(k_window_split, dim3(gs), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)ws,
+                               br, c->words, hdr, retry, 1u);
+            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(kBsWpc * (uint32_t)c->cus), dim3(kBsBlock), 0, s,
+                               (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1, bp.ib, c->words,
+                               c->keys[0], d_sa, retry, o);
+        } else {
+            hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
+                               (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words,
+                               bp.ib, c->keys[0], d_sa, skew, o, br.bits1 ? retry : (uint32_t*)nullptr, 7u);
+        }
+        if (br.bits1)   // rare: a small grid loops over the retried windows (measured span)
+            hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(std::min<uint32_t>(g, 1024)),
+                               dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, br_measured, (const uint32_t*)ws,
                                (const uint32_t*)retry, c->words, bp.ib, c->keys[0], d_sa, skew, o, (uint32_t*)nullptr,
                                (uint32_t)kRetryWord);
         // skewed windows are rare: a small grid loops over them (one
