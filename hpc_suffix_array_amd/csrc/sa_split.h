@@ -24,10 +24,9 @@
 #include "sa_onesweep.h"
 
 // When the bucket passes take the next tile's ticket (A/B at 2^30 DNA):
-// pass 1 (SA_EARLY_TICKET1) 0 = after the claims, 1 = after the digit
-// staging with the next tile's text loads right behind it (5.34 -> 5.71 ms:
-// slower), 2 = the ticket there, the loads after the claims; pass 2
-// (SA_EARLY_TICKET2) 0 = after the claims, 1 = at the start of the unit
+// pass 1 takes it after the digit staging and loads the next tile's text
+// after the claims (the loads right behind the ticket: 5.34 -> 5.71 ms,
+// slower); pass 2 takes it at the start of the unit, not after the claims
 // (5.885 -> 5.83 ms)
 // diagnostic: per-phase clock64 spans of k_split_seg printed by two
 // workgroups (scatter 36 %, write 22 %, base wait 18 %, ranking 12 %, claims
@@ -63,17 +62,6 @@
 #endif
 #ifndef SA_TEXT_PROF
 #define SA_TEXT_PROF 0
-#endif
-// the first pass's claims (atomic cursors) are waited for after the LDS
-// staging instead of before it (phase clocks: claims 15 % of the pass)
-#ifndef SA_LATE_CLAIM1
-#define SA_LATE_CLAIM1 1
-#endif
-#ifndef SA_EARLY_TICKET1
-#define SA_EARLY_TICKET1 2
-#endif
-#ifndef SA_EARLY_TICKET2
-#define SA_EARLY_TICKET2 1
 #endif
 
 namespace sa {
@@ -469,17 +457,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 s_dcw[w] = o;
             }
         }
-#if SA_EARLY_TICKET1
         // the next tile's ticket now: its round trip overlaps this tile's key
-        // computation (no look-back depends on the ticket order)
+        // computation (no look-back depends on the ticket order); its text
+        // loads wait until after the claims (loading right here was slower)
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
-#endif
         __syncthreads();
         TEXT_STAMP(0)
-#if SA_EARLY_TICKET1 == 1
-        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
-        load(tn < tiles ? tn : tiles - 1);
-#endif
         // key1 of positions tb + ITEMS dg + j (D < 64 sigma 2^bb <= 2^32 rolls
         // in 32 bits; the remainder in 64)
         uint64_t k[ITEMS];
@@ -535,8 +518,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         __syncthreads();
         TEXT_STAMP(1)
         uint32_t tile_cnt = 0;
-        // SA_LATE_CLAIM1: the claim, read after the LDS staging (no zero
-        // initialisation: a register write there is a write-after-write on
+        // the claim, waited for after the LDS staging (claims were 15 % of the
+        // pass before; no zero initialisation: a register write there is a write-after-write on
         // the previous tile's pending claim, and the compiler drained every
         // memory operation for it)
         uint32_t clm, dbase;
@@ -546,12 +529,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             // the pass need not be stable, so a tile's place in each digit
             // is claimed from a cursor (one atomic round trip, whatever the
             // other tiles do) instead of a look-back
-#if SA_LATE_CLAIM1
             dbase = digit_base[dg];
             clm = tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u;
-#else
-            s_gofs[dg] = digit_base[dg] + (tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u);
-#endif
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
@@ -564,18 +543,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
             if (dg == (uint32_t)RADIX - 1) s_kept = off + inc;   // pairs kept in this tile
         }
-#if SA_EARLY_TICKET1 == 1
-        __syncthreads();
-#else
-        // the next tile's ticket (unless taken already) and text loads
-#if SA_EARLY_TICKET1 == 0
-        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
-#endif
+        // the next tile's text loads
         __syncthreads();
         TEXT_STAMP(2)
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         load(tn < tiles ? tn : tiles - 1);
-#endif
         // PK8: the item is built here, not in the key loop (its extra live
         // values there spilled 19 VGPRs): the second pass's digit (the
         // bucket's high bits; one GPU: local = global bucket), key1 below its
@@ -598,11 +570,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 }
             }
         }
-#if SA_LATE_CLAIM1
         // the claims' round trips overlapped the staging (only the writes
         // need the tile's places)
         if (dg < (uint32_t)RADIX) s_gofs[dg] = dbase + clm;
-#endif
         __syncthreads();
         TEXT_STAMP(3)
         const uint32_t kept = s_kept;
@@ -915,11 +885,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
 #define SEG_STAMP(k)
 #endif
     while (u < units) {
-#if SA_EARLY_TICKET2
         // the next unit's ticket: its round trip overlaps the ranking and
         // claims (read after the claims' barrier)
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
-#endif
         // ranks within the unit (any order: one segment, one value of l)
         uint32_t dr[ITEMS];
 #pragma unroll
@@ -987,10 +955,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                 }
             }
         }
-        // the next unit's ticket and loads (see k_split)
-#if !SA_EARLY_TICKET2
-        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
-#endif
+        // the next unit's loads (see k_split)
         __syncthreads();
         const uint32_t un = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         SEG_STAMP(3)
