@@ -212,7 +212,27 @@ def reference_schedule(b, d_text, n, d_sa, sptr, a, torch, dev, reps: int = 2) -
     ms = 1e3 * statistics.median(times)
     return {"ms_per_step": round(ms, 3), "value": n / (ms / 1e3), "rounds": st["rounds"],
             "ms_per_round": [round(x, 3) for x in st["round_ms"]], "prefix_len_per_round": st["prefix_len"],
-            "passes_per_round": st["passes"], "verified": b.check(d_text, n, d_sa, stream=sptr)}
+            "passes_per_round": st["passes"], "distinct_per_round": st["distinct"],
+            "roofline_per_round": model_rounds(n, st["distinct"], st["round_ms"]),
+            "kernels_ms": {k: round(v["ms"], 3) for k, v in st["kernels"].items() if v["launches"]},
+            "verified": b.check(d_text, n, d_sa, stream=sptr)}
+
+
+def model_rounds(n: int, distinct, round_ms) -> list:
+    """SURVEY.md 8(d)'s per-round model against the measured round times:
+    B_j = n (3 rb + 2 S (P_j + 1)), P_j = ceil(2 w_j / 8), w_j = bit width
+    of D_{j-1} with D_0 = 256 (manber_myers.c:94), rb = 4, S = 12 below 2^31
+    (8 / 24 above); frac = B_j / t_j / the 8 TB/s HBM peak."""
+    rb, S = (4, 12) if n < (1 << 31) else (8, 24)
+    out, prev = [], 256
+    for d, ms in zip(distinct, round_ms):
+        P = -(-2 * int(prev).bit_length() // 8)
+        B = n * (3 * rb + 2 * S * (P + 1))
+        gbs = B / (ms / 1e3) / 1e9 if ms > 0 else None
+        out.append({"P_model": P, "model_bytes": B, "ms": round(ms, 3), "gbs": gbs and round(gbs, 1),
+                    "frac": gbs and round(gbs / HBM_PEAK_GBS, 4)})
+        prev = d
+    return out
 
 
 def run_single(a, torch, dev, world, rank, barrier):

@@ -36,7 +36,9 @@
 #include "sa_kernels.h"
 #include "sa_lcp.h"
 #include "sa_onesweep.h"
+#include "sa_permute.h"
 #include "sa_split.h"
+#include "sa_lsd.h"
 
 namespace sa {
 
@@ -122,6 +124,7 @@ struct sa_context {
     uint32_t* u_g[2] = {nullptr, nullptr};
     uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
     uint32_t* os = nullptr;                     // onesweep ghist / digit bases / tickets
+    uint32_t* lsd = nullptr;                    // k_lsd ghist [8][1024] | bases [8][1024] | tickets [8]
     uint32_t* segw = nullptr;                   // second bucket pass: per-segment cursors / bases / flags
     uint64_t* states = nullptr;                 // onesweep tile states [tiles][256]
     uint32_t epoch = 0;                         // onesweep state tag of the last pass
@@ -456,6 +459,169 @@ static void record_round(sa_stats* st, float ms, uint64_t D, uint32_t P, uint64_
 // ---------------------------------------------------------------------------
 // reference schedule: manber_myers.c:88-125 round for round
 // ---------------------------------------------------------------------------
+// the re-rank as a permutation (sa_permute.h) from this many suffixes; below
+// it rank[] stays inside the L2s and one random scatter (k_rerank) is cheaper
+// (SA_PERM_MIN overrides it, e.g. for tests at small n)
+constexpr int kPermErrWord = 13;
+static uint64_t perm_min_n() {
+    const char* e = std::getenv("SA_PERM_MIN");
+    return e ? std::strtoull(e, nullptr, 0) : (1ull << 22);
+}
+
+static PermPlan plan_perm(uint64_t n) {
+    PermPlan p;
+    const uint32_t lg = bit_width(n > 1 ? n - 1 : 1);   // ceil(log2 n)
+    p.s2 = kPermSub;
+    p.s1 = std::max<uint32_t>(p.s2, lg > 8 ? lg - 8 : 0);
+    p.nb1 = (uint32_t)((n + (1ull << p.s1) - 1) >> p.s1);
+    p.nsub = 1u << (p.s1 - p.s2);
+    p.tpb = (uint32_t)(((1ull << p.s1) + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems));
+    return p;
+}
+
+// rank[idx[p]] = dense rank of sorted position p, through the two key
+// buffers (the sorted keys are read by the first step and then free)
+static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa, const Chunking& ch,
+                          hipStream_t s, Timer& tm, sa_stats* st, uint32_t kshift = 0) {
+    const uint64_t n = ch.n;
+    const PermPlan p = plan_perm(n);
+    if (p.nb1 > 256 || p.nsub > kPermMaxSub || 256ull + (uint64_t)p.nb1 * p.nsub > (uint64_t)kRadix * kMaxChunks)
+        return set_err(SA_E_INTERNAL, "permutation plan out of range (n=%llu)", (unsigned long long)n);
+    uint64_t* other = sorted == c->keys[0] ? c->keys[1] : c->keys[0];
+    uint32_t* cur1 = c->hist;          // the chunk histograms are free after the sort
+    uint32_t* cur2 = c->hist + 256;
+    SA_HIP(hipMemsetAsync(c->hist, 0, (256ull + (uint64_t)p.nb1 * p.nsub) * 4, s));
+    tm.begin(SA_K_RERANK);
+    if (kshift)   // packed (key << kshift | idx) items
+        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, true>), dim3(ch.chunks), dim3(kPermBlock), 0, s,
+                           (const uint64_t*)sorted, d_sa, ch, (const uint32_t*)c->counts, p.s1, kshift, cur1, other);
+    else
+        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, false>), dim3(ch.chunks), dim3(kPermBlock), 0, s,
+                           (const uint64_t*)sorted, d_sa, ch, (const uint32_t*)c->counts, p.s1, 0u, cur1, other);
+    const uint64_t* placed = other;
+    if (p.s1 > p.s2) {
+        hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3(p.nb1 * p.tpb), dim3(kPermBlock), 0, s,
+                           (const uint64_t*)other, n, p.s1, p.s2, p.tpb, cur2, sorted);
+        placed = sorted;
+    }
+    hipLaunchKernelGGL((k_perm_place<kPermBlock>), dim3((uint32_t)((n + (1ull << kPermSub) - 1) >> kPermSub)),
+                       dim3(kPermBlock), 0, s, placed, n, c->rank, c->words + kPermErrWord);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_RERANK, (p.s1 > p.s2 ? 48ull : 32ull) * n - (kshift ? 4ull * n : 0ull));
+    return SA_OK;
+}
+
+// ---------------------------------------------------------------------------
+// the reference schedule's LSD sort (sa_lsd.h)
+// ---------------------------------------------------------------------------
+static uint32_t* lsd_ghist(sa_context* c) { return c->lsd; }
+static uint32_t* lsd_base(sa_context* c) { return c->lsd + kMaxPasses * kLsdMaxRadix; }
+static uint32_t* lsd_tickets(sa_context* c) { return c->lsd + 2 * kMaxPasses * kLsdMaxRadix; }
+
+// widest digit of the plan (SA_LSD_MAXBITS=8 restores 8-bit digits, A/B)
+static uint32_t lsd_max_bits() {
+    const char* e = std::getenv("SA_LSD_MAXBITS");
+    const uint32_t b = e ? (uint32_t)std::atoi(e) : 10u;
+    return std::min<uint32_t>(10, std::max<uint32_t>(8, b));
+}
+
+// B key bits above bit `base`: the pass count and widths of least relative
+// cost, a pass of 9 / 10 bits costing ~1.2 / 1.45 of an 8-bit one (longer
+// match-any, shorter digit runs per tile)
+static LsdPlan lsd_plan(uint32_t B, uint32_t base) {
+    const uint32_t maxb = lsd_max_bits();
+    auto cost = [](uint32_t w) { return w <= 8 ? 1.0 : w == 9 ? 1.2 : 1.45; };
+    LsdPlan pl{};
+    double best = 1e30;
+    for (uint32_t p = std::max<uint32_t>(1, (B + maxb - 1) / maxb); p <= std::max<uint32_t>(1, (B + 7) / 8); ++p) {
+        double cst = 0;
+        for (uint32_t i = 0; i < p; ++i) cst += cost(B / p + (i < B % p ? 1u : 0u));
+        if (cst < best - 1e-9) {
+            best = cst;
+            pl.P = p;
+        }
+    }
+    uint32_t sh = base;
+    for (uint32_t i = 0; i < pl.P; ++i) {
+        pl.bits[i] = std::max<uint32_t>(1, B / pl.P + (i < B % pl.P ? 1u : 0u));
+        pl.shift[i] = sh;
+        sh += pl.bits[i];
+    }
+    return pl;
+}
+
+template <class K>
+static int persist_grid(sa_context* c, K kernel) {
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kLsdBlock, 0) != hipSuccess || nb < 1) nb = 1;
+    return c->cus * nb;
+}
+
+template <class Src, bool PACKED>
+static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits, const uint32_t* base,
+                     uint32_t* ticket, uint64_t* ok, uint32_t* ov, hipStream_t s) {
+    const uint32_t epoch = next_epoch(c, s);
+    const uint64_t tiles = (n + kLsdTile - 1) / kLsdTile;
+#define SA_LSD_LAUNCH(RB)                                                                                   \
+    do {                                                                                                    \
+        auto kern = k_lsd<Src, RB, PACKED>;                                                                 \
+        static int grid = 0;                                                                                \
+        if (!grid) grid = persist_grid(c, kern);                                                            \
+        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, (uint64_t)grid)), dim3(kLsdBlock), 0, s, \
+                           src, n, shift, nbits, base, c->states, ticket, epoch, ok, ov, c->words + 4);      \
+    } while (0)
+    if (nbits <= 8) SA_LSD_LAUNCH(8);
+    else if (nbits == 9) SA_LSD_LAUNCH(9);
+    else SA_LSD_LAUNCH(10);
+#undef SA_LSD_LAUNCH
+}
+
+// Stable LSD sort of n pairs by the plan's digits, pass 0 reading `first`.
+// PACKED: one item buffer ping-pong; else keys + values, the last pass
+// writing its values into vals_final.  *sorted = the sorted key / item buffer.
+template <bool PACKED, class Src0>
+static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan& pl, uint32_t* vals_final,
+                    uint32_t* vals_other, hipStream_t s, Timer& tm, sa_stats* st, uint64_t** sorted) {
+    if (pl.P < 1 || pl.P > kMaxPasses) return set_err(SA_E_INTERNAL, "%u radix passes", pl.P);
+    uint64_t* kb[2] = {c->keys[0], c->keys[1]};
+    uint32_t* vb[2];
+    vb[(pl.P - 1) & 1] = vals_final;
+    vb[pl.P & 1] = vals_other;
+    SA_HIP(hipMemsetAsync(c->lsd, 0, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4, s));
+    tm.begin(SA_K_HIST_FIRST);
+    hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 1024)),
+                       dim3(kBlock), 0, s, first, n, pl, lsd_ghist(c));
+    tm.end();
+    add_bytes(st, SA_K_HIST_FIRST, 8 * n);
+    tm.begin(SA_K_SCAN);
+    hipLaunchKernelGGL(k_lsd_base, dim3(pl.P), dim3(1024), 0, s, (const uint32_t*)lsd_ghist(c), pl, lsd_base(c));
+    tm.end();
+    const uint64_t pair = PACKED ? 8 : 12;
+    for (uint32_t p = 0; p < pl.P; ++p) {
+        const uint32_t* base = lsd_base(c) + p * kLsdMaxRadix;
+        if (p == 0) {
+            tm.begin(SA_K_SCATTER_FIRST);
+            lsd_pass<Src0, PACKED>(c, first, n, pl.shift[0], pl.bits[0], base, lsd_tickets(c), kb[0], vb[0], s);
+            tm.end();
+            add_bytes(st, SA_K_SCATTER_FIRST, (8 + pair) * n);
+        } else {
+            tm.begin(SA_K_SCATTER_KEYS);
+            if constexpr (PACKED)
+                lsd_pass<SrcItems, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], base,
+                                         lsd_tickets(c) + p, kb[p & 1], nullptr, s);
+            else
+                lsd_pass<SrcKeys, false>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p],
+                                         base, lsd_tickets(c) + p, kb[p & 1], vb[p & 1], s);
+            tm.end();
+            add_bytes(st, SA_K_SCATTER_KEYS, 2 * pair * n);
+        }
+    }
+    SA_HIP(hipGetLastError());
+    *sorted = kb[(pl.P - 1) & 1];
+    return SA_OK;
+}
+
 static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                            sa_stats* st, Timer& tm) {
     Events ev;
@@ -492,17 +658,32 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     if (st) st->sigma = (int32_t)sigma;
 
     uint64_t D = sigma;   // ranks 1..sigma (manber_myers.c:94 sizes its bins for 256)
+    const uint64_t perm_min = perm_min_n();
+    const uint32_t ib = std::max<uint32_t>(1, bit_width(n - 1));   // index bits of a packed item
+    bool used_perm = false;
     for (uint64_t h = 1;; h *= 2) {
         SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t w = bit_width(D);          // ranks are 0..D
-        SA_TRACE("reference round h=%llu D=%llu w=%u", (unsigned long long)h, (unsigned long long)D, w);
+        // (key << ib | index) items while they fit 64 bits (onesweep only)
+        const bool packed = c->radix == 0 && 2 * w + ib <= 64;
+        SA_TRACE("reference round h=%llu D=%llu w=%u%s", (unsigned long long)h, (unsigned long long)D, w,
+                 packed ? " packed" : "");
         SrcRank src{c->rank, n, h, w};
         uint64_t* sorted;
         uint32_t P;
-        rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &sorted, &P);
+        if (c->radix == 0) {
+            const LsdPlan pl = lsd_plan(2 * w, packed ? ib : 0);
+            P = pl.P;
+            rc = packed ? lsd_sort<true>(c, SrcRankPk{c->rank, n, h, w, ib}, n, pl, d_sa, c->vals_alt, s, tm, st,
+                                         &sorted)
+                        : lsd_sort<false>(c, src, n, pl, d_sa, c->vals_alt, s, tm, st, &sorted);
+        } else {
+            rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &sorted,
+                            &P);
+        }
         if (rc) return rc;
         tm.begin(SA_K_HEADS);
-        hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts);
+        hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts, packed ? ib : 0u);
         tm.end();
         tm.begin(SA_K_HEADS_SCAN);
         hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, c->counts, ch.chunks, c->words);
@@ -515,13 +696,27 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
         const uint64_t Dn = c->host_words[0];
         const bool done = (Dn == n);                  // manber_myers.c:113
-        if (!done) {
+        if (done && packed) {
             tm.begin(SA_K_RERANK);
-            hipLaunchKernelGGL(k_rerank, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, (const uint32_t*)d_sa, ch,
-                               (const uint32_t*)c->counts, c->rank);
+            hipLaunchKernelGGL(k_items_to_sa, dim3((uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192)),
+                               dim3(kBlock), 0, s, (const uint64_t*)sorted, n, ib, d_sa);
             tm.end();
             SA_HIP(hipGetLastError());
-            add_bytes(st, SA_K_RERANK, 16 * n);
+            add_bytes(st, SA_K_RERANK, 12 * n);
+        }
+        if (!done) {
+            if (packed || n >= perm_min) {
+                used_perm = true;
+                rc = rerank_permute(c, sorted, d_sa, ch, s, tm, st, packed ? ib : 0u);
+                if (rc) return rc;
+            } else {
+                tm.begin(SA_K_RERANK);
+                hipLaunchKernelGGL(k_rerank, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, (const uint32_t*)d_sa, ch,
+                                   (const uint32_t*)c->counts, c->rank);
+                tm.end();
+                SA_HIP(hipGetLastError());
+                add_bytes(st, SA_K_RERANK, 16 * n);
+            }
         }
         SA_HIP(hipEventRecord(ev.e[1], s));
         SA_HIP(hipEventSynchronize(ev.e[1]));
@@ -532,6 +727,11 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         if (done) break;
         if (h > n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)", (unsigned long long)h);
         D = Dn;
+    }
+    if (used_perm) {
+        SA_HIP(hipMemcpyAsync(c->host_words + kPermErrWord, c->words + kPermErrWord, 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipStreamSynchronize(s));
+        if (c->host_words[kPermErrWord]) return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix");
     }
     return SA_OK;
 }
@@ -1200,6 +1400,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
+        hipMalloc(&c->lsd, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4) != hipSuccess ||
         hipMalloc(&c->segw, (kBstartOff + 2 * kBstartWords) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 16384, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -1233,6 +1434,7 @@ void sa_context_destroy(sa_context* c) {
     hipFree(c->alpha);
     hipFree(c->code);
     hipFree(c->os);
+    hipFree(c->lsd);
     hipFree(c->segw);
     hipFree(c->hist);
     hipFree(c->totals);

@@ -665,35 +665,39 @@ __global__ __launch_bounds__(kBlock) void k_scatter(Src src, Chunking ch, uint32
 // Each wave owns a contiguous 1024-key slice of the tile: rows of 64 keys,
 // ballot + popcount give the in-row prefix.
 // ---------------------------------------------------------------------------
+// kshift: the key is the word's bits above kshift (packed (key, idx) items of
+// the reference schedule, sa_onesweep.h k_lsd; 0 otherwise); key_out is the
+// whole word, prev_last the previous row's last KEY.
 __device__ __forceinline__ uint64_t wave_heads(const uint64_t* __restrict__ keys, uint64_t row0,
                                                uint64_t lim, uint64_t& prev_last, uint64_t& key_out,
-                                               bool& ok_out) {
+                                               bool& ok_out, uint32_t kshift = 0) {
     const uint64_t e = row0 + lane_id();
     const bool ok = e < lim;
-    const uint64_t key = ok ? keys[e] : 0ull;
+    const uint64_t word = ok ? keys[e] : 0ull;
+    const uint64_t key = word >> kshift;
     uint64_t prev = __shfl_up(key, 1, kWave);
     if (lane_id() == 0) prev = prev_last;
     prev_last = __shfl(key, kWave - 1, kWave);
     const bool head = ok && (e == 0 || key != prev);
-    key_out = key;
+    key_out = word;
     ok_out = ok;
     return __ballot(head);
 }
 
 __global__ __launch_bounds__(kBlock) void k_heads(const uint64_t* __restrict__ keys, Chunking ch,
-                                                  uint32_t* __restrict__ counts) {
+                                                  uint32_t* __restrict__ counts, uint32_t kshift = 0) {
     __shared__ uint32_t s_tmp[kWaves];
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
     uint32_t cnt = 0;
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave_id() * kWaveTile;
-        uint64_t prev_last = (w0 > 0 && w0 < e1) ? keys[w0 - 1] : 0ull;
+        uint64_t prev_last = (w0 > 0 && w0 < e1) ? keys[w0 - 1] >> kshift : 0ull;
 #pragma unroll 4
         for (int j = 0; j < kItems; ++j) {
             uint64_t key;
             bool ok;
-            const uint64_t m = wave_heads(keys, w0 + (uint64_t)j * kWave, e1, prev_last, key, ok);
+            const uint64_t m = wave_heads(keys, w0 + (uint64_t)j * kWave, e1, prev_last, key, ok, kshift);
             cnt += (uint32_t)__popcll(m);
         }
     }

@@ -1,0 +1,248 @@
+// sa_lsd.h -- the reference schedule's per-round LSD radix sort
+// (radix_sort_suffixes_seq, manber_myers.c:37-48: a stable counting pass on
+// rank[1], then on rank[0]) as single-pass digit scatters over the packed
+// key (rank[i] << w) | rank[i + h].
+//
+// Against k_onesweep (sa_onesweep.h, one 4096-pair tile per workgroup):
+//   * persistent workgroups taking 8192-pair tiles from a ticket in order,
+//     the next tile's loads in flight during the look-back, the LDS staging
+//     and the writes (the structure of sa_split.h's k_split; same deadlock
+//     argument: a tile waits only on tiles of running workgroups);
+//   * stable ranks from per-wave match-any ballots (the counting sort's
+//     stability, :27-31, is what LSD needs; LDS atomics would not keep it);
+//   * digits of 8 to 10 bits, the widths chosen per round by lsd_plan
+//     (sa_build.hip), so an 18-bit key takes two passes instead of three;
+//   * PACKED: while key bits + index bits <= 64 the pass moves one 64-bit
+//     item (key << ib | index) -- 16 bytes per pair and pass instead of 24.
+#pragma once
+#include "sa_split.h"
+
+namespace sa {
+
+constexpr int kLsdBlock = 1024;
+constexpr int kLsdItems = 8;                        // 8192 pairs per tile
+constexpr int kLsdTile = kLsdBlock * kLsdItems;
+constexpr int kLsdMaxRadix = 1024;
+
+// the passes of one sort: digit p is bits [shift[p], shift[p] + bits[p])
+struct LsdPlan {
+    uint32_t P;
+    uint32_t shift[kMaxPasses];
+    uint32_t bits[kMaxPasses];
+};
+
+// First pass of a PACKED round: item = ((rank[i] << w | rank[i+h]) << ib) | i.
+struct SrcRankPk {
+    const uint32_t* __restrict__ rank;
+    uint64_t n;
+    uint64_t h;
+    uint32_t w, ib;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const {
+        const uint64_t r0 = rank[e];
+        const uint64_t r1 = (e + h < n) ? rank[e + h] : 0u;
+        return (((r0 << w) | r1) << ib) | e;
+    }
+    __device__ __forceinline__ uint32_t val(uint64_t) const { return 0u; }
+};
+
+// Later passes of a PACKED round: the items themselves.
+struct SrcItems {
+    const uint64_t* __restrict__ keys;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const { return keys[e]; }
+    __device__ __forceinline__ uint32_t val(uint64_t) const { return 0u; }
+};
+
+// Digit totals of every pass of the plan in one read of the first source
+// (the multiset of keys is the same in every pass); one atomic per run of
+// equal digits across neighbouring lanes (hist_add_runs: a degenerate
+// text's equal keys would otherwise put 64 lanes on one bin).
+template <class Src>
+__global__ __launch_bounds__(kBlock) void k_lsd_hist(Src src, uint64_t n, LsdPlan plan,
+                                                     uint32_t* __restrict__ ghist) {
+    __shared__ uint32_t s_h[kMaxPasses * kLsdMaxRadix];
+    for (uint32_t i = threadIdx.x; i < plan.P * kLsdMaxRadix; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = src.key(e);
+        const uint32_t nact = (uint32_t)__popcll(__ballot(1));
+        for (uint32_t p = 0; p < plan.P; ++p) {
+            const uint32_t d = (uint32_t)(k >> plan.shift[p]) & ((1u << plan.bits[p]) - 1u);
+            const uint32_t dl = __shfl_up(d, 1, 64);
+            const bool head = lane == 0 || dl != d;
+            const uint64_t hm = __ballot(head) & above;
+            const uint32_t next = hm ? (uint32_t)__ffsll((long long)hm) - 1u : nact;
+            if (head) atomicAdd(&s_h[p * kLsdMaxRadix + d], next - lane);
+        }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < plan.P * kLsdMaxRadix; i += kBlock)
+        if (s_h[i]) atomicAdd(&ghist[i], s_h[i]);
+}
+
+// base[p][d] = exclusive scan of ghist[p][..] (one 1024-thread workgroup per pass)
+__global__ __launch_bounds__(1024) void k_lsd_base(const uint32_t* __restrict__ ghist, LsdPlan plan,
+                                                   uint32_t* __restrict__ base) {
+    __shared__ uint32_t s_tmp[16];
+    const uint32_t p = blockIdx.x, i = threadIdx.x;
+    const uint32_t bins = 1u << plan.bits[p];
+    const uint32_t x = i < bins ? ghist[p * kLsdMaxRadix + i] : 0u;
+    const uint32_t inc = wave_inclusive_sum(x);
+    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+    if (i < bins) base[p * kLsdMaxRadix + i] = off + inc - x;
+}
+
+// One stable pass over digit (key >> shift) & (2^nbits - 1), nbits <= RBITS.
+template <class Src, int RBITS, bool PACKED>
+__global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
+                                                   const uint32_t* __restrict__ digit_base,
+                                                   uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
+                                                   uint32_t epoch, uint64_t* __restrict__ out_keys,
+                                                   uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
+    constexpr int BLOCK = kLsdBlock;
+    constexpr int ITEMS = kLsdItems;
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int RADIX = 1 << RBITS;
+    constexpr int RWAVES = RADIX / kWave;
+    constexpr int WTILE = kWave * ITEMS;
+    constexpr int TILE = BLOCK * ITEMS;
+    static_assert(TILE <= 65535 && WTILE <= 65535, "16-bit tile offsets");
+    static_assert(BLOCK >= RADIX, "one thread per digit");
+    __shared__ uint64_t s_keys[TILE];
+    __shared__ uint32_t s_vals[PACKED ? 1 : TILE];
+    __shared__ uint16_t s_wcnt[WAVES][RADIX];   // per-wave digit counts, then wave offsets
+    __shared__ uint16_t s_start[RADIX];
+    __shared__ uint32_t s_gofs[RADIX];
+    __shared__ uint32_t s_tmp[RWAVES];
+    __shared__ uint32_t s_tile[2];
+
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint32_t dg = threadIdx.x;
+    const uint32_t mask = (1u << nbits) - 1u;
+    const uint64_t tiles = (n + TILE - 1) / TILE;
+    const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
+    uint32_t* const wc32 = reinterpret_cast<uint32_t*>(&s_wcnt[0][0]);
+    if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
+    for (int i = dg; i < WAVES * RADIX / 2; i += BLOCK) wc32[i] = 0;
+    __syncthreads();
+    uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint64_t k[ITEMS];
+    uint32_t v[ITEMS];
+    // clamped loads (pairs past the end are never ranked)
+    auto load = [&](uint64_t tt, uint64_t* kk, uint32_t* vv) {
+        const uint64_t tb = tt * TILE;
+        const uint32_t last = (uint32_t)min(n - 1 - tb, (uint64_t)(TILE - 1));
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const uint64_t e = tb + (le < last ? le : last);
+            kk[j] = src.key(e);
+            if constexpr (!PACKED) vv[j] = src.val(e);
+        }
+    };
+    if (t < tiles) load(t, k, v);
+    uint32_t par = 0;
+    while (t < tiles) {
+        const uint64_t tb = t * TILE;
+        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+        // rank in input order: items (j, lane) of wave w are its slice's
+        // positions j * 64 + lane; dr = digit << 16 | rank in the wave's run
+        uint32_t dr[ITEMS];
+        uint16_t* wc = s_wcnt[wave];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t le = wave * WTILE + j * kWave + lane;
+            const bool ok = le < valid;
+            const uint32_t d = ok ? (uint32_t)(k[j] >> shift) & mask : (uint32_t)RADIX;
+            uint64_t peers = __ballot(ok);
+            for (uint32_t b = 0; b < nbits; ++b) {
+                const bool bit = (d >> b) & 1u;
+                const uint64_t bal = __ballot(bit);
+                peers &= bit ? bal : ~bal;
+            }
+            const uint32_t cnt = ok ? (uint32_t)wc[d] : 0u;
+            const uint32_t below = (uint32_t)__popcll(peers & lanemask_lt());
+            if (ok && below == 0) wc[d] = (uint16_t)(cnt + (uint32_t)__popcll(peers));
+            dr[j] = (d << 16) | (cnt + below);
+        }
+        __syncthreads();
+        uint32_t tile_cnt = 0;
+        if (dg < (uint32_t)RADIX) {
+#pragma unroll
+            for (int w = 0; w < WAVES; ++w) {
+                const uint32_t x = s_wcnt[w][dg];
+                s_wcnt[w][dg] = (uint16_t)tile_cnt;
+                tile_cnt += x;
+            }
+            st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+        }
+        {
+            const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
+            const uint32_t inc = wave_inclusive_sum(x);
+            if (lane == kWave - 1 && wave < (uint32_t)RWAVES) s_tmp[wave] = inc;
+            __syncthreads();
+            uint32_t off = 0;
+#pragma unroll
+            for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
+            if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
+        }
+        if (dg < (uint32_t)RADIX) {
+            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
+            s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
+        }
+        // the next tile's ticket only now (see k_split), its loads in flight
+        // during the staging and the writes
+        if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        uint64_t kn[ITEMS];
+        uint32_t vn[ITEMS];
+        load(tn < tiles ? tn : tiles - 1, kn, vn);
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t d = dr[j] >> 16;
+            if (d < (uint32_t)RADIX) {
+                const uint32_t pos = s_start[d] + s_wcnt[wave][d] + (dr[j] & 0xFFFFu);
+                s_keys[pos] = k[j];
+                if constexpr (!PACKED) s_vals[pos] = v[j];
+            }
+        }
+        __syncthreads();
+        for (int i = dg; i < WAVES * RADIX / 2; i += BLOCK) wc32[i] = 0;   // the next tile ranks after a barrier
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t q = j * BLOCK + dg;
+            if (q < valid) {
+                const uint64_t key = s_keys[q];
+                const uint32_t dd = (uint32_t)(key >> shift) & mask;
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < n) {
+                    out_keys[g] = key;
+                    if constexpr (!PACKED) out_vals[g] = s_vals[q];
+                }
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            k[j] = kn[j];
+            if constexpr (!PACKED) v[j] = vn[j];
+        }
+        t = tn;
+        par ^= 1u;
+    }
+}
+
+// SA from the sorted items of a PACKED final round
+__global__ __launch_bounds__(kBlock) void k_items_to_sa(const uint64_t* __restrict__ items, uint64_t n,
+                                                        uint32_t ib, uint32_t* __restrict__ sa) {
+    const uint64_t m = (1ull << ib) - 1ull;
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock)
+        sa[e] = (uint32_t)(items[e] & m);
+}
+
+}  // namespace sa

@@ -1,0 +1,231 @@
+// sa_permute.h -- the re-rank scatter of the reference schedule as a
+// coalesced permutation by suffix index.
+//
+// manber_myers.c:101-110 writes rank_array[suffixes[i].index] = current_rank
+// for every sorted position i: one random 4-byte write per suffix.  As one
+// kernel (k_rerank) that is 39.5 ms per round at n = 2^30 (r02_a: every
+// write its own HBM line).  Here the same values reach rank[] in three
+// coalesced steps, an MSD partition of the (idx, rank) pairs by idx:
+//
+//   k_perm_rank   sorted keys + idx -> dense rank of each sorted position
+//                 (head flags, as k_rerank) -> pair (idx << 32 | rank),
+//                 partitioned by idx >> s1 into <= 256 bins.  idx is a
+//                 permutation of 0..n-1, so bin b holds exactly the idx of
+//                 [b << s1, (b + 1) << s1): its place is known without a
+//                 histogram, and tiles take their slots in it from a
+//                 per-bin atomic cursor (the order inside a bin is free).
+//   k_perm_split  each bin partitioned again by (idx >> s2) & (nsub - 1)
+//                 into 2^s2-entry sub-bins (skipped when s1 == s2).
+//   k_perm_place  one workgroup per sub-bin: the pairs land in an LDS copy
+//                 of rank[sub-bin] by idx, which is then written out whole.
+//
+// Bytes per suffix: 12 read + 8 written, 8 + 8, 8 + 4 (48 B, all streamed
+// or in runs of ~32 pairs) instead of 12 read + one random 4-byte write.
+#pragma once
+#include "sa_kernels.h"
+
+namespace sa {
+
+constexpr uint32_t kPermSub = 14;   // sub-bin = 2^14 ranks = 64 KiB of LDS
+constexpr int kPermBlock = 1024;
+constexpr int kPermItems = 8;       // 8192 pairs per tile (64 KiB staged)
+constexpr uint32_t kPermMaxSub = 1024;
+
+// bin shifts for n suffixes: <= 256 first-level bins, sub-bins of 2^kPermSub
+struct PermPlan {
+    uint32_t s1, s2, nb1, nsub, tpb;   // tpb: k_perm_split tiles per bin
+};
+
+// exclusive scan of x over the first NB threads of a BLOCK-thread workgroup
+// (every thread calls it; s_tmp holds NB / kWave words)
+template <int NB>
+__device__ __forceinline__ uint32_t perm_scan(uint32_t x, uint32_t* s_tmp) {
+    const uint32_t inc = wave_inclusive_sum(x);
+    if (lane_id() == kWave - 1 && wave_id() < (uint32_t)(NB / kWave)) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+#pragma unroll
+    for (int w = 0; w < NB / kWave; ++w) off += (w < (int)wave_id()) ? s_tmp[w] : 0u;
+    return off + inc - x;
+}
+
+// Level 1: one workgroup per chunk of the heads count (k_heads' Chunking, so
+// chunk_off[c] = heads before the chunk), tiles of BLOCK x ITEMS sorted
+// positions in order; wave w owns a contiguous slice of 64 x ITEMS of each.
+// PACKED: keys are (key << kshift | idx) items (sa_onesweep.h k_lsd), idx unused.
+template <int BLOCK, int ITEMS, bool PACKED>
+__global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict__ keys,
+                                                      const uint32_t* __restrict__ idx, Chunking ch,
+                                                      const uint32_t* __restrict__ chunk_off, uint32_t s1,
+                                                      uint32_t kshift, uint32_t* __restrict__ cur,
+                                                      uint64_t* __restrict__ out) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int WT = kWave * ITEMS;
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int NB = 256;
+    static_assert(BLOCK >= NB, "one thread per bin");
+    __shared__ uint64_t s_pair[T];
+    __shared__ uint32_t s_cnt[NB];
+    __shared__ uint32_t s_start[NB];
+    __shared__ uint32_t s_gofs[NB];
+    __shared__ uint32_t s_wtot[WAVES];
+    __shared__ uint32_t s_tmp[NB / kWave];
+    const uint32_t tid = threadIdx.x, wave = wave_id(), lane = lane_id();
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    uint32_t run = chunk_off[c];
+    if (tid < (uint32_t)NB) s_cnt[tid] = 0;
+    const uint64_t le_mask = lanemask_lt() | (1ull << lane);
+    for (uint64_t tb = e0; tb < e1; tb += T) {
+        const uint32_t valid = (uint32_t)((e1 - tb) < (uint64_t)T ? (e1 - tb) : (uint64_t)T);
+        const uint64_t w0 = tb + (uint64_t)wave * WT;
+        uint64_t prev_last = (w0 > 0 && w0 < e1) ? keys[w0 - 1] >> kshift : 0ull;
+        uint64_t m[ITEMS];
+        uint32_t x[ITEMS];
+        uint32_t wsum = 0;
+        const uint64_t imask = PACKED ? (1ull << kshift) - 1ull : 0ull;
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            uint64_t word;
+            bool ok;
+            m[j] = wave_heads(keys, w0 + (uint64_t)j * kWave, e1, prev_last, word, ok, kshift);
+            wsum += (uint32_t)__popcll(m[j]);
+            if constexpr (PACKED)
+                x[j] = ok ? (uint32_t)(word & imask) : ~0u;
+            else
+                x[j] = ok ? idx[w0 + (uint64_t)j * kWave + lane] : ~0u;
+        }
+        if (lane == 0) s_wtot[wave] = wsum;
+        __syncthreads();
+        uint32_t woff = run, ttot = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) {
+            const uint32_t v = s_wtot[w];
+            woff += (w < (int)wave) ? v : 0u;
+            ttot += v;
+        }
+        uint32_t slot[ITEMS];
+        uint64_t pr[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t r = woff + (uint32_t)__popcll(m[j] & le_mask);
+            woff += (uint32_t)__popcll(m[j]);
+            pr[j] = ((uint64_t)x[j] << 32) | r;
+            slot[j] = x[j] != ~0u ? atomicAdd(&s_cnt[x[j] >> s1], 1u) : 0u;
+        }
+        __syncthreads();
+        const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
+        const uint32_t st = perm_scan<NB>(cnt, s_tmp);
+        if (tid < (uint32_t)NB) {
+            s_start[tid] = st;
+            s_gofs[tid] = cnt ? (tid << s1) + atomicAdd(&cur[tid], cnt) : 0u;
+            s_cnt[tid] = 0;   // the next tile's atomics follow two barriers
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            if (x[j] != ~0u) s_pair[s_start[x[j] >> s1] + slot[j]] = pr[j];
+        __syncthreads();
+        for (uint32_t q = tid; q < valid; q += BLOCK) {
+            const uint64_t p = s_pair[q];
+            const uint32_t b = (uint32_t)(p >> 32) >> s1;
+            const uint64_t g = (uint64_t)s_gofs[b] + (q - s_start[b]);
+            if (g < ch.n) out[g] = p;
+        }
+        run += ttot;
+        __syncthreads();
+    }
+}
+
+// Level 2: tile t of bin b = workgroup b * tpb + t.
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
+                                                       uint32_t s2, uint32_t tpb, uint32_t* __restrict__ cur,
+                                                       uint64_t* __restrict__ out) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int NB = kPermMaxSub;
+    static_assert(BLOCK >= NB, "one thread per sub-bin");
+    __shared__ uint64_t s_pair[T];
+    __shared__ uint32_t s_cnt[NB];
+    __shared__ uint32_t s_start[NB];
+    __shared__ uint32_t s_gofs[NB];
+    __shared__ uint32_t s_tmp[NB / kWave];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t b = blockIdx.x / tpb, t = blockIdx.x % tpb;
+    const uint32_t nsub = 1u << (s1 - s2);
+    const uint64_t bin0 = (uint64_t)b << s1;
+    const uint64_t bin1 = (bin0 + (1ull << s1)) < n ? bin0 + (1ull << s1) : n;
+    const uint64_t tb = bin0 + (uint64_t)t * T;
+    if (tb >= bin1) return;   // uniform over the workgroup
+    const uint32_t valid = (uint32_t)((bin1 - tb) < (uint64_t)T ? (bin1 - tb) : (uint64_t)T);
+    if (tid < (uint32_t)NB) s_cnt[tid] = 0;
+    __syncthreads();
+    uint64_t p[ITEMS];
+    uint32_t sub[ITEMS], slot[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + tid;
+        p[j] = q < valid ? in[tb + q] : 0ull;
+        sub[j] = q < valid ? ((uint32_t)(p[j] >> 32) >> s2) & (nsub - 1u) : NB;
+        slot[j] = sub[j] < (uint32_t)NB ? atomicAdd(&s_cnt[sub[j]], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
+    const uint32_t st = perm_scan<NB>(cnt, s_tmp);
+    if (tid < (uint32_t)NB) {
+        s_start[tid] = st;
+        s_gofs[tid] = cnt ? (uint32_t)bin0 + (tid << s2) + atomicAdd(&cur[(uint64_t)b * nsub + tid], cnt) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (sub[j] < (uint32_t)NB) s_pair[s_start[sub[j]] + slot[j]] = p[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + tid;
+        if (q < valid) {
+            const uint64_t v = s_pair[q];
+            const uint32_t sb = ((uint32_t)(v >> 32) >> s2) & (nsub - 1u);
+            const uint64_t g = (uint64_t)s_gofs[sb] + (q - s_start[sb]);
+            if (g < n) out[g] = v;
+        }
+    }
+}
+
+// Level 3: one workgroup per 2^kPermSub sub-bin; a pair whose idx lies
+// outside the sub-bin (a broken partition) raises err[0] and is dropped.
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict__ in, uint64_t n,
+                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ err) {
+    constexpr uint32_t S = 1u << kPermSub;
+    __shared__ uint32_t s_r[S];
+    const uint64_t base = (uint64_t)blockIdx.x << kPermSub;
+    const uint32_t valid = (uint32_t)((n - base) < (uint64_t)S ? (n - base) : (uint64_t)S);
+    bool bad = false;
+    for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) {
+        const uint64_t p = in[base + q];
+        const uint32_t x = (uint32_t)(p >> 32);
+        if ((x >> kPermSub) != blockIdx.x || (x & (S - 1u)) >= valid) {
+            bad = true;
+            continue;
+        }
+        s_r[x & (S - 1u)] = (uint32_t)p;
+    }
+    if (bad) atomicOr(err, 2u);
+    __syncthreads();
+    for (uint32_t q = threadIdx.x * 4; q < valid; q += BLOCK * 4) {
+        if (q + 4 <= valid) {
+            uint4 v;
+            v.x = s_r[q];
+            v.y = s_r[q + 1];
+            v.z = s_r[q + 2];
+            v.w = s_r[q + 3];
+            *reinterpret_cast<uint4*>(rank + base + q) = v;
+        } else {
+            for (uint32_t i = q; i < valid; ++i) rank[base + i] = s_r[i];
+        }
+    }
+}
+
+}  // namespace sa

@@ -71,6 +71,25 @@ def test_random_vs_oracle(gpu, oracle, kind, n, schedule):
         assert st["distinct"][-1] == n
 
 
+@pytest.mark.parametrize("kind", ["dna", "alnum", "byte256", "binary"])
+def test_reference_rerank_permutation(gpu, oracle, kind, monkeypatch):
+    """The reference schedule's re-rank as a partition by index
+    (sa_permute.h) forced at every size: one level (n <= 2^22), two levels
+    with 2 / 4 sub-bins, ragged last bins and sub-bins; D_j stay the
+    reference's round for round."""
+    from hpc_suffix_array_amd import build_suffix_array
+    monkeypatch.setenv("SA_PERM_MIN", "1")
+    for n in (2, 3, 4095, 16385, 100_003, (1 << 22) + 1, 3 * (1 << 21) + 7):
+        t = oracle.gen_text(kind, n, seed=n + 3)
+        got, st = build_suffix_array(t, return_stats=True, schedule="reference")
+        ref, rounds, _, dj = oracle.sa_c(t, stats=True)
+        assert (got == ref).all(), (kind, n)
+        assert st["rounds"] == rounds and st["distinct"] == dj, (kind, n)
+    t = np.full(70_001, ord("a"), np.uint8)
+    got = build_suffix_array(t, schedule="reference")
+    assert (got == np.arange(70_000, -1, -1, dtype=np.uint32)).all()
+
+
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("radix", ["onesweep", "reduce_scan"])
 def test_radix_algorithms(gpu, oracle, schedule, radix):
