@@ -481,23 +481,31 @@ static PermPlan plan_perm(uint64_t n) {
 
 // rank[idx[p]] = dense rank of sorted position p, through the two key
 // buffers (the sorted keys are read by the first step and then free)
+// first-level tiles of the permutation and their head offsets (k_tile_heads)
+constexpr uint64_t kPermTile = (uint64_t)kPermBlock * kPermItems;
+static uint32_t* perm_tile_off(sa_context* c) { return c->hist + ((uint64_t)kRadix * kMaxChunks) / 2; }
+
 static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa, const Chunking& ch,
                           hipStream_t s, Timer& tm, sa_stats* st, uint32_t kshift = 0) {
     const uint64_t n = ch.n;
     const PermPlan p = plan_perm(n);
-    if (p.nb1 > 256 || p.nsub > kPermMaxSub || 256ull + (uint64_t)p.nb1 * p.nsub > (uint64_t)kRadix * kMaxChunks)
+    const uint64_t half = (uint64_t)kRadix * kMaxChunks / 2;   // cursors below, tile offsets above
+    if (p.nb1 > 256 || p.nsub > kPermMaxSub || 256ull + (uint64_t)p.nb1 * p.nsub > half ||
+        (n + kPermTile - 1) / kPermTile > half)
         return set_err(SA_E_INTERNAL, "permutation plan out of range (n=%llu)", (unsigned long long)n);
     uint64_t* other = sorted == c->keys[0] ? c->keys[1] : c->keys[0];
     uint32_t* cur1 = c->hist;          // the chunk histograms are free after the sort
     uint32_t* cur2 = c->hist + 256;
     SA_HIP(hipMemsetAsync(c->hist, 0, (256ull + (uint64_t)p.nb1 * p.nsub) * 4, s));
     tm.begin(SA_K_RERANK);
+    const uint32_t tiles = (uint32_t)((n + kPermTile - 1) / kPermTile);
+    const uint32_t* toff = perm_tile_off(c);
     if (kshift)   // packed (key << kshift | idx) items
-        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, true>), dim3(ch.chunks), dim3(kPermBlock), 0, s,
-                           (const uint64_t*)sorted, d_sa, ch, (const uint32_t*)c->counts, p.s1, kshift, cur1, other);
+        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, true>), dim3(tiles), dim3(kPermBlock), 0, s,
+                           (const uint64_t*)sorted, d_sa, n, toff, p.s1, kshift, cur1, other);
     else
-        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, false>), dim3(ch.chunks), dim3(kPermBlock), 0, s,
-                           (const uint64_t*)sorted, d_sa, ch, (const uint32_t*)c->counts, p.s1, 0u, cur1, other);
+        hipLaunchKernelGGL((k_perm_rank<kPermBlock, kPermItems, false>), dim3(tiles), dim3(kPermBlock), 0, s,
+                           (const uint64_t*)sorted, d_sa, n, toff, p.s1, 0u, cur1, other);
     const uint64_t* placed = other;
     if (p.s1 > p.s2) {
         hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3(p.nb1 * p.tpb), dim3(kPermBlock), 0, s,
@@ -552,29 +560,46 @@ static LsdPlan lsd_plan(uint32_t B, uint32_t base) {
 }
 
 template <class K>
-static int persist_grid(sa_context* c, K kernel) {
+static int persist_grid(sa_context* c, K kernel, int block) {
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kLsdBlock, 0) != hipSuccess || nb < 1) nb = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb < 1) nb = 1;
     return c->cus * nb;
 }
 
 template <class Src, bool PACKED>
 static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits, const uint32_t* base,
-                     uint32_t* ticket, uint64_t* ok, uint32_t* ov, hipStream_t s) {
+                     uint32_t* ticket, uint64_t* ok, uint32_t* ov, hipStream_t s, uint32_t nshift, uint32_t nnbits,
+                     uint32_t* next_hist) {
     const uint32_t epoch = next_epoch(c, s);
-    const uint64_t tiles = (n + kLsdTile - 1) / kLsdTile;
+    uint64_t tiles = 0;
+    unsigned long long* prof = reinterpret_cast<unsigned long long*>(lsd_tickets(c) + kMaxPasses);
+    if (SA_LSD_PROF) hipMemsetAsync(prof, 0, 5 * 8, s);
 #define SA_LSD_LAUNCH(RB)                                                                                   \
     do {                                                                                                    \
         auto kern = k_lsd<Src, RB, PACKED>;                                                                 \
+        constexpr int B = lsd_block<PACKED, RB>();                                                          \
+        constexpr uint64_t T = (uint64_t)B * lsd_items<PACKED, RB>();                                       \
+        tiles = (n + T - 1) / T;                                                                            \
         static int grid = 0;                                                                                \
-        if (!grid) grid = persist_grid(c, kern);                                                            \
-        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, (uint64_t)grid)), dim3(kLsdBlock), 0, s, \
-                           src, n, shift, nbits, base, c->states, ticket, epoch, ok, ov, c->words + 4);      \
+        if (!grid) grid = persist_grid(c, kern, B);                                                         \
+        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, (uint64_t)grid)), dim3(B), 0, s,  \
+                           src, n, shift, nbits, base, c->states, ticket, epoch, ok, ov, c->words + 4, prof,   \
+                           nshift, nnbits, next_hist);                                                     \
     } while (0)
     if (nbits <= 8) SA_LSD_LAUNCH(8);
     else if (nbits == 9) SA_LSD_LAUNCH(9);
     else SA_LSD_LAUNCH(10);
 #undef SA_LSD_LAUNCH
+    if (SA_LSD_PROF) {
+        unsigned long long h[5];
+        hipMemcpyAsync(h, prof, sizeof h, hipMemcpyDeviceToHost, s);
+        hipStreamSynchronize(s);
+        double tot = 0;
+        for (double x : h) tot += x;
+        std::fprintf(stderr, "[lsd-prof] n=%llu bits=%u packed=%d clk/tile %.0f: rank %.1f%% scan %.1f%% lookback %.1f%% stage %.1f%% write %.1f%%\n",
+                     (unsigned long long)n, nbits, (int)PACKED, tot / (double)tiles,
+                     100 * h[0] / tot, 100 * h[1] / tot, 100 * h[2] / tot, 100 * h[3] / tot, 100 * h[4] / tot);
+    }
 }
 
 // Stable LSD sort of n pairs by the plan's digits, pass 0 reading `first`.
@@ -589,30 +614,39 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
     vb[(pl.P - 1) & 1] = vals_final;
     vb[pl.P & 1] = vals_other;
     SA_HIP(hipMemsetAsync(c->lsd, 0, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4, s));
+    // the first digit's totals here; every pass counts the next one's
+    LsdPlan first_only = pl;
+    first_only.P = 1;
     tm.begin(SA_K_HIST_FIRST);
-    hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 1024)),
-                       dim3(kBlock), 0, s, first, n, pl, lsd_ghist(c));
+    hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + 8 * kBlock - 1) / (8 * kBlock),
+                                                                           (uint64_t)c->cus * 4)),
+                       dim3(kBlock), 0, s, first, n, first_only, lsd_ghist(c));
     tm.end();
     add_bytes(st, SA_K_HIST_FIRST, 8 * n);
-    tm.begin(SA_K_SCAN);
-    hipLaunchKernelGGL(k_lsd_base, dim3(pl.P), dim3(1024), 0, s, (const uint32_t*)lsd_ghist(c), pl, lsd_base(c));
-    tm.end();
     const uint64_t pair = PACKED ? 8 : 12;
     for (uint32_t p = 0; p < pl.P; ++p) {
-        const uint32_t* base = lsd_base(c) + p * kLsdMaxRadix;
+        uint32_t* base = lsd_base(c) + p * kLsdMaxRadix;
+        tm.begin(SA_K_SCAN);
+        hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s,
+                           (const uint32_t*)lsd_ghist(c) + p * kLsdMaxRadix, 1u << pl.bits[p], base);
+        tm.end();
+        const bool more = p + 1 < pl.P;
+        const uint32_t nsh = more ? pl.shift[p + 1] : 0u, nnb = more ? pl.bits[p + 1] : 1u;
+        uint32_t* nh = more ? lsd_ghist(c) + (p + 1) * kLsdMaxRadix : nullptr;
         if (p == 0) {
             tm.begin(SA_K_SCATTER_FIRST);
-            lsd_pass<Src0, PACKED>(c, first, n, pl.shift[0], pl.bits[0], base, lsd_tickets(c), kb[0], vb[0], s);
+            lsd_pass<Src0, PACKED>(c, first, n, pl.shift[0], pl.bits[0], base, lsd_tickets(c), kb[0], vb[0], s, nsh,
+                                   nnb, nh);
             tm.end();
             add_bytes(st, SA_K_SCATTER_FIRST, (8 + pair) * n);
         } else {
             tm.begin(SA_K_SCATTER_KEYS);
             if constexpr (PACKED)
                 lsd_pass<SrcItems, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], base,
-                                         lsd_tickets(c) + p, kb[p & 1], nullptr, s);
+                                         lsd_tickets(c) + p, kb[p & 1], nullptr, s, nsh, nnb, nh);
             else
                 lsd_pass<SrcKeys, false>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p],
-                                         base, lsd_tickets(c) + p, kb[p & 1], vb[p & 1], s);
+                                         base, lsd_tickets(c) + p, kb[p & 1], vb[p & 1], s, nsh, nnb, nh);
             tm.end();
             add_bytes(st, SA_K_SCATTER_KEYS, 2 * pair * n);
         }
@@ -682,11 +716,21 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                             &P);
         }
         if (rc) return rc;
+        // the permutation's first level counts heads per tile of its own
+        const bool use_perm = packed || n >= perm_min;
+        const uint32_t ptiles = (uint32_t)((n + kPermTile - 1) / kPermTile);
         tm.begin(SA_K_HEADS);
-        hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts, packed ? ib : 0u);
+        if (use_perm)
+            hipLaunchKernelGGL((k_tile_heads<kPermBlock, kPermItems>), dim3(ptiles), dim3(kPermBlock), 0, s,
+                               (const uint64_t*)sorted, n, packed ? ib : 0u, perm_tile_off(c));
+        else
+            hipLaunchKernelGGL(k_heads, dim3(ch.chunks), dim3(kBlock), 0, s, sorted, ch, c->counts, 0u);
         tm.end();
         tm.begin(SA_K_HEADS_SCAN);
-        hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, c->counts, ch.chunks, c->words);
+        if (use_perm)
+            hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, perm_tile_off(c), ptiles, c->words);
+        else
+            hipLaunchKernelGGL(k_scan_heads, dim3(1), dim3(kBlock), 0, s, c->counts, ch.chunks, c->words);
         tm.end();
         SA_HIP(hipGetLastError());
         add_bytes(st, SA_K_HEADS, 8 * n);
@@ -705,7 +749,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             add_bytes(st, SA_K_RERANK, 12 * n);
         }
         if (!done) {
-            if (packed || n >= perm_min) {
+            if (use_perm) {
                 used_perm = true;
                 rc = rerank_permute(c, sorted, d_sa, ch, s, tm, st, packed ? ib : 0u);
                 if (rc) return rc;
@@ -1400,7 +1444,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->words, 64) != hipSuccess || hipMalloc(&c->alpha, 256 * 4) != hipSuccess ||
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
-        hipMalloc(&c->lsd, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4) != hipSuccess ||
+        hipMalloc(&c->lsd, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4 + 64) != hipSuccess ||
         hipMalloc(&c->segw, (kBstartOff + 2 * kBstartWords) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 16384, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();

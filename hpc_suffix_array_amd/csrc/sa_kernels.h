@@ -57,6 +57,14 @@ struct SrcRank {
         return (r0 << w) | r1;
     }
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return (uint32_t)e; }
+    // two-step form (loads, then the key) for the prefetch of sa_lsd.h k_lsd
+    static constexpr bool kRaw = true;
+    __device__ __forceinline__ uint64_t raw(uint64_t e) const {
+        return (uint64_t)rank[e] | ((uint64_t)((e + h < n) ? rank[e + h] : 0u) << 32);
+    }
+    __device__ __forceinline__ uint64_t finish(uint64_t r, uint64_t) const {
+        return ((r & 0xFFFFFFFFull) << w) | (r >> 32);
+    }
 };
 
 // Packed schedule, first round: key = the first K symbols of suffix i packed

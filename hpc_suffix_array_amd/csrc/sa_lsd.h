@@ -13,15 +13,42 @@
 //   * digits of 8 to 10 bits, the widths chosen per round by lsd_plan
 //     (sa_build.hip), so an 18-bit key takes two passes instead of three;
 //   * PACKED: while key bits + index bits <= 64 the pass moves one 64-bit
-//     item (key << ib | index) -- 16 bytes per pair and pass instead of 24.
+//     item (key << ib | index) -- 16 bytes per pair and pass instead of 24;
+//   * each pass counts the next pass's digits of the keys it ranks (one LDS
+//     atomic per key, flushed per workgroup), so the histogram kernel reads
+//     the ranks for the first digit only (k_lsd_hist over every digit of a
+//     60-bit key: 6.6 ms at 2^30);
+//   * the first pass prefetches the raw rank words and builds the keys when
+//     its tile is ranked (building them at the load made the staging wait).
 #pragma once
 #include "sa_split.h"
 
 namespace sa {
 
-constexpr int kLsdBlock = 1024;
-constexpr int kLsdItems = 8;                        // 8192 pairs per tile
-constexpr int kLsdTile = kLsdBlock * kLsdItems;
+#ifndef SA_LSD_LOOK
+#define SA_LSD_LOOK 4   // predecessor states read per look-back step (8: 1.02x, 16: 1.3x the pass time)
+#endif
+#ifndef SA_LSD_PROF
+#define SA_LSD_PROF 0       // per-phase clock64 spans of k_lsd printed per pass (diagnostic builds)
+#endif
+// workgroup shapes (A/B overridable): PACKED passes of <= 9-bit digits and
+// unpacked ones; 10-bit digits always take 1024 x 8 (one thread per digit)
+#ifndef SA_LSD_PK_BLOCK
+#define SA_LSD_PK_BLOCK 1024
+#endif
+#ifndef SA_LSD_PK_ITEMS
+#define SA_LSD_PK_ITEMS 8
+#endif
+#ifndef SA_LSD_UP_BLOCK
+#define SA_LSD_UP_BLOCK 1024
+#endif
+#ifndef SA_LSD_UP_ITEMS
+#define SA_LSD_UP_ITEMS 8
+#endif
+template <bool PACKED, int RBITS>
+constexpr int lsd_block() { return RBITS > 9 ? 1024 : PACKED ? SA_LSD_PK_BLOCK : SA_LSD_UP_BLOCK; }
+template <bool PACKED, int RBITS>
+constexpr int lsd_items() { return RBITS > 9 ? 8 : PACKED ? SA_LSD_PK_ITEMS : SA_LSD_UP_ITEMS; }
 constexpr int kLsdMaxRadix = 1024;
 
 // the passes of one sort: digit p is bits [shift[p], shift[p] + bits[p])
@@ -43,7 +70,23 @@ struct SrcRankPk {
         return (((r0 << w) | r1) << ib) | e;
     }
     __device__ __forceinline__ uint32_t val(uint64_t) const { return 0u; }
+    // two-step form for a prefetch: the loads, then the key (k_lsd issues
+    // the next tile's loads before the staging and builds keys only when the
+    // tile is ranked, so nothing waits for them in between)
+    static constexpr bool kRaw = true;
+    __device__ __forceinline__ uint64_t raw(uint64_t e) const {
+        return (uint64_t)rank[e] | ((uint64_t)((e + h < n) ? rank[e + h] : 0u) << 32);
+    }
+    __device__ __forceinline__ uint64_t finish(uint64_t r, uint64_t e) const {
+        return ((((r & 0xFFFFFFFFull) << w) | (r >> 32)) << ib) | e;
+    }
 };
+
+// the two-step (raw, finish) form of a source, when it has one
+template <class S, class = void>
+struct has_raw { static constexpr bool value = false; };
+template <class S>
+struct has_raw<S, decltype((void)S::kRaw)> { static constexpr bool value = S::kRaw; };
 
 // Later passes of a PACKED round: the items themselves.
 struct SrcItems {
@@ -64,16 +107,29 @@ __global__ __launch_bounds__(kBlock) void k_lsd_hist(Src src, uint64_t n, LsdPla
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < n; e += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t k = src.key(e);
-        const uint32_t nact = (uint32_t)__popcll(__ballot(1));
-        for (uint32_t p = 0; p < plan.P; ++p) {
-            const uint32_t d = (uint32_t)(k >> plan.shift[p]) & ((1u << plan.bits[p]) - 1u);
-            const uint32_t dl = __shfl_up(d, 1, 64);
-            const bool head = lane == 0 || dl != d;
-            const uint64_t hm = __ballot(head) & above;
-            const uint32_t next = hm ? (uint32_t)__ffsll((long long)hm) - 1u : nact;
-            if (head) atomicAdd(&s_h[p * kLsdMaxRadix + d], next - lane);
+    // 8 keys per lane per step, all loads issued before the counting
+    constexpr int U = 8;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * U;
+    for (uint64_t b = (uint64_t)blockIdx.x * kBlock * U; b < n; b += step) {
+        uint64_t k[U];
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t e = b + (uint64_t)j * kBlock + threadIdx.x;
+            k[j] = src.key(e < n ? e : n - 1);
+        }
+#pragma unroll
+        for (int j = 0; j < U; ++j) {
+            const uint64_t e = b + (uint64_t)j * kBlock + threadIdx.x;
+            if (e >= n) break;   // the active lanes stay a prefix of the wave
+            const uint32_t nact = (uint32_t)__popcll(__ballot(1));
+            for (uint32_t p = 0; p < plan.P; ++p) {
+                const uint32_t d = (uint32_t)(k[j] >> plan.shift[p]) & ((1u << plan.bits[p]) - 1u);
+                const uint32_t dl = __shfl_up(d, 1, 64);
+                const bool head = lane == 0 || dl != d;
+                const uint64_t hm = __ballot(head) & above;
+                const uint32_t next = hm ? (uint32_t)__ffsll((long long)hm) - 1u : nact;
+                if (head) atomicAdd(&s_h[p * kLsdMaxRadix + d], next - lane);
+            }
         }
     }
     __syncthreads();
@@ -98,13 +154,15 @@ __global__ __launch_bounds__(1024) void k_lsd_base(const uint32_t* __restrict__ 
 
 // One stable pass over digit (key >> shift) & (2^nbits - 1), nbits <= RBITS.
 template <class Src, int RBITS, bool PACKED>
-__global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
+__global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
                                                    const uint32_t* __restrict__ digit_base,
                                                    uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
                                                    uint32_t epoch, uint64_t* __restrict__ out_keys,
-                                                   uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err) {
-    constexpr int BLOCK = kLsdBlock;
-    constexpr int ITEMS = kLsdItems;
+                                                   uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err,
+                                                   unsigned long long* __restrict__ prof, uint32_t nshift,
+                                                   uint32_t nnbits, uint32_t* __restrict__ next_hist) {
+    constexpr int BLOCK = lsd_block<PACKED, RBITS>();
+    constexpr int ITEMS = lsd_items<PACKED, RBITS>();
     constexpr int WAVES = BLOCK / kWave;
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
@@ -119,10 +177,13 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
+    __shared__ uint32_t s_nh[kLsdMaxRadix];     // the next pass's digit totals of this workgroup's tiles
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint32_t mask = (1u << nbits) - 1u;
+    const uint32_t nmask = (1u << nnbits) - 1u;
+    for (int i = dg; i < kLsdMaxRadix; i += BLOCK) s_nh[i] = 0;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
     uint32_t* const wc32 = reinterpret_cast<uint32_t*>(&s_wcnt[0][0]);
@@ -140,12 +201,24 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t le = wave * WTILE + j * kWave + lane;
             const uint64_t e = tb + (le < last ? le : last);
-            kk[j] = src.key(e);
+            if constexpr (has_raw<Src>::value)
+                kk[j] = src.raw(e);
+            else
+                kk[j] = src.key(e);
             if constexpr (!PACKED) vv[j] = src.val(e);
         }
     };
     if (t < tiles) load(t, k, v);
     uint32_t par = 0;
+    // SA_LSD_PROF (diagnostic builds): thread 0's clock64 spans per phase
+    uint64_t tacc[5] = {0, 0, 0, 0, 0}, tlast = SA_LSD_PROF ? clock64() : 0;
+    auto stamp = [&](int q) {
+        if constexpr (SA_LSD_PROF != 0) {
+            const uint64_t now = clock64();
+            tacc[q] += now - tlast;
+            tlast = now;
+        }
+    };
     while (t < tiles) {
         const uint64_t tb = t * TILE;
         const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
@@ -153,10 +226,19 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
         // positions j * 64 + lane; dr = digit << 16 | rank in the wave's run
         uint32_t dr[ITEMS];
         uint16_t* wc = s_wcnt[wave];
+        if constexpr (has_raw<Src>::value) {
+            const uint32_t last = valid - 1;
+#pragma unroll
+            for (int j = 0; j < ITEMS; ++j) {
+                const uint32_t le = wave * WTILE + j * kWave + lane;
+                k[j] = src.finish(k[j], tb + (le < last ? le : last));
+            }
+        }
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t le = wave * WTILE + j * kWave + lane;
             const bool ok = le < valid;
+            if (next_hist && ok) atomicAdd(&s_nh[(uint32_t)(k[j] >> nshift) & nmask], 1u);
             const uint32_t d = ok ? (uint32_t)(k[j] >> shift) & mask : (uint32_t)RADIX;
             uint64_t peers = __ballot(ok);
             for (uint32_t b = 0; b < nbits; ++b) {
@@ -170,6 +252,7 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
             dr[j] = (d << 16) | (cnt + below);
         }
         __syncthreads();
+        stamp(0);
         uint32_t tile_cnt = 0;
         if (dg < (uint32_t)RADIX) {
 #pragma unroll
@@ -190,14 +273,16 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
             for (int w = 0; w < RWAVES; ++w) off += (w < (int)wave) ? s_tmp[w] : 0u;
             if (dg < (uint32_t)RADIX) s_start[dg] = (uint16_t)(off + inc - x);
         }
+        stamp(1);
         if (dg < (uint32_t)RADIX) {
-            const uint64_t excl = tile_lookback<RADIX>(states, t, dg, tile_cnt, tag, err);
+            const uint64_t excl = tile_lookback<RADIX, false, SA_LSD_LOOK>(states, t, dg, tile_cnt, tag, err);
             s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
         }
         // the next tile's ticket only now (see k_split), its loads in flight
         // during the staging and the writes
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         __syncthreads();
+        stamp(2);
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
@@ -212,6 +297,7 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
             }
         }
         __syncthreads();
+        stamp(3);
         for (int i = dg; i < WAVES * RADIX / 2; i += BLOCK) wc32[i] = 0;   // the next tile ranks after a barrier
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
@@ -227,6 +313,7 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
             }
         }
         __syncthreads();
+        stamp(4);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             k[j] = kn[j];
@@ -234,6 +321,14 @@ __global__ __launch_bounds__(kLsdBlock) void k_lsd(Src src, uint64_t n, uint32_t
         }
         t = tn;
         par ^= 1u;
+    }
+    if constexpr (SA_LSD_PROF != 0)
+        if (dg == 0)
+            for (int q = 0; q < 5; ++q) atomicAdd(prof + q, (unsigned long long)tacc[q]);
+    if (next_hist) {
+        __syncthreads();
+        for (uint32_t i = dg; i <= nmask; i += BLOCK)
+            if (s_nh[i]) atomicAdd(&next_hist[i], s_nh[i]);
     }
 }
 

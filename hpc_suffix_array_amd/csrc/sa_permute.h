@@ -49,14 +49,68 @@ __device__ __forceinline__ uint32_t perm_scan(uint32_t x, uint32_t* s_tmp) {
     return off + inc - x;
 }
 
-// Level 1: one workgroup per chunk of the heads count (k_heads' Chunking, so
-// chunk_off[c] = heads before the chunk), tiles of BLOCK x ITEMS sorted
-// positions in order; wave w owns a contiguous slice of 64 x ITEMS of each.
-// PACKED: keys are (key << kshift | idx) items (sa_onesweep.h k_lsd), idx unused.
+// Loads the words of wave slice [w0, w0 + 64 ITEMS) (rows of 64) and the
+// key before it, all issued before any use (wave_heads row by row waited
+// for each row's load in turn), and returns the rows' head masks: key =
+// word >> kshift, head = first position or key != its predecessor's.
+template <int ITEMS>
+__device__ __forceinline__ void slice_heads(const uint64_t* __restrict__ keys, uint64_t w0, uint64_t e1,
+                                            uint32_t kshift, uint64_t* wd, uint64_t* m) {
+    const uint32_t lane = lane_id();
+    uint64_t prev_last = (w0 > 0 && w0 < e1) ? keys[w0 - 1] : 0ull;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+        wd[j] = e < e1 ? keys[e] : 0ull;
+    }
+    prev_last >>= kshift;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+        const uint64_t key = wd[j] >> kshift;
+        uint64_t prev = __shfl_up(key, 1, kWave);
+        if (lane == 0) prev = prev_last;
+        prev_last = __shfl(key, kWave - 1, kWave);
+        m[j] = __ballot(e < e1 && (e == 0 || key != prev));
+    }
+}
+
+// Head counts per first-level tile (sorted positions [t T, (t + 1) T));
+// k_scan_heads turns them into offsets and D.
+template <int BLOCK, int ITEMS>
+__global__ __launch_bounds__(BLOCK) void k_tile_heads(const uint64_t* __restrict__ keys, uint64_t n,
+                                                       uint32_t kshift, uint32_t* __restrict__ counts) {
+    constexpr int WAVES = BLOCK / kWave;
+    constexpr int WT = kWave * ITEMS;
+    __shared__ uint32_t s_w[WAVES];
+    const uint64_t tb = (uint64_t)blockIdx.x * BLOCK * ITEMS;
+    const uint64_t e1 = (tb + BLOCK * ITEMS) < n ? tb + BLOCK * ITEMS : n;
+    uint64_t wd[ITEMS], m[ITEMS];
+    slice_heads<ITEMS>(keys, tb + (uint64_t)wave_id() * WT, e1, kshift, wd, m);
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) cnt += (uint32_t)__popcll(m[j]);
+    if (lane_id() == 0) s_w[wave_id()] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) t += s_w[w];
+        counts[blockIdx.x] = t;
+    }
+}
+
+// Level 1: one workgroup per tile of BLOCK x ITEMS sorted positions (tile_off
+// = heads before the tile, k_tile_heads + k_scan_heads); wave w owns a
+// contiguous slice of 64 x ITEMS of it.  Slots in a bin come from the bin's
+// cursor, one device-scope atomic per tile and bin (exact per-tile offsets
+// from a counting pass measured slower: 223.5 vs 216 ms for the 1 GiB DNA
+// reference schedule, the counts' scattered writes and scan cost more).
+// PACKED: keys are (key << kshift | idx) items (sa_lsd.h k_lsd), idx unused.
 template <int BLOCK, int ITEMS, bool PACKED>
 __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict__ keys,
-                                                      const uint32_t* __restrict__ idx, Chunking ch,
-                                                      const uint32_t* __restrict__ chunk_off, uint32_t s1,
+                                                      const uint32_t* __restrict__ idx, uint64_t n,
+                                                      const uint32_t* __restrict__ tile_off, uint32_t s1,
                                                       uint32_t kshift, uint32_t* __restrict__ cur,
                                                       uint64_t* __restrict__ out) {
     constexpr int WAVES = BLOCK / kWave;
@@ -71,69 +125,64 @@ __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict_
     __shared__ uint32_t s_wtot[WAVES];
     __shared__ uint32_t s_tmp[NB / kWave];
     const uint32_t tid = threadIdx.x, wave = wave_id(), lane = lane_id();
-    const uint32_t c = blockIdx.x;
-    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
-    uint32_t run = chunk_off[c];
+    const uint64_t tb = (uint64_t)blockIdx.x * T;
+    const uint64_t e1 = (tb + T) < n ? tb + T : n;
+    const uint32_t valid = (uint32_t)(e1 - tb);
     if (tid < (uint32_t)NB) s_cnt[tid] = 0;
     const uint64_t le_mask = lanemask_lt() | (1ull << lane);
-    for (uint64_t tb = e0; tb < e1; tb += T) {
-        const uint32_t valid = (uint32_t)((e1 - tb) < (uint64_t)T ? (e1 - tb) : (uint64_t)T);
-        const uint64_t w0 = tb + (uint64_t)wave * WT;
-        uint64_t prev_last = (w0 > 0 && w0 < e1) ? keys[w0 - 1] >> kshift : 0ull;
-        uint64_t m[ITEMS];
-        uint32_t x[ITEMS];
-        uint32_t wsum = 0;
-        const uint64_t imask = PACKED ? (1ull << kshift) - 1ull : 0ull;
+    const uint64_t w0 = tb + (uint64_t)wave * WT;
+    uint32_t x[ITEMS];
+    if constexpr (!PACKED) {
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            uint64_t word;
-            bool ok;
-            m[j] = wave_heads(keys, w0 + (uint64_t)j * kWave, e1, prev_last, word, ok, kshift);
-            wsum += (uint32_t)__popcll(m[j]);
-            if constexpr (PACKED)
-                x[j] = ok ? (uint32_t)(word & imask) : ~0u;
-            else
-                x[j] = ok ? idx[w0 + (uint64_t)j * kWave + lane] : ~0u;
+            const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+            x[j] = e < e1 ? idx[e] : ~0u;
         }
-        if (lane == 0) s_wtot[wave] = wsum;
-        __syncthreads();
-        uint32_t woff = run, ttot = 0;
+    }
+    uint64_t wd[ITEMS], m[ITEMS];
+    slice_heads<ITEMS>(keys, w0, e1, kshift, wd, m);
+    uint32_t wsum = 0;
+    const uint64_t imask = (1ull << kshift) - 1ull;
 #pragma unroll
-        for (int w = 0; w < WAVES; ++w) {
-            const uint32_t v = s_wtot[w];
-            woff += (w < (int)wave) ? v : 0u;
-            ttot += v;
-        }
-        uint32_t slot[ITEMS];
-        uint64_t pr[ITEMS];
+    for (int j = 0; j < ITEMS; ++j) {
+        wsum += (uint32_t)__popcll(m[j]);
+        if constexpr (PACKED) x[j] = (w0 + (uint64_t)j * kWave + lane) < e1 ? (uint32_t)(wd[j] & imask) : ~0u;
+    }
+    if (lane == 0) s_wtot[wave] = wsum;
+    __syncthreads();
+    uint32_t woff = tile_off[blockIdx.x];
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const uint32_t r = woff + (uint32_t)__popcll(m[j] & le_mask);
-            woff += (uint32_t)__popcll(m[j]);
-            pr[j] = ((uint64_t)x[j] << 32) | r;
-            slot[j] = x[j] != ~0u ? atomicAdd(&s_cnt[x[j] >> s1], 1u) : 0u;
-        }
-        __syncthreads();
-        const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
-        const uint32_t st = perm_scan<NB>(cnt, s_tmp);
-        if (tid < (uint32_t)NB) {
-            s_start[tid] = st;
-            s_gofs[tid] = cnt ? (tid << s1) + atomicAdd(&cur[tid], cnt) : 0u;
-            s_cnt[tid] = 0;   // the next tile's atomics follow two barriers
-        }
-        __syncthreads();
+    for (int w = 0; w < WAVES; ++w) woff += (w < (int)wave) ? s_wtot[w] : 0u;
+    uint32_t slot[ITEMS];
+    uint64_t pr[ITEMS];
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j)
-            if (x[j] != ~0u) s_pair[s_start[x[j] >> s1] + slot[j]] = pr[j];
-        __syncthreads();
-        for (uint32_t q = tid; q < valid; q += BLOCK) {
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t r = woff + (uint32_t)__popcll(m[j] & le_mask);
+        woff += (uint32_t)__popcll(m[j]);
+        pr[j] = ((uint64_t)x[j] << 32) | r;
+        slot[j] = x[j] != ~0u ? atomicAdd(&s_cnt[x[j] >> s1], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
+    const uint32_t st = perm_scan<NB>(cnt, s_tmp);
+    if (tid < (uint32_t)NB) {
+        s_start[tid] = st;
+        s_gofs[tid] = cnt ? (tid << s1) + atomicAdd(&cur[tid], cnt) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (x[j] != ~0u) s_pair[s_start[x[j] >> s1] + slot[j]] = pr[j];
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + tid;
+        if (q < valid) {
             const uint64_t p = s_pair[q];
             const uint32_t b = (uint32_t)(p >> 32) >> s1;
             const uint64_t g = (uint64_t)s_gofs[b] + (q - s_start[b]);
-            if (g < ch.n) out[g] = p;
+            if (g < n) out[g] = p;
         }
-        run += ttot;
-        __syncthreads();
     }
 }
 
@@ -165,7 +214,11 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t q = j * BLOCK + tid;
-        p[j] = q < valid ? in[tb + q] : 0ull;
+        p[j] = in[tb + (q < valid ? q : valid - 1)];   // every load before the first use
+    }
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + tid;
         sub[j] = q < valid ? ((uint32_t)(p[j] >> 32) >> s2) & (nsub - 1u) : NB;
         slot[j] = sub[j] < (uint32_t)NB ? atomicAdd(&s_cnt[sub[j]], 1u) : 0u;
     }

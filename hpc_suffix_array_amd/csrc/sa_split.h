@@ -85,13 +85,12 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t x) {
 // Decoupled look-back of digit dg for tile t (the tile's AGGREGATE is
 // already published): sums predecessors' counts, kLook state words per
 // step, until an INCLUSIVE prefix; publishes this tile's own prefix.
-template <int RADIX, bool PROF = false>
+template <int RADIX, bool PROF = false, int kLook = 4>
 __device__ __forceinline__ uint64_t tile_lookback(uint64_t* __restrict__ states, uint64_t t, uint32_t dg,
                                                   uint32_t tile_cnt, uint64_t tag, uint32_t* __restrict__ err,
                                                   uint32_t* steps = nullptr) {
     uint64_t excl = 0;
     if (t == 0) return 0;
-    constexpr int kLook = 4;
     const uint32_t ep_now = (uint32_t)(tag >> 48) & kEpochMask;
     int64_t tp = (int64_t)t - 1;
     uint32_t spins = 0;
