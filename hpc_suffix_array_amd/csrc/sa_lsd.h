@@ -32,12 +32,15 @@ namespace sa {
 #define SA_LSD_PROF 0       // per-phase clock64 spans of k_lsd printed per pass (diagnostic builds)
 #endif
 // workgroup shapes (A/B overridable): PACKED passes of <= 9-bit digits and
-// unpacked ones; 10-bit digits always take 1024 x 8 (one thread per digit)
+// unpacked ones; 10-bit digits always take 1024 x 8 (one thread per digit).
+// 1 GiB DNA reference schedule (interleaved A/B, one box): packed 1024 x 8
+// 194.6 / 195.0 ms, 512 x 12 (two workgroups per CU) 191.4 / 191.7, 512 x 8
+// 202.3; unpacked 512 x 8 206 (kept 1024 x 8); 512 x 16 spills 45-78 VGPRs.
 #ifndef SA_LSD_PK_BLOCK
-#define SA_LSD_PK_BLOCK 1024
+#define SA_LSD_PK_BLOCK 512
 #endif
 #ifndef SA_LSD_PK_ITEMS
-#define SA_LSD_PK_ITEMS 8
+#define SA_LSD_PK_ITEMS 12
 #endif
 #ifndef SA_LSD_UP_BLOCK
 #define SA_LSD_UP_BLOCK 1024
