@@ -37,6 +37,7 @@
 #include "sa_lcp.h"
 #include "sa_onesweep.h"
 #include "sa_permute.h"
+#include "sa_pivot.h"
 #include "sa_split.h"
 #include "sa_lsd.h"
 
@@ -879,6 +880,76 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     return SA_OK;
 }
 
+// Unsorted-set round by a three-way pivot split (sa_pivot.h): dense ranks,
+// large groups on average.  Returns SA_OK with *sorted = nullptr when the
+// tied blocks turn out small (the caller then sorts the whole set).
+static bool pivot_ok(uint64_t m, uint64_t G, uint32_t wr, bool sparse, int radix) {
+    return std::getenv("SA_NO_PIVOT") == nullptr && radix == 0 && !sparse && m >= (1u << 16) && G >= 1 && G <= m / 4 && bit_width(2 * G + 1) + wr <= 64;
+}
+
+static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, uint64_t G, uint64_t h, uint32_t wr,
+                       uint64_t* ukb0, uint64_t* ukb1, uint64_t* kbA, const Chunking& cu, hipStream_t s, Timer& tm,
+                       sa_stats* st, uint64_t** sorted, uint32_t* P) {
+    *sorted = nullptr;
+    uint32_t* const gs = c->u_pos[uo];   // G + 1 group starts (the next set is written by segments())
+    uint32_t* const gP = c->vals_alt;    // 3 (G + 1): members of each class before each group
+    uint32_t* const cc = c->hist;        // 3 x chunks class counts, scanned in place
+    const uint32_t Gu = (uint32_t)G;
+    tm.begin(SA_K_SORT_U);
+    hipLaunchKernelGGL(k_pivot_keys, dim3((uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192)), dim3(kBlock),
+                       0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m, (const uint32_t*)c->rank,
+                       n, h, wr, Gu, ukb1, gs);
+    hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
+                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs, Gu, wr, cc,
+                       gP, nullptr, nullptr, nullptr, nullptr);
+    hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_SORT_U, 28 * m);
+    SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
+    if (t0 + t1 + t2 != m) return set_err(SA_E_INTERNAL, "pivot classes %llu + %llu + %llu != %llu",
+                                          (unsigned long long)t0, (unsigned long long)t1, (unsigned long long)t2,
+                                          (unsigned long long)m);
+    SA_TRACE("  round h=%llu: pivot split, tied %llu of %llu", (unsigned long long)h, (unsigned long long)t1,
+             (unsigned long long)m);
+    if (t1 * 2 < m) return SA_OK;   // mostly distinct keys: the full sort is cheaper
+    tm.begin(SA_K_SORT_U);
+    hipLaunchKernelGGL(k_pivot_gp, dim3((uint32_t)std::min<uint64_t>((G + kBlock) / kBlock, 8192)), dim3(kBlock), 0, s,
+                       (const uint32_t*)gs, Gu, (const uint32_t*)cc, cu, (const uint32_t*)c->totals, gP);
+    hipLaunchKernelGGL(k_pivot_pass<2>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
+                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs, Gu, wr, cc,
+                       gP, ukb0, c->vals_u, kbA, c->u_idx[uo]);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_SORT_U, 36 * m);
+    const uint64_t mr = t0 + t2;
+    uint32_t Pr = 0;
+    if (mr > 0) {
+        // the rest sorted by (2 g + [> pivot], rank): values in u_idx / u_g
+        // of the next set (free until segments()), keys through kbA and ukb1
+        const uint32_t bits = bit_width(2 * G - 1) + wr;
+        const uint32_t Pn = (bits + 7) / 8;
+        uint32_t* vfinal = (Pn & 1u) ? c->u_g[uo] : c->u_idx[uo];
+        uint32_t* vother = (Pn & 1u) ? c->u_idx[uo] : c->u_g[uo];
+        uint64_t* rs = nullptr;
+        int rc = radix_sort(c, SrcKeys{kbA, c->u_idx[uo]}, 12 * mr, plan_chunks(mr), bits, vfinal, vother, ukb1, kbA, s,
+                            tm, st, &rs, &Pr, false, true);
+        if (rc) return rc;
+        tm.begin(SA_K_SORT_U);
+        hipLaunchKernelGGL(k_pivot_place, dim3((uint32_t)std::min<uint64_t>((mr + kBlock - 1) / kBlock, 8192)),
+                           dim3(kBlock), 0, s, (const uint64_t*)rs, (const uint32_t*)vfinal, mr, (const uint32_t*)gs,
+                           (const uint32_t*)gP, Gu, wr, ukb0, c->vals_u, m);
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_SORT_U, 24 * mr);
+    }
+    *sorted = ukb0;
+    *P = 1 + Pr;
+    return SA_OK;
+}
+
 static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                         const sa_opts* opts, sa_stats* st, Timer& tm) {
     Events ev;
@@ -1037,6 +1108,11 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             }
             SA_TRACE("  round h=%llu: per-group register sort %s", (unsigned long long)h,
                      sorted ? "done" : "found a large group");
+        }
+        if (!sorted && pivot_ok(m, G, wr, sparse, c->radix)) {
+            uint64_t* kbA = ukb0 == c->keys[0] ? c->keys[1] : c->keys[0];   // the round-1 keys: dead with dense ranks
+            rc = pivot_round(c, ui, uo, n, m, G, h, wr, ukb0, ukb1, kbA, cu, s, tm, st, &sorted, &P);
+            if (rc) return rc;
         }
         if (sorted) {
             rc = SA_OK;

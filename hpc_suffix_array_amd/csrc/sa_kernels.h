@@ -1188,20 +1188,33 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
             tuh += b;
             tl = l > tl ? l : tl;
         }
-#pragma unroll 2
+        // every row's index and position loaded before any is used; the
+        // position of a member's group head comes from its row by a shuffle,
+        // or is carried from the last head of an earlier row (one load per
+        // wave and tile instead of a dependent load per member)
+        uint32_t xs[kItems], ps[kItems];
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t s = w0 + (uint64_t)j * kWave + lane;
+            xs[j] = s < e1 ? idx[s] : 0u;
+            ps[j] = s < e1 ? pos(s) : 0u;
+        }
+        uint32_t carried_pos = carried > 0 ? pos((uint64_t)carried - 1u) : 0u;
+#pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t rb = w0 + (uint64_t)j * kWave;
-            if (rb >= e1) break;
             const uint64_t mf = s_m[wave][j][0], mu = s_m[wave][j][1], muh = s_m[wave][j][2];
             const uint64_t s = rb + lane;
+            const uint64_t mh = mf & le;
+            const uint32_t hl = mh ? 63u - (uint32_t)__clzll(mh) : 0u;
+            const uint32_t hrow = (uint32_t)__shfl((int)ps[j], (int)hl, kWave);
+            const uint32_t hp = mh ? hrow : carried_pos;
             // sparse first round: rows without unsorted members write nothing
             if ((dense_rank || sa || mu) && s < e1) {
-                const uint64_t mh = mf & le;
-                const uint64_t hs = mh ? rb + 63 - __clzll(mh) : (uint64_t)carried - 1u;
-                const uint32_t x = idx[s];
-                const uint32_t p = pos(s);
+                const uint32_t x = xs[j];
+                const uint32_t p = ps[j];
                 const bool in_u = (mu >> lane) & 1ull;
-                if (dense_rank || in_u) rank[rm.slot(x)] = rank_off + (hs == s ? p : pos(hs)) + 1u;
+                if (dense_rank || in_u) rank[rm.slot(x)] = rank_off + hp + 1u;
                 if (sa) sa[p] = x;
                 if (member && in_u) atomicOr(&member[x >> 5], 1u << (x & 31));
                 if (in_u) {
@@ -1213,7 +1226,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
             }
             off_u += __popcll(mu);
             off_uh += __popcll(muh);
-            if (mf) carried = (uint32_t)(rb + 63 - __clzll(mf)) + 1u;
+            if (mf) {
+                const uint32_t ll = 63u - (uint32_t)__clzll(mf);
+                carried = (uint32_t)(rb + ll) + 1u;
+                carried_pos = (uint32_t)__shfl((int)ps[j], (int)ll, kWave);
+            }
         }
         run_u += tu;
         run_uh += tuh;

@@ -1,0 +1,196 @@
+// sa_pivot.h -- three-way pivot split of an unsorted-set round with large
+// groups (Larsson-Sadakane's ternary split, applied once per round).
+//
+// An unsorted-set round (packed schedule, rounds h >= K) sorts every group g
+// of the unsorted set U by its members' keys rank[x + h] (manber_myers.c:98,
+// the two counting passes, restricted to U).  Ties may end in any order: the
+// round only needs the classes of equal keys.  When groups are large, most
+// members of a group often share one key -- a text of one repeated symbol
+// (configs[4]: every round keeps one group of ~n members, all but ~h of them
+// with the group's own rank as key), long repeats, short periods.  There the
+// LSD sort of all m members (4 passes of 12 bytes at 2^30) moves everything
+// to reorder a few.  Instead, per group, with pivot p = the key of the
+// group's first member:
+//   * members with key == p keep nothing but their group: they are written
+//     once, in U order, as one tied block;
+//   * members with key < p and key > p (the "rest", m' of them) are sorted by
+//     (2 g + [key > p], key) with the ordinary radix sort and placed before /
+//     after the tied block.
+// New layout of group g (its U slots [gs_g, gs_{g+1}) keep their SA
+// positions): [< p sorted][== p][> p sorted].  segments() then sees the same
+// (key, index) stream a full sort would produce, up to the order of ties.
+//
+// Kernels (Chunking over U, one workgroup per chunk walking 4096-member
+// tiles; wave w owns a contiguous 1024 slice, rows of 64 lanes):
+//   k_pivot_keys    key(e) = g << wr | rank[x + h] (dense ranks) and the
+//                   group starts gs[g] (gs[G] = m)
+//   k_pivot_pass<0> class counts per chunk (k_scan_rows then gives P_c at
+//                   each chunk start) and per group start inside its chunk
+//   k_pivot_gp      gP[c][g] = P_c(gs_g) (members of class c before g)
+//   k_pivot_pass<2> tied members to their final slots, the rest compacted
+//   k_pivot_place   the sorted rest to their final slots
+#pragma once
+#include "sa_kernels.h"
+
+namespace sa {
+
+// keys of a pivot round (dense ranks only) and the group starts
+__global__ __launch_bounds__(kBlock) void k_pivot_keys(const uint32_t* __restrict__ u_idx,
+                                                       const uint32_t* __restrict__ u_g, uint64_t m,
+                                                       const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
+                                                       uint32_t wr, uint32_t G, uint64_t* __restrict__ keys,
+                                                       uint32_t* __restrict__ gs) {
+    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < m; e += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t x = u_idx[e];
+        const uint32_t g = u_g[e];
+        const uint64_t r1 = x + h < n ? rank[x + h] : 0u;
+        keys[e] = ((uint64_t)g << wr) | r1;
+        if (e == 0 || u_g[e - 1] != g) gs[g] = (uint32_t)e;
+        if (e == m - 1) gs[G] = (uint32_t)m;
+    }
+}
+
+// MODE 0: cc[c * chunks + chunk] = members of class c in the chunk, and for
+//         every group starting in the chunk gP[c * (G + 1) + g] = members of
+//         class c before gs_g inside the chunk (k_pivot_gp adds the chunk's
+//         scanned offset).
+// MODE 2: tied members -> okeys / oidx at their final slots; the rest ->
+//         rkeys / ridx at (members of classes 0 and 2 before them).
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restrict__ keys,
+                                                       const uint32_t* __restrict__ u_idx,
+                                                       const uint32_t* __restrict__ u_g, Chunking ch,
+                                                       const uint32_t* __restrict__ gs, uint32_t G, uint32_t wr,
+                                                       uint32_t* __restrict__ cc, uint32_t* __restrict__ gP,
+                                                       uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
+                                                       uint64_t* __restrict__ rkeys, uint32_t* __restrict__ ridx) {
+    __shared__ uint32_t s_w[3][kWaves];
+    const uint32_t c = blockIdx.x;
+    const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
+    const uint32_t wave = wave_id(), lane = lane_id();
+    const uint64_t lt = lanemask_lt();
+    uint32_t run[3] = {0, 0, 0};
+    if (MODE == 2)
+        for (int k = 0; k < 3; ++k) run[k] = cc[(uint64_t)k * ch.chunks + c];
+    const uint64_t gstride = (uint64_t)G + 1;
+    for (uint64_t tb = e0; tb < e1; tb += kTile) {
+        const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
+        uint64_t key[kItems];
+        uint32_t g[kItems];
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+            key[j] = e < e1 ? keys[e] : 0ull;
+            g[j] = e < e1 ? u_g[e] : 0u;
+        }
+        uint32_t cls[kItems];
+        uint32_t wc[3] = {0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < kItems; ++j) {
+            const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+            const uint64_t p = e < e1 ? keys[gs[g[j]]] : 0ull;
+            cls[j] = e < e1 ? (key[j] < p ? 0u : key[j] == p ? 1u : 2u) : 3u;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) wc[k] += (uint32_t)__popcll(__ballot(cls[j] == (uint32_t)k));
+        }
+        if (lane == 0)
+            for (int k = 0; k < 3; ++k) s_w[k][wave] = wc[k];
+        __syncthreads();
+        uint32_t off[3], tot[3];
+        for (int k = 0; k < 3; ++k) {
+            off[k] = run[k];
+            tot[k] = 0;
+            for (int w = 0; w < kWaves; ++w) {
+                const uint32_t v = s_w[k][w];
+                off[k] += (w < (int)wave) ? v : 0u;
+                tot[k] += v;
+            }
+        }
+        {
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                uint64_t bm[3];
+#pragma unroll
+                for (int k = 0; k < 3; ++k) bm[k] = __ballot(cls[j] == (uint32_t)k);
+                if (e < e1) {
+                    // P_c(e): members of class c before e
+                    const uint32_t P0 = off[0] + (uint32_t)__popcll(bm[0] & lt);
+                    const uint32_t P1 = off[1] + (uint32_t)__popcll(bm[1] & lt);
+                    const uint32_t P2 = off[2] + (uint32_t)__popcll(bm[2] & lt);
+                    const uint32_t gg = g[j];
+                    const uint32_t s0 = gs[gg];
+                    if (MODE == 0) {
+                        if (s0 == (uint32_t)e) {   // in-chunk counts before the group start
+                            gP[gg] = P0;
+                            gP[gstride + gg] = P1;
+                            gP[2 * gstride + gg] = P2;
+                        }
+                    } else {
+                        const uint32_t x = u_idx[e];
+                        if (cls[j] == 1u) {
+                            const uint32_t cnt0 = gP[gg + 1] - gP[gg];
+                            const uint64_t ne = (uint64_t)s0 + cnt0 + (P1 - gP[gstride + gg]);
+                            okeys[ne] = key[j];
+                            oidx[ne] = x;
+                        } else {
+                            const uint64_t ri = (uint64_t)P0 + P2;
+                            rkeys[ri] = ((uint64_t)(2u * gg + (cls[j] == 2u ? 1u : 0u)) << wr) |
+                                        (key[j] & ((1ull << wr) - 1ull));
+                            ridx[ri] = x;
+                        }
+                    }
+                }
+#pragma unroll
+                for (int k = 0; k < 3; ++k) off[k] += (uint32_t)__popcll(bm[k]);
+            }
+        }
+        for (int k = 0; k < 3; ++k) run[k] += tot[k];
+        __syncthreads();
+    }
+    if (MODE == 0 && threadIdx.x == 0)
+        for (int k = 0; k < 3; ++k) cc[(uint64_t)k * ch.chunks + c] = run[k];
+}
+
+// gP[c][g] += the scanned class-c count before the chunk holding gs_g;
+// gP[c][G] = the class totals (one thread per group)
+__global__ __launch_bounds__(kBlock) void k_pivot_gp(const uint32_t* __restrict__ gs, uint32_t G,
+                                                     const uint32_t* __restrict__ cc, Chunking ch,
+                                                     const uint32_t* __restrict__ totals, uint32_t* __restrict__ gP) {
+    const uint64_t gstride = (uint64_t)G + 1;
+    const uint64_t csize = (uint64_t)ch.tiles_per_chunk * kTile;
+    for (uint64_t g = (uint64_t)blockIdx.x * kBlock + threadIdx.x; g <= G; g += (uint64_t)gridDim.x * kBlock) {
+        if (g == G) {
+            for (int k = 0; k < 3; ++k) gP[k * gstride + G] = totals[k];
+        } else {
+            const uint64_t chunk = gs[g] / csize;
+            for (int k = 0; k < 3; ++k) gP[k * gstride + g] += cc[(uint64_t)k * ch.chunks + chunk];
+        }
+    }
+}
+
+// the sorted rest (keys (2 g + [> p]) << wr | rank) to the final slots of
+// their group: class 0 first, class 2 after the tied block
+__global__ __launch_bounds__(kBlock) void k_pivot_place(const uint64_t* __restrict__ rkeys,
+                                                        const uint32_t* __restrict__ ridx, uint64_t mr,
+                                                        const uint32_t* __restrict__ gs,
+                                                        const uint32_t* __restrict__ gP, uint32_t G, uint32_t wr,
+                                                        uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
+                                                        uint64_t m) {
+    const uint64_t gstride = (uint64_t)G + 1;
+    for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < mr; j += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t k = rkeys[j];
+        const uint32_t sub = (uint32_t)(k >> wr);
+        const uint32_t g = sub >> 1;
+        if (g >= G) continue;
+        const uint32_t R = gP[g] + gP[2 * gstride + g];           // rest members before group g
+        const uint32_t cnt1 = gP[gstride + g + 1] - gP[gstride + g];
+        const uint64_t ne = (sub & 1u) ? (uint64_t)gs[g] + cnt1 + (j - R) : (uint64_t)gs[g] + (j - R);
+        if (ne < m) {
+            okeys[ne] = ((uint64_t)g << wr) | (k & ((1ull << wr) - 1ull));
+            oidx[ne] = ridx[j];
+        }
+    }
+}
+
+}  // namespace sa

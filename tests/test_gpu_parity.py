@@ -149,6 +149,36 @@ def test_degenerate(gpu, n, schedule):
     assert st["distinct"][-1] == n
 
 
+@pytest.mark.parametrize("pivot", [True, False])
+def test_pivot_split_rounds(gpu, oracle, pivot, monkeypatch):
+    """Unsorted-set rounds with large groups by the three-way pivot split
+    (sa_pivot.h): periodic texts with sparse noise (a dominant key per group,
+    plus members below and above the pivot), runs of one symbol inside random
+    text, and a short first key on random DNA (many distinct keys per group:
+    the split gives up and the full sort runs); SA_NO_PIVOT forces the full
+    LSD sort for comparison."""
+    from hpc_suffix_array_amd import build_suffix_array
+    if not pivot:
+        monkeypatch.setenv("SA_NO_PIVOT", "1")
+    rng = np.random.default_rng(7)
+    cases = []
+    for period, noise, n in ((b"ab", 0.002, 400_003), (b"abc", 0.01, 300_001), (b"aab", 0.0005, 1 << 20)):
+        t = np.frombuffer((period * (n // len(period) + 1))[:n], np.uint8).copy()
+        hit = rng.random(n) < noise
+        t[hit] = rng.integers(ord("a"), ord("e"), int(hit.sum()), dtype=np.uint8)
+        cases.append(t)
+    t = oracle.gen_text("dna", 500_000, seed=3)
+    t[100_000:260_000] = ord("G")
+    cases.append(t)
+    for t in cases:
+        got = build_suffix_array(t)
+        assert (got == oracle.sa_c(t)).all(), (len(t), pivot)
+    for n in (70_001, 1_000_000):
+        t = oracle.gen_text("dna", n, seed=n)
+        got = build_suffix_array(t, init_chars=2)
+        assert (got == oracle.sa_c(t)).all(), (n, pivot)
+
+
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
 def test_periodic(gpu, oracle, schedule):
     from hpc_suffix_array_amd import build_suffix_array
