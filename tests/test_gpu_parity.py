@@ -407,13 +407,19 @@ def _multi_rank_worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 5])
 def test_distributed_hip_multi_rank(gpu, world):
-    """The range-partitioned build with real HIP phases on 2-3 ranks (all on
+    """The range-partitioned build with real HIP phases on 2-5 ranks (all on
     the box's one GPU; the 8-GPU RCCL run is the driver's): cuts into
     unequal ranges, rank requests answered by other ranks, several doubling
     rounds (periodic text), the sample-sort fallback (one symbol) -- every SA
-    equal to the oracle's."""
+    equal to the oracle's.  From 4 ranks a range holds <= 0.3 n suffixes and
+    round 1 sorts records counted and emitted by k_bucket_hist<.., 1 / 2>
+    (k_split_list) instead of filtering the text in k_split_text."""
+    _multi_rank(world)
+
+
+def _multi_rank(world):
     import socket
 
     import torch.multiprocessing as mp
