@@ -145,6 +145,27 @@ def test_bench_picks_the_profile_of_the_current_sources(tmp_path):
     assert s is not None and s["tag"] != "r02_o"
 
 
+def test_reference_schedule_round_model():
+    """bench.py's per-round roofline of the reference schedule follows
+    SURVEY.md 8(d): P_j from D_{j-1} with D_0 = 256, B_j = n (3 rb + 2 S
+    (P_j + 1)); configs[2] (1 GiB DNA) gives P = [3, 2, 3, 5, 8], 684 B per
+    suffix over the five rounds (734 GB, the 91.8 ms floor)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 1 << 30
+    d = [17, 259, 65543, 950039036, n]
+    rows = bench.model_rounds(n, d, [10.0] * 5)
+    assert [r["P_model"] for r in rows] == [3, 2, 3, 5, 8]
+    assert sum(r["model_bytes"] for r in rows) == 684 * n
+    assert abs(sum(r["model_bytes"] for r in rows) / 8.0e12 * 1e3 - 91.8) < 0.1
+    assert abs(rows[0]["frac"] - 108 * n / 10e-3 / 8.0e12) < 1e-3
+    # configs[1] (64 MiB DNA): P = [3, 2, 3, 5, 7], 660 B per suffix
+    m = 1 << 26
+    rows = bench.model_rounds(m, [17, 259, 65543, 16744000 * 4, m], [1.0] * 5)
+    assert [r["P_model"] for r in rows] == [3, 2, 3, 5, 7]
+    assert sum(r["model_bytes"] for r in rows) == 660 * m
+
+
 def test_scaling_harness_columns_and_commands():
     """scripts/benchmark_scaling.py: the mpi_results.csv columns of the
     reference's sweep (benchmark_mpi.py:180-210) from bench.py JSON lines, and
