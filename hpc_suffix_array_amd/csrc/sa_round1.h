@@ -51,6 +51,21 @@ constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
 // bucketed round's one-GPU maximum; their starts live in the onesweep base
 // scratch after the second pass's 2^hb (<= 1024) digit bases
 constexpr uint64_t kPadMinN = 1ull << 26;
+// first-pass cursor stripes with padded segments (SA_TEXT_STRIPES overrides:
+// 1 = one cursor per digit shared by every tile, ticketed tiles)
+static uint32_t text_stripes() {
+    const char* e = std::getenv("SA_TEXT_STRIPES");
+    const uint32_t v = e ? (uint32_t)std::atoi(e) : 8u;
+    return v >= 8 ? 8u : v >= 4 ? 4u : v >= 2 ? 2u : 1u;
+}
+
+// out[d] = sum of rows r < rows of in[r][d] (kLoRadix columns)
+__global__ __launch_bounds__(kLoRadix) void k_sum_rows(const uint32_t* __restrict__ in, uint32_t rows,
+                                                       uint32_t* __restrict__ out) {
+    uint32_t t = 0;
+    for (uint32_t r = 0; r < rows; ++r) t += in[r * kLoRadix + threadIdx.x];
+    out[threadIdx.x] = t;
+}
 constexpr uint64_t kPadMaxN = 1ull << 31;
 constexpr uint32_t kPadStartOff = kLoRadix + 1024;                 // kLoRadix + 1 words
 constexpr uint32_t kPadDenseOff = kPadStartOff + kLoRadix + 64;    // kLoRadix words
@@ -287,7 +302,13 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // low, [kLoRadix, +2^hb) high
     uint32_t* const g_lo = os_ghist(c);
     uint32_t* const g_hi = os_ghist(c) + kLoRadix;
-    uint32_t* const cursor = os_ghist(c) + 5 * kRadix;
+    // padded segments: the first pass's cursors striped over `stripes`
+    // sub-segments (k_split_text; rows [s][digit] in the chunk histograms,
+    // free in the bucketed round), the row sums after them
+    const uint32_t stripes = padded ? text_stripes() : 1u;
+    uint32_t* const cursor = stripes > 1 ? c->hist : os_ghist(c) + 5 * kRadix;
+    uint32_t* const cursor_sum = stripes > 1 ? c->hist + kMaxStripes * kLoRadix : cursor;
+    if (stripes > 1) SA_HIP(hipMemsetAsync(cursor, 0, (size_t)stripes * kLoRadix * 4, s));
     if (!padded) {
         tm.begin(SA_K_SCAN);
         hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_lo, kLoRadix, os_base(c));
@@ -314,7 +335,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n,  \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
-                       padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib)
+                       padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib, \
+                       stripes)
         if (listed) {
             constexpr int kItemsL = SA_ITEMS_B, kListBlock = SA_LIST_BLOCK;
             const uint64_t tl = (uint64_t)kListBlock * kItemsL;
@@ -343,8 +365,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
     // padded: the dense segment starts from the first pass's final cursors
-    if (padded)
-        hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)cursor, kLoRadix, dlo);
+    if (padded) {
+        if (stripes > 1)
+            hipLaunchKernelGGL(k_sum_rows, dim3(1), dim3(kLoRadix), 0, s, (const uint32_t*)cursor, stripes, cursor_sum);
+        hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)cursor_sum, kLoRadix, dlo);
+    }
     tm.end();
     tm.begin(SA_K_SCATTER_KEYS);
     {
@@ -368,7 +393,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock)>), dim3(grid),                    \
                        dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                                  \
                        (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,          \
-                       c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr)
+                       c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr, \
+                       stripes)
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
         if (pk8) SA_SEG_LAUNCH(SrcPk8, B, sp, 64u - B, kItemsPk);                                             \

@@ -358,7 +358,15 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                                                          uint64_t m, uint32_t blo, uint32_t bhi,
                                                          const uint32_t* __restrict__ seg_end = nullptr,
                                                          uint32_t* __restrict__ ovf = nullptr, uint32_t pk_hb = 0,
-                                                         uint32_t pk_ib = 0) {
+                                                         uint32_t pk_ib = 0, uint32_t stripes = 1) {
+    // stripes > 1 (padded segments only): digit d's segment is cut into
+    // `stripes` equal sub-segments and workgroup w claims in sub-segment
+    // w % stripes from its own cursor cursor[(w % stripes) * RADIX + d]:
+    // device-scope atomics on one address serialise at ~19 ns each
+    // (microbench_claims.hip), and 256 cursors shared by every tile took a
+    // claim per tile and digit.  1 GiB DNA, interleaved A/B: 1 stripe 4.01 /
+    // 4.02 ms, 8 stripes 3.70 / 3.70 (tiles assigned statically instead of
+    // by the ticket: 3.80 / 3.91; 2 or 4 stripes static 4.16 / 4.22).
     static_assert(!PK8 || POW2, "packed items need a power-of-two alphabet (Dmin(bucket) by a shift)");
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
@@ -387,8 +395,15 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     const uint32_t dg = threadIdx.x;
     const uint64_t tiles = (n + TILE - 1) / TILE;
     const uint32_t K = b.s + b.R;
+    const uint32_t stripe = blockIdx.x % stripes;
+    uint32_t sbase = 0;               // this workgroup's sub-segment start in digit dg
     for (uint32_t i = dg; i < 1024u; i += BLOCK) s_hhi[i] = 0;
-    if (seg_end && dg < (uint32_t)RADIX) s_gend[dg] = seg_end[dg];
+    if (seg_end && dg < (uint32_t)RADIX) {
+        const uint32_t lo = digit_base[dg], hi = seg_end[dg], sc = (hi - lo) / stripes;
+        sbase = lo + stripe * sc;
+        s_gend[dg] = stripe + 1 == stripes ? hi : sbase + sc;
+    }
+    cursor += stripe * RADIX;
     if (dg < 256u) {
         const uint32_t cv = code[dg];
         s_map[dg] = (uint8_t)(cv ? cv - 1u : 0u);
@@ -528,7 +543,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             // the pass need not be stable, so a tile's place in each digit
             // is claimed from a cursor (one atomic round trip, whatever the
             // other tiles do) instead of a look-back
-            dbase = digit_base[dg];
+            dbase = seg_end ? sbase : digit_base[dg];
             clm = tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u;
         }
         {
@@ -772,6 +787,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
 // 8 B written (and read by the local sort) instead of 12.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kSegs = kLoRadix;
+constexpr uint32_t kMaxStripes = 8;   // first-pass cursor stripes (k_split_text)
 constexpr uint64_t segw_words(int radix) { return 3ull * kSegs * radix + kSegs; }
 // the bucket starts live after the widest pass's segment words
 constexpr uint64_t kBstartOff = segw_words(1024);
@@ -787,7 +803,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                                                         uint32_t ib, uint64_t* __restrict__ out_w,
                                                         uint32_t* __restrict__ err,
                                                         const uint32_t* __restrict__ seg_cnt = nullptr,
-                                                        const uint32_t* __restrict__ dense_lo = nullptr) {
+                                                        const uint32_t* __restrict__ dense_lo = nullptr,
+                                                        uint32_t stripes = 1) {
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
@@ -801,7 +818,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     __shared__ uint16_t s_start[RADIX];
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[(BLOCK / kWave)];
-    __shared__ uint32_t s_ubase[kSegs + 1];   // units before segment l (exclusive scan)
+    __shared__ uint32_t s_ubase[kSegs * kMaxStripes + 1];   // units before sub-segment q (exclusive scan)
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_last;
     __shared__ uint32_t s_claim[RADIX];
@@ -813,42 +830,57 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint32_t mask = RADIX - 1;
-    // segment l of the input: [lo_base[l], the next segment's start) or,
-    // padded (seg_cnt), [lo_base[l], lo_base[l] + seg_cnt[l]); dense_lo: the
-    // pairs before segment l (0: every earlier segment is empty)
-    auto seg_lo = [&](uint32_t l) -> uint64_t { return lo_base[l]; };
-    auto seg_hi = [&](uint32_t l) -> uint64_t {
-        if (seg_cnt) return (uint64_t)lo_base[l] + seg_cnt[l];
+    // sub-segment q = l * stripes + s of the input (s < stripes; one per
+    // segment unless the first pass striped its cursors): [lo, hi) with
+    // lo = lo_base[l] + s * ((lo_base[l + 1] - lo_base[l]) / stripes) and,
+    // padded (seg_cnt), hi = lo + seg_cnt[s * kSegs + l]; unpadded, segment l
+    // is [lo_base[l], the next segment's start).  dense_lo: the pairs before
+    // segment l (0: every earlier segment is empty)
+    const uint32_t nsub = kSegs * stripes;
+    auto sub_lo = [&](uint32_t q) -> uint64_t {
+        const uint32_t l = q / stripes, sidx = q % stripes;
+        if (stripes == 1) return lo_base[l];
+        return (uint64_t)lo_base[l] + sidx * ((lo_base[l + 1] - lo_base[l]) / stripes);
+    };
+    auto sub_hi = [&](uint32_t q) -> uint64_t {
+        const uint32_t l = q / stripes, sidx = q % stripes;
+        if (seg_cnt) return sub_lo(q) + seg_cnt[sidx * kSegs + l];
         return l + 1 < kSegs ? (uint64_t)lo_base[l + 1] : n;
     };
     const uint32_t* const dlo = dense_lo ? dense_lo : lo_base;
-    auto units_of = [&](uint32_t l) -> uint32_t { return (uint32_t)((seg_hi(l) - seg_lo(l) + TILE - 1) / TILE); };
-    // unit numbering: segment by segment
+    // unit numbering: sub-segment by sub-segment (nsub <= BLOCK * 2)
     {
-        const uint32_t x = dg < kSegs ? units_of(dg) : 0u;
+        uint32_t x0 = 0, x1 = 0;
+        const uint32_t q0 = 2 * dg, q1 = 2 * dg + 1;
+        if (q0 < nsub) x0 = (uint32_t)((sub_hi(q0) - sub_lo(q0) + TILE - 1) / TILE);
+        if (q1 < nsub) x1 = (uint32_t)((sub_hi(q1) - sub_lo(q1) + TILE - 1) / TILE);
+        const uint32_t x = x0 + x1;
         const uint32_t inc = wave_inclusive_sum(x);
         if (lane == kWave - 1) s_tmp[wave] = inc;
         __syncthreads();
         uint32_t off = 0;
         for (uint32_t w = 0; w < wave; ++w) off += s_tmp[w];
-        if (dg < kSegs) s_ubase[dg] = off + inc - x;
-        if (dg == kSegs - 1) s_ubase[kSegs] = off + inc;
+        if (q0 < nsub) s_ubase[q0] = off + inc - x;
+        if (q1 < nsub) s_ubase[q1] = off + inc - x1;
+        if (q1 + 1 >= nsub && q0 < nsub) s_ubase[nsub] = off + inc;
     }
     if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
     __syncthreads();
-    const uint32_t units = s_ubase[kSegs];
+    const uint32_t units = s_ubase[nsub];
+    // units of segment l (all its sub-segments)
+    auto units_of = [&](uint32_t l) -> uint32_t { return s_ubase[(l + 1) * stripes] - s_ubase[l * stripes]; };
     // unit -> (segment, first position, size)
     auto locate = [&](uint32_t u, uint32_t& l, uint64_t& tb, uint32_t& valid) {
-        uint32_t a = 0, b = kSegs;   // last l with s_ubase[l] <= u (units of empty segments are skipped)
+        uint32_t a = 0, b = nsub;   // last q with s_ubase[q] <= u (units of empty sub-segments are skipped)
         while (b - a > 1) {
             const uint32_t mid = (a + b) / 2;
             if (s_ubase[mid] <= u) a = mid;
             else b = mid;
         }
-        l = a;
-        tb = seg_lo(a) + (uint64_t)(u - s_ubase[a]) * TILE;
-        const uint64_t e = seg_hi(a);
+        l = a / stripes;
+        tb = sub_lo(a) + (uint64_t)(u - s_ubase[a]) * TILE;
+        const uint64_t e = sub_hi(a);
         valid = (uint32_t)(e - tb < (uint64_t)TILE ? e - tb : (uint64_t)TILE);
     };
     uint64_t k[ITEMS];
@@ -950,7 +982,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                 for (uint32_t l2 = l + 1; l2 < kSegs; ++l2) {
                     __hip_atomic_store(&sbase[(uint64_t)l2 * RADIX + dg], kReady | (uint64_t)(s_claim[dg] + tot),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if (seg_hi(l2) > seg_lo(l2)) break;
+                    if (units_of(l2) > 0) break;
                 }
             }
         }
