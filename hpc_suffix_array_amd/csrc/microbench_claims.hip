@@ -24,7 +24,10 @@ __global__ __launch_bounds__(512) void k_claims(uint32_t* cur, uint32_t* ticket,
         const uint32_t t = s_t;
         __syncthreads();
         if (t >= tiles) break;
-        if (threadIdx.x < radix) acc += atomicAdd(&cur[(t % stripes) * radix + threadIdx.x], 24u);
+        // stripes > 0: row t % stripes; stripes == 0: row t / per_seg (the
+        // second pass: consecutive units share a segment's cursors)
+        const uint32_t row = stripes ? t % stripes : (t / 341u) % 256u;
+        if (threadIdx.x < radix) acc += atomicAdd(&cur[row * radix + threadIdx.x], 24u);
         __syncthreads();
     }
     if (acc == 0xFFFFFFFFu) sink[0] = acc;
@@ -33,7 +36,7 @@ __global__ __launch_bounds__(512) void k_claims(uint32_t* cur, uint32_t* ticket,
 int main(int argc, char** argv) {
     const uint32_t tiles = argc > 1 ? std::atoi(argv[1]) : 174763;
     uint32_t *cur, *tick, *sink;
-    CK(hipMalloc(&cur, 64 * 1024 * 4));
+    CK(hipMalloc(&cur, 256 * 1024 * 4));
     CK(hipMalloc(&tick, 4));
     CK(hipMalloc(&sink, 4));
     int cus = 0;
@@ -42,11 +45,11 @@ int main(int argc, char** argv) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     for (uint32_t radix : {256u, 512u}) {
-        for (uint32_t stripes : {1u, 8u, 64u}) {
+        for (uint32_t stripes : {1u, 8u, 64u, 0u}) {
             for (int wpc : {1, 2}) {
                 std::vector<float> t;
                 for (int r = 0; r < 4; ++r) {
-                    CK(hipMemset(cur, 0, 64 * 1024 * 4));
+                    CK(hipMemset(cur, 0, 256 * 1024 * 4));
                     CK(hipMemset(tick, 0, 4));
                     CK(hipEventRecord(a));
                     hipLaunchKernelGGL(k_claims, dim3(cus * wpc), dim3(512), 0, 0, cur, tick, tiles, radix, stripes, sink);
