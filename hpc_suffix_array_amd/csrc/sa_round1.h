@@ -492,9 +492,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     br_measured.bits1 = 0;
     // the fixed-span 32-bit local sort (k_bucket_sort): the key bits below a
     // sub-bucket fit beside the load slot, and buckets are large enough that
-    // windows hold one bucket each (n / 2^bb >= 4 window strides)
+    // windows hold one bucket each (suffixes per bucket of the range >= 4
+    // window strides; a rank's range holds m suffixes in bhi - blo buckets --
+    // m >> bb undercounted them by G, and ranges took k_bucket_sort_wide)
     const bool fast32 = br.bits1 > (uint32_t)kSubBits && br.bits1 - kSubBits <= kLowMax &&
-                        (m >> bp.bs.bb) >= 4 * kWinStride && !std::getenv("SA_NO_FAST32");
+                        m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !std::getenv("SA_NO_FAST32");
     // one-bucket window headers after the retry list (16-byte aligned; 11 nw + 8 <= capacity)
     uint4* const hdr = reinterpret_cast<uint4*>(((uintptr_t)(retry + nw + 4) + 15) & ~(uintptr_t)15);
     auto local_sort = [&](const SegOut& o) {

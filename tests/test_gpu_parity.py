@@ -349,9 +349,11 @@ def test_distributed_hip_single_rank(gpu, oracle):
         dist.destroy_process_group()
 
 
-def _multi_rank_worker(rank, world, port, q):
+def _multi_rank_worker(rank, world, port, q, large=False):
     """One rank of a world sharing the box's GPU: HIP phases on cuda:0, the
-    collectives through a gloo group (staged via host memory)."""
+    collectives through a gloo group (staged via host memory).  large: one
+    DNA text of 402 M suffixes generated on the GPU, the gathered SA compared
+    with the single-GPU build (too large for the CPU oracle)."""
     import os
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -378,6 +380,36 @@ def _multi_rank_worker(rank, world, port, q):
     try:
         ops = HipRangeOps(0, 0)
         res = {}
+        if large:
+            from hpc_suffix_array_amd import DeviceBuilder
+            n = 3 * (1 << 27) + 17
+            t = torch.empty(n, dtype=torch.uint8, device="cuda")
+            ops.b.generate_text(t, n, b"ACGT", seed=5)
+            torch.cuda.synchronize()
+            say("build large")
+            d = DistributedSA(ops)
+            sa_local, sa_off = d.build(t, n)
+            say("built large", d.stats)
+            # each rank compares its slice with the same slice of the
+            # single-GPU build (a 3 GiB gather through gloo would take minutes)
+            b = DeviceBuilder(n, device=0)
+            want = torch.empty(n, dtype=torch.int32, device="cuda")
+            b.build(t, n, want)
+            torch.cuda.synchronize()
+            m = sa_local.numel()
+            mine = sa_local.to(torch.int64) & 0xFFFFFFFF
+            ref = want[int(sa_off): int(sa_off) + m].to(torch.int64) & 0xFFFFFFFF
+            ok = torch.tensor([1 if bool((mine == ref).all().item()) else 0, m], dtype=torch.int64)
+            b.close()
+            del want
+            dist.all_reduce(ok[:1], op=dist.ReduceOp.MIN)
+            tot = ok[1:].clone()
+            dist.all_reduce(tot)
+            say("checked large", ok.tolist(), tot.tolist())
+            if rank == 0:
+                res["dna_large"] = (bool(ok[0] == 1 and int(tot[0]) == n), d.stats["path"], len(d.stats["unsorted"]))
+                q.put(res)
+            return
         for name, kind, n, seed in (("dna", "dna", 3_000_017, 8), ("byte256", "byte256", 2_000_003, 2),
                                     ("alnum", "alnum", 1_048_576, 1), ("binary", "binary", 1_000_003, 4),
                                     ("periodic", None, 300_000, 11), ("degenerate", None, 70_001, 0)):
@@ -419,7 +451,16 @@ def test_distributed_hip_multi_rank(gpu, world):
     _multi_rank(world)
 
 
-def _multi_rank(world):
+@pytest.mark.slow
+def test_distributed_hip_multi_rank_large(gpu):
+    """Four ranks on one GPU at n = 3 * 2^27 + 17 DNA: ~100 M suffixes per
+    range, buckets large enough that each rank's local sort takes the fixed-
+    span 32-bit kernel (k_bucket_sort), checked against the single-GPU build."""
+    res = _multi_rank(4, large=True)
+    assert res["dna_large"][0] and res["dna_large"][1] == "range", res
+
+
+def _multi_rank(world, large=False):
     import socket
 
     import torch.multiprocessing as mp
@@ -428,7 +469,7 @@ def _multi_rank(world):
         port = s.getsockname()[1]
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_multi_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_multi_rank_worker, args=(r, world, port, q, large)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=240)
@@ -436,6 +477,8 @@ def _multi_rank(world):
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
+    if large:
+        return res
     for name, (ok, path, rounds) in res.items():
         assert ok, (name, world)
         assert path == ("sample-sort" if name == "degenerate" else "range"), (name, path)
