@@ -195,13 +195,33 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     const uint64_t tiles = (p1 - p0 + kTile - 1) / kTile;
     uint32_t kept_lane = 0;                        // LM = 1: this lane's kept positions
     uint32_t run = LM == 2 ? wg[blockIdx.x] : 0u;  // LM = 2: the workgroup's next record slot
+    // the next tile's 16 text bytes per lane (and the halo byte of lanes <
+    // kMaxK) are loaded while the current tile is counted: clamped to the
+    // last tile, unconditional (a conditional load is waited for at the join)
+    auto fetch = [&](uint64_t tt2, uint4& v, uint32_t& hv) {
+        const uint64_t tb2 = p0 + tt2 * kTile;
+        const uint64_t i2 = tb2 + (uint64_t)threadIdx.x * RUN;
+        v = (i2 + RUN <= n && (((uintptr_t)(text + i2)) & 15) == 0) ? *reinterpret_cast<const uint4*>(text + i2)
+                                                                     : make_uint4(0u, 0u, 0u, 0u);
+        const uint64_t h2 = tb2 + kTile + threadIdx.x;
+        hv = (threadIdx.x < (uint32_t)kMaxK && h2 < n) ? (uint32_t)text[h2] : 0u;
+    };
+    uint4 cv = make_uint4(0u, 0u, 0u, 0u);
+    uint32_t chv = 0;
+    if (blockIdx.x < tiles) fetch(blockIdx.x, cv, chv);
     for (uint64_t tt = blockIdx.x; tt < tiles; tt += gridDim.x) {
         const uint64_t tb = p0 + tt * kTile;
+        uint4 nv;
+        uint32_t nhv;
+        {
+            const uint64_t tn = tt + gridDim.x;
+            fetch(tn < tiles ? tn : tiles - 1, nv, nhv);
+        }
         {
             const uint64_t i = tb + (uint64_t)threadIdx.x * RUN;
             uint32_t w[4];
             if (i + RUN <= n && (((uintptr_t)(text + i)) & 15) == 0) {
-                const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+                const uint4 v = cv;
                 w[0] = v.x;
                 w[1] = v.y;
                 w[2] = v.z;
@@ -227,9 +247,11 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
             *reinterpret_cast<uint4*>(s_dc + threadIdx.x * RUN) = make_uint4(w[0], w[1], w[2], w[3]);
             if (threadIdx.x < (uint32_t)kMaxK) {
                 const uint64_t h = tb + kTile + threadIdx.x;
-                s_dc[kTile + threadIdx.x] = (h < n) ? s_map[text[h]] : (uint8_t)0;
+                s_dc[kTile + threadIdx.x] = (h < n) ? s_map[chv] : (uint8_t)0;
             }
         }
+        cv = nv;
+        chv = nhv;
         __syncthreads();
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
