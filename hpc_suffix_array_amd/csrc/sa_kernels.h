@@ -26,6 +26,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sa_search.h"
+
 namespace sa {
 
 constexpr int kWave = 64;
@@ -181,54 +183,6 @@ __device__ __forceinline__ uint64_t key1_words(const uint8_t* __restrict__ text,
     *D_out = (uint32_t)D;
     if (!FULL) return 0;
     return (D << b.rb) | bucket_low(b, r, n - j);
-}
-
-// Lower bound of x among the sorted key1 of SA positions [lo, hi) when the
-// first round kept only every 2^ksh-th of them (keys[t] = key1 at position
-// t << ksh, store_window in sa_bucket.h): a binary search of the samples
-// inside [lo, hi) narrows it to at most 2^ksh slots, searched by key1
-// rebuilt from the text at sa[p] (key_at).  ksh = 0: keys holds every key1.
-template <class KeyAt>
-__device__ __forceinline__ uint64_t lower_bound_sampled(const uint64_t* __restrict__ keys, uint32_t ksh,
-                                                        const uint32_t* __restrict__ sa, uint64_t lo, uint64_t hi,
-                                                        uint64_t x, const KeyAt& key_at) {
-    if (ksh == 0) {
-        uint64_t len = hi - lo;
-        while (len > 0) {
-            const uint64_t half = len >> 1;
-            if (keys[lo + half] < x) {
-                lo += half + 1;
-                len -= half + 1;
-            } else {
-                len = half;
-            }
-        }
-        return lo;
-    }
-    const uint64_t s0 = (lo + (1ull << ksh) - 1) >> ksh, s1 = (hi + (1ull << ksh) - 1) >> ksh;
-    uint64_t t = s0, len = s1 - s0;   // first sample in [s0, s1) with key >= x
-    while (len > 0) {
-        const uint64_t half = len >> 1;
-        if (keys[t + half] < x) {
-            t += half + 1;
-            len -= half + 1;
-        } else {
-            len = half;
-        }
-    }
-    uint64_t l = t > s0 ? ((t - 1) << ksh) + 1 : lo;   // sample t - 1 is < x
-    const uint64_t r = t < s1 ? (t << ksh) : hi;       // sample t is >= x
-    len = r - l;
-    while (len > 0) {
-        const uint64_t half = len >> 1;
-        if (key_at(sa[l + half]) < x) {
-            l += half + 1;
-            len -= half + 1;
-        } else {
-            len = half;
-        }
-    }
-    return l;
 }
 
 // Packed schedule, later rounds: only the suffixes whose group is not yet a

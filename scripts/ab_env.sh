@@ -13,6 +13,6 @@ for v in default "$@" default "$@"; do
 import json,sys
 d=json.loads([l for l in open(sys.argv[2]) if l.startswith('{')][0])
 k=d['kernels_ms_per_step']
-print(sys.argv[1], d['ms_per_step'], d['verified'], 'first', k['scatter_first'], 'second', k['scatter_keys'], 'local', k['local_sort'], 'hist', k['pack'])
+print(sys.argv[1], d['ms_per_step'], d['verified'], ' '.join(f'{a}={b}' for a, b in k.items() if b))
 PY
 done
