@@ -40,7 +40,8 @@ __global__ __launch_bounds__(B) void k_pass(const uint64_t* __restrict__ in, uin
     }
 }
 
-int main() {
+int main(int argc, char** argv) {
+    const bool skip_offsets = argc > 1;   // any argument: allocations only
     const uint64_t n = 1ull << 30;
     uint64_t* in;
     CK(hipMalloc(&in, n * 8));
@@ -52,7 +53,7 @@ int main() {
     CK(hipEventCreate(&b));
     // one allocation, the output at different offsets inside it: address
     // bits below the page (channel / bank interleave) vs the pages themselves
-    {
+    if (!skip_offsets) {
         uint64_t* big;
         CK(hipMalloc(&big, n * 8 + (64ull << 20)));
         for (uint64_t off : {0ull, 4096ull, 65536ull, 1ull << 21, 3ull << 21, 1ull << 25}) {
@@ -73,9 +74,13 @@ int main() {
         CK(hipFree(big));
     }
     std::vector<uint64_t*> keep;
-    for (int alloc = 0; alloc < 6; ++alloc) {
+    // allocations alternate between hipMalloc and hipExtMallocWithFlags(
+    // hipDeviceMallocContiguous) (physically contiguous pages)
+    for (int alloc = 0; alloc < 10; ++alloc) {
         uint64_t* out;
-        CK(hipMalloc(&out, n * 8));
+        const bool contig = alloc & 1;
+        if (contig) CK(hipExtMallocWithFlags((void**)&out, n * 8, hipDeviceMallocContiguous));
+        else CK(hipMalloc(&out, n * 8));
         keep.push_back(out);   // a new allocation every time (the old ones stay mapped)
         for (int local = 0; local < 2; ++local) {
             std::vector<float> ts;
@@ -89,7 +94,8 @@ int main() {
                 ts.push_back(ms);
             }
             std::sort(ts.begin(), ts.end());
-            std::printf("allocation %d %s: %.3f ms (%.0f GB/s)\n", alloc, local ? "local 64 MiB windows" : "spread over 8 GiB  ",
+            std::printf("allocation %d %s %s: %.3f ms (%.0f GB/s)\n", alloc, contig ? "contiguous" : "hipMalloc ",
+                        local ? "local 64 MiB windows" : "spread over 8 GiB  ",
                         ts[1], 16.0 * n / ts[1] / 1e6);
         }
         if (keep.size() >= 3) {   // bounded memory: free the oldest
