@@ -14,9 +14,10 @@ namespace sa {
 
 // Lower bound of x among the sorted key1 of SA positions [lo, hi) when the
 // first round kept only every 2^ksh-th of them (keys[t] = key1 at position
-// t << ksh, store_window in sa_bucket.h): a binary search of the samples
-// inside [lo, hi) narrows it to at most 2^ksh slots, searched by key1
-// rebuilt from the text at sa[p] (key_at).  ksh = 0: keys holds every key1.
+// t << ksh, store_window in sa_bucket.h): an interpolation-guided search of
+// the samples inside [lo, hi) narrows it to at most 2^ksh slots, searched by
+// key1 rebuilt from the text at sa[p] (key_at).  ksh = 0: keys holds every
+// key1.
 template <class KeyAt>
 SA_HD uint64_t lower_bound_sampled(const uint64_t* __restrict__ keys, uint32_t ksh,
                                                         const uint32_t* __restrict__ sa, uint64_t lo, uint64_t hi,
@@ -103,28 +104,10 @@ SA_HD uint64_t lower_bound_sampled(const uint64_t* __restrict__ keys, uint32_t k
     }
     uint64_t l = t > s0 ? ((t - 1) << ksh) + 1 : lo;   // sample t - 1 is < x
     const uint64_t r = t < s1 ? (t << ksh) : hi;       // sample t is >= x
-    // the last <= 2^ksh slots: 4-ary steps (three key rebuilds in flight per
-    // step, each an SA load and the text words of its suffix) while more
-    // than 4 remain, then binary
+    // the last <= 2^ksh slots by key1 rebuilt from the text, binary (4-ary
+    // steps, three rebuilds in flight per step, were slower: sort_u 0.53 ms
+    // with them, 0.43 without; profiles/r03_w_ab_search.txt)
     len = r - l;
-    while (len > 4) {
-        const uint64_t q = len >> 2;
-        const uint64_t p1 = l + q, p2 = l + 2 * q, p3 = l + 3 * q;
-        const uint32_t y1 = sa[p1], y2 = sa[p2], y3 = sa[p3];
-        const bool c1 = key_at(y1) < x, c2 = key_at(y2) < x, c3 = key_at(y3) < x;
-        if (c3) {
-            len -= p3 + 1 - l;
-            l = p3 + 1;
-        } else if (c2) {
-            len = p3 - (p2 + 1);
-            l = p2 + 1;
-        } else if (c1) {
-            len = p2 - (p1 + 1);
-            l = p1 + 1;
-        } else {
-            len = p1 - l;
-        }
-    }
     while (len > 0) {
         const uint64_t half = len >> 1;
         if (key_at(sa[l + half]) < x) {
