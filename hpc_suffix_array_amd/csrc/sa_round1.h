@@ -571,10 +571,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             // the member bitmap is complete: its popcount prefix gives each
             // member's slot in the compact rank map
             const uint64_t nwb = (n + 31) / 32;
-            const uint32_t pb = (uint32_t)((nwb + kWsBlock - 1) / kWsBlock);
+            const uint32_t pb = (uint32_t)((nwb + kPcBlock - 1) / kPcBlock);
             uint32_t* ppart = br_.prefix + nwb + 1;
             hipLaunchKernelGGL(k_popc_reduce, dim3(pb), dim3(kBlock), 0, s, (const uint32_t*)member, nwb, ppart);
-            hipLaunchKernelGGL(k_popc_top, dim3(1), dim3(kBlock), 0, s, ppart, pb);
+            hipLaunchKernelGGL(k_popc_top, dim3(1), dim3(kPcTop), 0, s, ppart, pb);
             hipLaunchKernelGGL(k_popc_apply, dim3(pb), dim3(kBlock), 0, s, (const uint32_t*)member, nwb,
                                (const uint32_t*)ppart, br_.prefix);
             rm = RankMap{member, br_.prefix};
