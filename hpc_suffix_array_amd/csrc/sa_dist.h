@@ -41,6 +41,12 @@
 // Groups never straddle ranks (a group is a set of equal K-prefixes, inside
 // one bucket), so every sort and re-rank is local; only rank look-ups cross.
 #pragma once
+// workgroups per CU of the coarse histogram (each flushes its 4096 bins
+// with device atomics)
+#ifndef SA_COARSE_WPC
+#define SA_COARSE_WPC 16
+#endif
+
 
 constexpr int kDistMaxWorld = 1024;
 
@@ -355,7 +361,7 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
         const uint64_t lo = n * (uint64_t)rank / world, hi = n * (uint64_t)(rank + 1) / world;
         if (hi > lo) {
             const uint64_t tiles = (hi - lo + kTile - 1) / kTile;
-            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, 16ull * (uint32_t)c->cus));
+            const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_COARSE_WPC * (uint32_t)c->cus));
             if ((sigma & (sigma - 1)) == 0)
                 hipLaunchKernelGGL((k_bucket_hist<true, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,
                                    (const uint16_t*)c->code, bp.bs, (uint32_t*)d_coarse, lo, hi, 0u, 1u << bp.bs.bb);
