@@ -42,9 +42,10 @@
 // one bucket), so every sort and re-rank is local; only rank look-ups cross.
 #pragma once
 // workgroups per CU of the coarse histogram (each flushes its 4096 bins
-// with device atomics)
+// with device atomics): over an eighth of 1 GiB DNA 2 / 4 / 16 per CU took
+// 109 / 82 / 115 us (profiles/r03_z_ab_coarse_grid.txt)
 #ifndef SA_COARSE_WPC
-#define SA_COARSE_WPC 16
+#define SA_COARSE_WPC 4
 #endif
 
 
