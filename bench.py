@@ -287,7 +287,19 @@ def run_single(a, torch, dev, world, rank, barrier):
                         "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_src,
                         "kernel": KERNEL_NAMES.get(dom, dom) + (" [bucketed round 1]" if bucketed else ""),
                         "kind": dom, "bytes_per_launch": int(per_launch), "avg_launch_ms": round(avg_s * 1e3, 4)}
+    # SURVEY.md 8(d)'s whole-build figure: the algorithmic bytes of every
+    # kernel of one build over the build's wall time (t_SA), beside the
+    # dominant kernel's roofline
+    build_bytes = sum(v["bytes"] for v in kern.values()) / a.steps
+    t_sa = elapsed / a.steps
+    build_roofline = None
+    if build_bytes and t_sa > 0:
+        ach_b = build_bytes / t_sa / 1e9
+        build_roofline = {"bound": "hbm", "achieved": round(ach_b, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                          "frac": round(ach_b / HBM_PEAK_GBS, 4), "bytes_per_build": int(build_bytes),
+                          "bytes_per_suffix": round(build_bytes / n, 2), "t_sa_ms": round(1e3 * t_sa, 3)}
     extra = {
+        "build_roofline": build_roofline,
         "ms_per_round": [round(x, 3) for x in round_ms],
         "rounds": rounds,
         "distinct_per_round": stats[-1]["distinct"],

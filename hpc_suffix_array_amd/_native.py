@@ -31,7 +31,7 @@ SA_K_COUNT = len(KERNEL_KINDS)
 # every symbol include/*.h declares
 DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_array",
                   "build_lcp_array", "find_longest_repeated_substring", "is_valid_suffix_array"]
-EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_workspace_bytes", "sa_build_device",
+EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_context_set_debug", "sa_workspace_bytes", "sa_build_device",
                "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
                "sa_gather_u64_device", "sa_running_max_i64_device",
@@ -44,9 +44,25 @@ class SAError(RuntimeError):
     """A libsa_hip entry point returned an error code."""
 
 
+# sa_opts.debug flags (include/sa_hip.h SA_DEBUG_*): alternative paths the
+# tests force; every combination gives the same suffix array
+DEBUG_FLAGS = {"no_cmp": 0x1, "no_pk8": 0x2, "no_pad": 0x4, "pad_overflow": 0x8, "no_fast32": 0x10,
+               "no_pivot": 0x20, "perm_always": 0x40}
+
+
+def debug_bits(names) -> int:
+    bits = 0
+    for x in names or ():
+        if x not in DEBUG_FLAGS:
+            raise ValueError(f"unknown debug flag {x!r} (one of {sorted(DEBUG_FLAGS)})")
+        bits |= DEBUG_FLAGS[x]
+    return bits
+
+
 class SaOpts(ctypes.Structure):
     _fields_ = [("profile", ctypes.c_int32), ("schedule", ctypes.c_int32), ("init_chars", ctypes.c_int32),
-                ("radix", ctypes.c_int32), ("round1", ctypes.c_int32), ("reserved", ctypes.c_int32 * 3)]
+                ("radix", ctypes.c_int32), ("round1", ctypes.c_int32), ("debug", ctypes.c_uint32),
+                ("span_extra", ctypes.c_int32), ("tune", ctypes.c_int32)]
 
 
 class SaStats(ctypes.Structure):
@@ -158,6 +174,8 @@ def lib() -> ctypes.CDLL:
     L.sa_context_create.restype = i32
     L.sa_context_destroy.argtypes = [vp]
     L.sa_context_destroy.restype = None
+    L.sa_context_set_debug.argtypes = [vp, ctypes.POINTER(SaOpts)]
+    L.sa_context_set_debug.restype = i32
     L.sa_workspace_bytes.argtypes = [u64]
     L.sa_workspace_bytes.restype = u64
     L.sa_build_device.argtypes = [vp, vp, u64, vp, vp, ctypes.POINTER(SaOpts), ctypes.POINTER(SaStats)]

@@ -36,19 +36,26 @@ ROUND1 = {"auto": N.ROUND1_AUTO, "lsd": N.ROUND1_LSD, "bucketed": N.ROUND1_BUCKE
 
 
 def _opts(profile: bool = False, schedule: str = "packed", init_chars: int = 0,
-          radix: str = "onesweep", round1: str = "auto") -> N.SaOpts:
+          radix: str = "onesweep", round1: str = "auto", debug=(), span_extra: int = 0,
+          tune: int = 0) -> N.SaOpts:
+    """sa_opts; ``debug``: names of N.DEBUG_FLAGS (alternative paths the
+    tests force), ``span_extra`` / ``tune``: the debug / A/B fields of
+    include/sa_hip.h."""
     o = N.SaOpts()
     o.profile = 1 if profile else 0
     o.schedule = SCHEDULES[schedule]
     o.init_chars = int(init_chars)
     o.radix = RADIX[radix]
     o.round1 = ROUND1[round1]
+    o.debug = N.debug_bits(debug)
+    o.span_extra = int(span_extra)
+    o.tune = int(tune)
     return o
 
 
 def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats: bool = False,
                        schedule: str = "packed", init_chars: int = 0, radix: str = "onesweep",
-                       round1: str = "auto"):
+                       round1: str = "auto", debug=(), span_extra: int = 0, tune: int = 0):
     """Suffix array of ``text`` (bytes / uint8 array), built on the GPU.
 
     Unsigned-byte order, end of string smallest (== the reference's order on
@@ -58,7 +65,8 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     re-sort unsorted groups only) or "reference" (h = 1, 2, 4, ... over all
     n suffixes, round for round as manber_myers.c:94-125).  ``round1``
     (packed): "auto", "lsd" (full radix sort of the packed first key) or
-    "bucketed" (two bucket passes + per-window LDS sort)."""
+    "bucketed" (two bucket passes + per-window LDS sort).  ``debug`` /
+    ``span_extra`` / ``tune``: forced alternative paths (tests, A/B runs)."""
     t = _as_bytes_array(text)
     n = int(t.size)
     N.require_device()
@@ -66,7 +74,8 @@ def build_suffix_array(text, width: int = 4, profile: bool = False, return_stats
     st = N.SaStats()
     L = N.lib()
     N.check(L.sa_build_ex(t.ctypes.data if n else None, n, out.ctypes.data, width,
-                          ctypes.byref(_opts(profile, schedule, init_chars, radix, round1)), ctypes.byref(st)),
+                          ctypes.byref(_opts(profile, schedule, init_chars, radix, round1, debug, span_extra, tune)),
+                          ctypes.byref(st)),
             "sa_build_ex")
     out = out[:n]
     return (out, st.to_dict()) if return_stats else out
@@ -198,15 +207,23 @@ class DeviceBuilder:
         return x if isinstance(x, int) else int(x.data_ptr())
 
     def build(self, d_text, n: int, d_sa, stream=None, profile: bool = False, schedule: str = "packed",
-              init_chars: int = 0, radix: str = "onesweep", round1: str = "auto") -> dict:
+              init_chars: int = 0, radix: str = "onesweep", round1: str = "auto", debug=(), span_extra: int = 0,
+              tune: int = 0) -> dict:
         """Build the SA of the n bytes at d_text into the n uint32 at d_sa."""
         st = N.SaStats()
         s = None if stream is None else ctypes.c_void_p(int(stream))
         N.check(self.L.sa_build_device(self.ctx, self._ptr(d_text), n, self._ptr(d_sa), s,
-                                       ctypes.byref(_opts(profile, schedule, init_chars, radix, round1)),
+                                       ctypes.byref(_opts(profile, schedule, init_chars, radix, round1, debug,
+                                                          span_extra, tune)),
                                        ctypes.byref(st)),
                 "sa_build_device")
         return st.to_dict()
+
+    def set_debug(self, debug=(), span_extra: int = 0, tune: int = 0) -> None:
+        """Debug / tune fields for the context's sa_dist_* phases (they take
+        no sa_opts; sa_build_device applies its own)."""
+        N.check(self.L.sa_context_set_debug(self.ctx, ctypes.byref(_opts(debug=debug, span_extra=span_extra,
+                                                                          tune=tune))), "sa_context_set_debug")
 
     def generate_text(self, d_out, n: int, alphabet: bytes, seed: int = 1, stream=None) -> None:
         """Fill n device bytes with the seeded splitmix64 text."""

@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdarg>
 #include <cstdio>
@@ -143,6 +144,11 @@ struct sa_context {
     hipEvent_t ev[sa::kEvPool];
     int ev_ready = 0;
     sa::DistState* dist = nullptr;   // range-partitioned build state (sa_dist.h)
+    // sa_opts debug / tune fields of the current build (sa_build_device's
+    // opts, or sa_context_set_debug for the sa_dist_* phases)
+    uint32_t dbg = 0;
+    int32_t span_extra = 0;
+    int32_t tune = 0;
 };
 
 namespace sa {
@@ -199,6 +205,13 @@ static void free_u_buffers(sa_context* c) {
         c->u_pos[i] = c->u_idx[i] = c->u_g[i] = nullptr;
     }
     c->ucap = 0;
+}
+
+// sa_opts debug / tune fields -> the context (NULL: production defaults)
+static void set_debug(sa_context* c, const sa_opts* o) {
+    c->dbg = o ? o->debug : 0u;
+    c->span_extra = o ? o->span_extra : 0;
+    c->tune = o ? o->tune : 0;
 }
 
 static int ensure_capacity(sa_context* c, uint64_t n) {
@@ -462,12 +475,9 @@ static void record_round(sa_stats* st, float ms, uint64_t D, uint32_t P, uint64_
 // ---------------------------------------------------------------------------
 // the re-rank as a permutation (sa_permute.h) from this many suffixes; below
 // it rank[] stays inside the L2s and one random scatter (k_rerank) is cheaper
-// (SA_PERM_MIN overrides it, e.g. for tests at small n)
+// (SA_DEBUG_PERM_ALWAYS: from any n, for tests at small n)
 constexpr int kPermErrWord = 13;
-static uint64_t perm_min_n() {
-    const char* e = std::getenv("SA_PERM_MIN");
-    return e ? std::strtoull(e, nullptr, 0) : (1ull << 22);
-}
+static uint64_t perm_min_n(const sa_context* c) { return (c->dbg & SA_DEBUG_PERM_ALWAYS) ? 1ull : (1ull << 22); }
 
 static PermPlan plan_perm(uint64_t n) {
     PermPlan p;
@@ -528,18 +538,17 @@ static uint32_t* lsd_ghist(sa_context* c) { return c->lsd; }
 static uint32_t* lsd_base(sa_context* c) { return c->lsd + kMaxPasses * kLsdMaxRadix; }
 static uint32_t* lsd_tickets(sa_context* c) { return c->lsd + 2 * kMaxPasses * kLsdMaxRadix; }
 
-// widest digit of the plan (SA_LSD_MAXBITS=8 restores 8-bit digits, A/B)
-static uint32_t lsd_max_bits() {
-    const char* e = std::getenv("SA_LSD_MAXBITS");
-    const uint32_t b = e ? (uint32_t)std::atoi(e) : 10u;
-    return std::min<uint32_t>(10, std::max<uint32_t>(8, b));
+// widest digit of the plan (sa_opts.tune bits 0-7 = 8 restores 8-bit
+// digits, A/B)
+static uint32_t lsd_max_bits(const sa_context* c) {
+    const uint32_t b = (uint32_t)c->tune & 0xFFu;
+    return b ? std::min<uint32_t>(10, std::max<uint32_t>(8, b)) : 10u;
 }
 
 // B key bits above bit `base`: the pass count and widths of least relative
 // cost, a pass of 9 / 10 bits costing ~1.2 / 1.45 of an 8-bit one (longer
 // match-any, shorter digit runs per tile)
-static LsdPlan lsd_plan(uint32_t B, uint32_t base) {
-    const uint32_t maxb = lsd_max_bits();
+static LsdPlan lsd_plan(uint32_t B, uint32_t base, uint32_t maxb) {
     auto cost = [](uint32_t w) { return w <= 8 ? 1.0 : w == 9 ? 1.2 : 1.45; };
     LsdPlan pl{};
     double best = 1e30;
@@ -560,11 +569,14 @@ static LsdPlan lsd_plan(uint32_t B, uint32_t base) {
     return pl;
 }
 
+// resident workgroups per CU of a persistent kernel (a property of the code
+// object, the same on every gfx950 device; the grid is this times the
+// launching context's CU count)
 template <class K>
-static int persist_grid(sa_context* c, K kernel, int block) {
+static int blocks_per_cu(K kernel, int block) {
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, block, 0) != hipSuccess || nb < 1) nb = 1;
-    return c->cus * nb;
+    return nb;
 }
 
 template <class Src, bool PACKED>
@@ -581,9 +593,10 @@ static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, 
         constexpr int B = lsd_block<PACKED, RB>();                                                          \
         constexpr uint64_t T = (uint64_t)B * lsd_items<PACKED, RB>();                                       \
         tiles = (n + T - 1) / T;                                                                            \
-        static int grid = 0;                                                                                \
-        if (!grid) grid = persist_grid(c, kern, B);                                                         \
-        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, (uint64_t)grid)), dim3(B), 0, s,  \
+        static std::atomic<int> per_cu{0};                                                                  \
+        if (!per_cu.load(std::memory_order_relaxed)) per_cu.store(blocks_per_cu(kern, B));                  \
+        const uint64_t grid = (uint64_t)c->cus * (uint64_t)per_cu.load(std::memory_order_relaxed);          \
+        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, grid)), dim3(B), 0, s,             \
                            src, n, shift, nbits, base, c->states, ticket, epoch, ok, ov, c->words + 4, prof,   \
                            nshift, nnbits, next_hist);                                                     \
     } while (0)
@@ -693,7 +706,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     if (st) st->sigma = (int32_t)sigma;
 
     uint64_t D = sigma;   // ranks 1..sigma (manber_myers.c:94 sizes its bins for 256)
-    const uint64_t perm_min = perm_min_n();
+    const uint64_t perm_min = perm_min_n(c);
     const uint32_t ib = std::max<uint32_t>(1, bit_width(n - 1));   // index bits of a packed item
     bool used_perm = false;
     for (uint64_t h = 1;; h *= 2) {
@@ -707,7 +720,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         uint64_t* sorted;
         uint32_t P;
         if (c->radix == 0) {
-            const LsdPlan pl = lsd_plan(2 * w, packed ? ib : 0);
+            const LsdPlan pl = lsd_plan(2 * w, packed ? ib : 0, lsd_max_bits(c));
             P = pl.P;
             rc = packed ? lsd_sort<true>(c, SrcRankPk{c->rank, n, h, w, ib}, n, pl, d_sa, c->vals_alt, s, tm, st,
                                          &sorted)
@@ -736,9 +749,13 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         SA_HIP(hipGetLastError());
         add_bytes(st, SA_K_HEADS, 8 * n);
         add_bytes(st, SA_K_HEADS_SCAN, 8ull * ch.chunks);
-        SA_HIP(hipMemcpyAsync(c->host_words, c->words, 20, hipMemcpyDeviceToHost, s));
+        // (with the permutation re-rank's error word: the previous round's
+        // placement is checked before this round's ranks are used)
+        SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4 * (kPermErrWord + 1), hipMemcpyDeviceToHost, s));
         SA_HIP(hipStreamSynchronize(s));
         if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
+        if (used_perm && c->host_words[kPermErrWord])
+            return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix (flags %u)", c->host_words[kPermErrWord]);
         const uint64_t Dn = c->host_words[0];
         const bool done = (Dn == n);                  // manber_myers.c:113
         if (done && packed) {
@@ -776,7 +793,8 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     if (used_perm) {
         SA_HIP(hipMemcpyAsync(c->host_words + kPermErrWord, c->words + kPermErrWord, 4, hipMemcpyDeviceToHost, s));
         SA_HIP(hipStreamSynchronize(s));
-        if (c->host_words[kPermErrWord]) return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix");
+        if (c->host_words[kPermErrWord])
+            return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix (flags %u)", c->host_words[kPermErrWord]);
     }
     return SA_OK;
 }
@@ -883,8 +901,8 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
 // Unsorted-set round by a three-way pivot split (sa_pivot.h): dense ranks,
 // large groups on average.  Returns SA_OK with *sorted = nullptr when the
 // tied blocks turn out small (the caller then sorts the whole set).
-static bool pivot_ok(uint64_t m, uint64_t G, uint32_t wr, bool sparse, int radix) {
-    return std::getenv("SA_NO_PIVOT") == nullptr && radix == 0 && !sparse && m >= (1u << 16) && G >= 1 && G <= m / 4 && bit_width(2 * G + 1) + wr <= 64;
+static bool pivot_ok(const sa_context* c, uint64_t m, uint64_t G, uint32_t wr, bool sparse) {
+    return !(c->dbg & SA_DEBUG_NO_PIVOT) && c->radix == 0 && !sparse && m >= (1u << 16) && G >= 1 && G <= m / 4 && bit_width(2 * G + 1) + wr <= 64;
 }
 
 static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, uint64_t G, uint64_t h, uint32_t wr,
@@ -991,7 +1009,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // LSD sort of the packed key
     BucketPlan bp;
     const int r1 = opts ? opts->round1 : SA_ROUND1_AUTO;
-    bool bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, !std::getenv("SA_NO_CMP"));
+    bool bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, !(c->dbg & SA_DEBUG_NO_CMP));
     if (bucketed && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
         bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, false);
     bool fused = false;
@@ -1109,7 +1127,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             SA_TRACE("  round h=%llu: per-group register sort %s", (unsigned long long)h,
                      sorted ? "done" : "found a large group");
         }
-        if (!sorted && pivot_ok(m, G, wr, sparse, c->radix)) {
+        if (!sorted && pivot_ok(c, m, G, wr, sparse)) {
             uint64_t* kbA = ukb0 == c->keys[0] ? c->keys[1] : c->keys[0];   // the round-1 keys: dead with dense ranks
             rc = pivot_round(c, ui, uo, n, m, G, h, wr, ukb0, ukb1, kbA, cu, s, tm, st, &sorted, &P);
             if (rc) return rc;
@@ -1183,6 +1201,7 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     if (rc) return rc;
     Timer tm{c, s, opts && opts->profile, st};
     c->radix = opts ? opts->radix : 0;
+    set_debug(c, opts);
     if (c->radix != 0 && c->radix != 1) return set_err(SA_E_INVALID, "unknown radix algorithm %d", c->radix);
     SA_HIP(hipMemsetAsync(c->words, 0, 64, s));
     Events ev;
@@ -1563,6 +1582,12 @@ void sa_context_destroy(sa_context* c) {
     if (c->host_words) hipHostFree(c->host_words);
     for (int i = 0; i < c->ev_ready; ++i) hipEventDestroy(c->ev[i]);
     delete c;
+}
+
+int sa_context_set_debug(sa_context* ctx, const sa_opts* opts) {
+    if (!ctx) return set_err(SA_E_INVALID, "NULL context");
+    set_debug(ctx, opts);
+    return SA_OK;
 }
 
 int sa_build_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, void* stream,

@@ -343,7 +343,7 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     info->sigma = (int32_t)sigma;
     BucketPlan bp;
     c->radix = 0;
-    bool planned = plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world, !std::getenv("SA_NO_CMP"));
+    bool planned = plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world, !(c->dbg & SA_DEBUG_NO_CMP));
     if (planned && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
         planned = plan_bucketed(sigma, n, K, SA_ROUND1_BUCKETED, 0, &bp, world, false);
     if (!planned) {

@@ -247,7 +247,9 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
 }
 
 // Level 3: one workgroup per 2^kPermSub sub-bin; a pair whose idx lies
-// outside the sub-bin (a broken partition) raises err[0] and is dropped.
+// outside the sub-bin (a broken partition) raises err bit 1 and is dropped.
+// Dense ranks are >= 1, so the sub-bin's LDS copy starts at 0 and a slot
+// still 0 at the write (a missing or duplicated idx) raises err bit 2.
 template <int BLOCK>
 __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict__ in, uint64_t n,
                                                        uint32_t* __restrict__ rank, uint32_t* __restrict__ err) {
@@ -256,6 +258,8 @@ __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict
     const uint64_t base = (uint64_t)blockIdx.x << kPermSub;
     const uint32_t valid = (uint32_t)((n - base) < (uint64_t)S ? (n - base) : (uint64_t)S);
     bool bad = false;
+    for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) s_r[q] = 0u;
+    __syncthreads();
     for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) {
         const uint64_t p = in[base + q];
         const uint32_t x = (uint32_t)(p >> 32);
@@ -267,6 +271,7 @@ __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict
     }
     if (bad) atomicOr(err, 2u);
     __syncthreads();
+    bool hole = false;
     for (uint32_t q = threadIdx.x * 4; q < valid; q += BLOCK * 4) {
         if (q + 4 <= valid) {
             uint4 v;
@@ -274,11 +279,16 @@ __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict
             v.y = s_r[q + 1];
             v.z = s_r[q + 2];
             v.w = s_r[q + 3];
+            hole |= (v.x == 0u) | (v.y == 0u) | (v.z == 0u) | (v.w == 0u);
             *reinterpret_cast<uint4*>(rank + base + q) = v;
         } else {
-            for (uint32_t i = q; i < valid; ++i) rank[base + i] = s_r[i];
+            for (uint32_t i = q; i < valid; ++i) {
+                hole |= s_r[i] == 0u;
+                rank[base + i] = s_r[i];
+            }
         }
     }
+    if (hole) atomicOr(err, 4u);
 }
 
 }  // namespace sa

@@ -51,11 +51,11 @@ constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
 // bucketed round's one-GPU maximum; their starts live in the onesweep base
 // scratch after the second pass's 2^hb (<= 1024) digit bases
 constexpr uint64_t kPadMinN = 1ull << 26;
-// first-pass cursor stripes with padded segments (SA_TEXT_STRIPES overrides:
-// 1 = one cursor per digit shared by every tile, ticketed tiles)
-static uint32_t text_stripes() {
-    const char* e = std::getenv("SA_TEXT_STRIPES");
-    const uint32_t v = e ? (uint32_t)std::atoi(e) : 8u;
+// first-pass cursor stripes with padded segments (sa_opts.tune bits 8-15
+// override: 1 = one cursor per digit shared by every tile, ticketed tiles)
+static uint32_t text_stripes(const sa_context* c) {
+    const uint32_t e = ((uint32_t)c->tune >> 8) & 0xFFu;
+    const uint32_t v = e ? e : 8u;
     return v >= 8 ? 8u : v >= 4 ? 4u : v >= 2 ? 2u : 1u;
 }
 
@@ -172,9 +172,9 @@ static bool short_suffix_ties(const uint8_t* tail, uint64_t n, uint32_t t, const
 // (k_split_text / k_split_list <.., PK8>, SrcPk8): a power-of-two alphabet,
 // and the second pass's digit (of the local bucket), key1 below its bucket and
 // the index fitting 64 bits
-static bool plan_pk8(const BucketPlan& bp, uint32_t hb) {
+static bool plan_pk8(const BucketPlan& bp, uint32_t hb, uint32_t dbg) {
     const uint32_t sg = bp.bs.sigma;
-    if (sg < 2 || (sg & (sg - 1)) != 0 || std::getenv("SA_NO_PK8")) return false;
+    if (sg < 2 || (sg & (sg - 1)) != 0 || (dbg & SA_DEBUG_NO_PK8)) return false;
     const uint32_t lg = (uint32_t)__builtin_ctz(sg);
     if (lg * bp.bs.s < bp.bs.bb) return false;
     return hb + (lg * bp.bs.s - bp.bs.bb) + bp.bs.rb + bp.ib <= 64;
@@ -249,7 +249,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // one GPU, the whole bucket range: padded first-pass segments sized from a
     // sample instead of the exact totals (k_bucket_sample, sa_bucket.h)
     const bool padded = allow_pad && !listed && blo == 0 && bhi == (1u << bp.bs.bb) && n >= kPadMinN &&
-                        n <= kPadMaxN && c->cap_pad >= pad_capacity(n) && !std::getenv("SA_NO_PAD");
+                        n <= kPadMaxN && c->cap_pad >= pad_capacity(n) && !(c->dbg & SA_DEBUG_NO_PAD);
     const uint32_t ssh = std::max<uint32_t>(6u, bit_width(n) > 21 ? bit_width(n) - 21 : 0u);
     uint32_t* const pstart = os_base(c) + kPadStartOff;   // kLoRadix + 1 padded segment starts
     uint32_t* const dlo = os_base(c) + kPadDenseOff;      // kLoRadix dense segment starts
@@ -265,10 +265,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         else
             hipLaunchKernelGGL(k_bucket_sample<false>, dim3(g), dim3(kBlock), 0, s, d_text, n,
                                (const uint16_t*)c->code, bp.bs, ssh, os_ghist(c));
-        // SA_PAD_TEST_OVERFLOW (tests): segments of exactly the sampled
+        // SA_DEBUG_PAD_OVERFLOW (tests): segments of exactly the sampled
         // estimate, so the first pass overflows and the round re-runs exactly
         hipLaunchKernelGGL(k_pad_starts, dim3(1), dim3(kLoRadix), 0, s, (const uint32_t*)os_ghist(c), ssh,
-                           std::getenv("SA_PAD_TEST_OVERFLOW") ? 1u : 0u, (uint32_t)c->cap_pad, pstart);
+                           (c->dbg & SA_DEBUG_PAD_OVERFLOW) ? 1u : 0u, (uint32_t)c->cap_pad, pstart);
     } else {
         const uint64_t tiles = (n + kTile - 1) / kTile;
         const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus));
@@ -295,7 +295,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
     const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
-    const bool pk8 = plan_pk8(bp, hb);
+    const bool pk8 = plan_pk8(bp, hb, c->dbg);
     if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0);
     // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
     // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
@@ -305,7 +305,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // padded segments: the first pass's cursors striped over `stripes`
     // sub-segments (k_split_text; rows [s][digit] in the chunk histograms,
     // free in the bucketed round), the row sums after them
-    const uint32_t stripes = padded ? text_stripes() : 1u;
+    const uint32_t stripes = padded ? text_stripes(c) : 1u;
     uint32_t* const cursor = stripes > 1 ? c->hist : os_ghist(c) + 5 * kRadix;
     uint32_t* const cursor_sum = stripes > 1 ? c->hist + kMaxStripes * kLoRadix : cursor;
     if (stripes > 1) SA_HIP(hipMemsetAsync(cursor, 0, (size_t)stripes * kLoRadix * 4, s));
@@ -473,8 +473,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         br.bits1 = bit_width(per - 1) + bp.bs.rb;
         // tests: a span wider than the keys' (they cluster in the low
         // sub-buckets), so every window takes the measured-span recount
-        if (const char* e = std::getenv("SA_TEST_SPAN_EXTRA"))
-            br.bits1 = std::min<uint32_t>(br.bits1 + (uint32_t)std::atoi(e), 64u - bp.ib);
+        if (c->span_extra > 0) br.bits1 = std::min<uint32_t>(br.bits1 + (uint32_t)c->span_extra, 64u - bp.ib);
     }
     SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
     uint32_t* const rank_arr = br_.rank ? br_.rank : c->rank;
@@ -496,7 +495,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // window strides; a rank's range holds m suffixes in bhi - blo buckets --
     // m >> bb undercounted them by G, and ranges took k_bucket_sort_wide)
     const bool fast32 = br.bits1 > (uint32_t)kSubBits && br.bits1 - kSubBits <= kLowMax &&
-                        m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !std::getenv("SA_NO_FAST32");
+                        m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !(c->dbg & SA_DEBUG_NO_FAST32);
     // one-bucket window headers after the retry list (16-byte aligned; 11 nw + 8 <= capacity)
     uint4* const hdr = reinterpret_cast<uint4*>(((uintptr_t)(retry + nw + 4) + 15) & ~(uintptr_t)15);
     auto local_sort = [&](const SegOut& o) {

@@ -794,7 +794,13 @@ constexpr uint64_t kBstartOff = segw_words(1024);
 constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 
 // (BLOCK 512 x 10 items, two workgroups per CU, measured slower: 7.2 -> 9.1 ms;
-// again with PK8 items, 512 x 12 (SA_SEG_BLOCK=512): 4.64 -> 6.27 ms)
+// again with PK8 items, 512 x 12 (SA_SEG_BLOCK=512): 4.64 -> 6.27 ms.
+// Whole packed items staged (digit from their top bits, no s_dig) with the
+// next unit's loads issued after the staging into the same registers, so
+// that 14 or 16 items per lane fit: 12 / 14 / 16 items 5.07 / 5.20 / 6.4 ms
+// against 4.68 for this kernel, profiles/r04_b_ab_seg_late.txt -- the loads
+// must be in flight through the base wait and the staging, and larger units
+// do not make the 512-way writes faster.)
 template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint64_t n, uint32_t shift,
                                                         const uint32_t* __restrict__ lo_base,
@@ -810,6 +816,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     constexpr int WTILE = kWave * ITEMS;
     constexpr int TILE = BLOCK * ITEMS;
     static_assert(BLOCK >= RADIX && (int)kSegs <= BLOCK, "one thread per digit / segment");
+    static_assert((int)(kSegs * kMaxStripes) <= 2 * BLOCK, "two sub-segments per thread in the unit numbering");
     static_assert(TILE <= 65535, "16-bit tile offsets");
     __shared__ uint64_t s_keys[TILE];   // bucket-relative items, digit-sorted
     __shared__ uint16_t s_dig[TILE];

@@ -282,14 +282,16 @@ class DistributedSA:
         return out
 
     def _phase(self, name: str, dev, fn, *args):
-        """Run one native phase and agree on its outcome: a libsa_hip error on
-        one rank (NOMEM, a request outside the range, ...) makes EVERY rank
-        raise here, instead of leaving the others blocked in the next
-        collective until its timeout (one all_reduce MAX per phase, G > 1)."""
+        """Run one native phase and agree on its outcome: an error on one rank
+        (a libsa_hip SAError -- NOMEM, a request outside the range --, a
+        torch OOM, a binding error, ...) makes EVERY rank raise here, instead
+        of leaving the others blocked in the next collective until its
+        timeout (one all_reduce MAX per phase, G > 1); the failing rank
+        re-raises its own exception."""
         err, res = None, None
         try:
             res = fn(*args)
-        except N.SAError as e:
+        except Exception as e:   # noqa: BLE001 -- agreed on, then re-raised
             err = e
         if self.G > 1:
             t = torch.tensor([1 if err is not None else 0], dtype=I64, device=dev)
@@ -340,7 +342,7 @@ class DistributedSA:
         self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
         if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
             return self._fallback(text, n, "unbalanced bucket ranges")
-        sa_local = self.ops.empty(info["m"], I32)
+        sa_local = self._phase("sa_local", dev, self.ops.empty, info["m"], I32)
         self._mark("round1", dev)
         info = self._phase("round1", dev, self.ops.round1, sa_local)
         _trace("round1", info)

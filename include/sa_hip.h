@@ -68,6 +68,17 @@ enum sa_kernel_kind {
                                     94-125): h = 1, 2, 4, ...; D_0 = 256; every
                                     round sorts all n (rank[i], rank[i+h]) pairs */
 
+/* sa_opts.debug: alternative code paths the tests and A/B runs force (0 in
+ * production; the library reads no environment variable that changes a
+ * build).  Every combination gives the same suffix array. */
+#define SA_DEBUG_NO_CMP 0x1u            /* bucketed round 1: original key1 low, not the compact one */
+#define SA_DEBUG_NO_PK8 0x2u            /* bucketed round 1: key1 + position, not packed 8-byte items */
+#define SA_DEBUG_NO_PAD 0x4u            /* bucketed round 1: exact digit totals, not sampled padded segments */
+#define SA_DEBUG_PAD_OVERFLOW 0x8u      /* padded segments with no slack: the round overflows and re-runs exactly */
+#define SA_DEBUG_NO_FAST32 0x10u        /* local sort: measured-span kernel, not the fixed-span 32-bit one */
+#define SA_DEBUG_NO_PIVOT 0x20u         /* later rounds: full sorts, never the three-way pivot split */
+#define SA_DEBUG_PERM_ALWAYS 0x40u      /* reference schedule: permutation re-rank at every n */
+
 typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
     int32_t schedule;       /* SA_SCHEDULE_* */
@@ -75,7 +86,12 @@ typedef struct {
     int32_t radix;          /* 0: single-pass radix (decoupled look-back, default);
                                1: reduce-then-scan radix (3 kernels per pass) */
     int32_t round1;         /* SA_ROUND1_* (packed schedule, onesweep radix) */
-    int32_t reserved[3];
+    uint32_t debug;         /* SA_DEBUG_* flags (0 = production paths) */
+    int32_t span_extra;     /* debug: bits added to the local sort's fixed key span
+                               (its windows all take the measured-span retry) */
+    int32_t tune;           /* A/B shapes, 0 = defaults: bits 0-7 the reference
+                               schedule's widest LSD digit (8..10), bits 8-15 the
+                               first bucket pass's cursor stripes (1, 2, 4, 8) */
 } sa_opts;
 
 typedef struct {
@@ -108,6 +124,10 @@ typedef struct sa_context sa_context;
 
 /* Device workspace for texts of up to max_n symbols on `device`. */
 int sa_context_create(int device, uint64_t max_n, sa_context** out);
+/* The debug / tune fields of opts (NULL: defaults) for the calls on ctx that
+ * take no sa_opts -- the range-partitioned build's sa_dist_* phases;
+ * sa_build_device applies its own opts. */
+int sa_context_set_debug(sa_context* ctx, const sa_opts* opts);
 void sa_context_destroy(sa_context* ctx);
 /* bytes of device memory a context for max_n needs */
 uint64_t sa_workspace_bytes(uint64_t max_n);

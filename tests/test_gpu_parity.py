@@ -72,21 +72,20 @@ def test_random_vs_oracle(gpu, oracle, kind, n, schedule):
 
 
 @pytest.mark.parametrize("kind", ["dna", "alnum", "byte256", "binary"])
-def test_reference_rerank_permutation(gpu, oracle, kind, monkeypatch):
+def test_reference_rerank_permutation(gpu, oracle, kind):
     """The reference schedule's re-rank as a partition by index
     (sa_permute.h) forced at every size: one level (n <= 2^22), two levels
     with 2 / 4 sub-bins, ragged last bins and sub-bins; D_j stay the
     reference's round for round."""
     from hpc_suffix_array_amd import build_suffix_array
-    monkeypatch.setenv("SA_PERM_MIN", "1")
     for n in (2, 3, 4095, 16385, 100_003, (1 << 22) + 1, 3 * (1 << 21) + 7):
         t = oracle.gen_text(kind, n, seed=n + 3)
-        got, st = build_suffix_array(t, return_stats=True, schedule="reference")
+        got, st = build_suffix_array(t, return_stats=True, schedule="reference", debug=("perm_always",))
         ref, rounds, _, dj = oracle.sa_c(t, stats=True)
         assert (got == ref).all(), (kind, n)
         assert st["rounds"] == rounds and st["distinct"] == dj, (kind, n)
     t = np.full(70_001, ord("a"), np.uint8)
-    got = build_suffix_array(t, schedule="reference")
+    got = build_suffix_array(t, schedule="reference", debug=("perm_always",))
     assert (got == np.arange(70_000, -1, -1, dtype=np.uint32)).all()
 
 
@@ -150,16 +149,15 @@ def test_degenerate(gpu, n, schedule):
 
 
 @pytest.mark.parametrize("pivot", [True, False])
-def test_pivot_split_rounds(gpu, oracle, pivot, monkeypatch):
+def test_pivot_split_rounds(gpu, oracle, pivot):
     """Unsorted-set rounds with large groups by the three-way pivot split
     (sa_pivot.h): periodic texts with sparse noise (a dominant key per group,
     plus members below and above the pivot), runs of one symbol inside random
     text, and a short first key on random DNA (many distinct keys per group:
-    the split gives up and the full sort runs); SA_NO_PIVOT forces the full
-    LSD sort for comparison."""
+    the split gives up and the full sort runs); debug "no_pivot"
+    (SA_DEBUG_NO_PIVOT) forces the full LSD sort for comparison."""
     from hpc_suffix_array_amd import build_suffix_array
-    if not pivot:
-        monkeypatch.setenv("SA_NO_PIVOT", "1")
+    dbg = () if pivot else ("no_pivot",)
     rng = np.random.default_rng(7)
     cases = []
     for period, noise, n in ((b"ab", 0.002, 400_003), (b"abc", 0.01, 300_001), (b"aab", 0.0005, 1 << 20)):
@@ -171,11 +169,11 @@ def test_pivot_split_rounds(gpu, oracle, pivot, monkeypatch):
     t[100_000:260_000] = ord("G")
     cases.append(t)
     for t in cases:
-        got = build_suffix_array(t)
+        got = build_suffix_array(t, debug=dbg)
         assert (got == oracle.sa_c(t)).all(), (len(t), pivot)
     for n in (70_001, 1_000_000):
         t = oracle.gen_text("dna", n, seed=n)
-        got = build_suffix_array(t, init_chars=2)
+        got = build_suffix_array(t, init_chars=2, debug=dbg)
         assert (got == oracle.sa_c(t)).all(), (n, pivot)
 
 
@@ -595,21 +593,18 @@ def test_bucketed_round1_dense_ranks(gpu, oracle):
 
 
 @pytest.mark.parametrize("mode", ["padded", "overflow", "exact"])
-def test_round1_padded_segments(gpu, oracle, golden, mode, monkeypatch):
+def test_round1_padded_segments(gpu, oracle, golden, mode):
     """From 2^26 suffixes the first bucket pass writes into segments sized
     from a 1-in-2^ssh sample (k_bucket_sample, sa_bucket.h) instead of exact
-    digit totals; a segment that overflows (forced here by
-    SA_PAD_TEST_OVERFLOW: no slack) makes the round run again with the exact
-    totals; SA_NO_PAD takes the exact totals at once.  Config-2 known answer
+    digit totals; a segment that overflows (forced here by debug
+    "pad_overflow": no slack) makes the round run again with the exact
+    totals; "no_pad" takes the exact totals at once.  Config-2 known answer
     (64 MiB DNA) through all three."""
     from hpc_suffix_array_amd import build_suffix_array
-    if mode == "overflow":
-        monkeypatch.setenv("SA_PAD_TEST_OVERFLOW", "1")
-    if mode == "exact":
-        monkeypatch.setenv("SA_NO_PAD", "1")
+    dbg = {"padded": (), "overflow": ("pad_overflow",), "exact": ("no_pad",)}[mode]
     k = golden["known"]["dna_64MiB"]
     t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
-    got, st = build_suffix_array(t, return_stats=True)
+    got, st = build_suffix_array(t, return_stats=True, debug=dbg)
     assert st["round1"] == "bucketed"
     assert st["round1_segments"] == {"padded": "padded", "overflow": "padded-overflow", "exact": "exact"}[mode], st
     assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
@@ -637,20 +632,17 @@ def test_round1_padded_segments_skewed(gpu, oracle):
 
 
 @pytest.mark.parametrize("layout", ["default", "no_pk8", "no_cmp"])
-def test_round1_layouts(gpu, oracle, golden, layout, monkeypatch):
+def test_round1_layouts(gpu, oracle, golden, layout):
     """Key layouts of the bucketed first round (sa_kernels.h BucketSpec,
     sa_split.h k_split_text<.., PK8>): the compact low (cmp) with packed
     8-byte first-pass items (pk8, power-of-two alphabets with the bits to
     spare), the compact low alone, and the original layout -- same SA."""
     from hpc_suffix_array_amd import build_suffix_array
-    if layout == "no_pk8":
-        monkeypatch.setenv("SA_NO_PK8", "1")
-    if layout == "no_cmp":
-        monkeypatch.setenv("SA_NO_CMP", "1")
+    dbg = () if layout == "default" else (layout,)
     for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21), ("alnum", 1_500_007), ("binary", 1 << 20)):
         t = oracle.gen_text(kind, n, seed=n + 1)
         t[-1] = t.max()   # no tail run of the smallest symbol (test_compact_layout_text_tails)
-        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed", debug=dbg)
         assert st["round1"] == "bucketed", (kind, st)
         lay = st["round1_layout"]
         assert lay["compact"] == (layout != "no_cmp"), (kind, lay)
@@ -683,7 +675,7 @@ def test_compact_layout_text_tails(gpu, oracle, tail):
 
 
 @pytest.mark.parametrize("extra", [0, 6])
-def test_local_sort_fixed_span(gpu, oracle, extra, monkeypatch):
+def test_local_sort_fixed_span(gpu, oracle, extra):
     """One-bucket windows of the compact layout split the bucket's whole key
     span into sub-buckets without measuring it (sa_bucket.h load_window,
     SA_LS_FIXED_SPAN); a window whose keys cluster (forced here by a span 2^6
@@ -691,12 +683,10 @@ def test_local_sort_fixed_span(gpu, oracle, extra, monkeypatch):
     launch that measures its span (sa_round1.h, retry list) instead of going
     to the LSD kernel."""
     from hpc_suffix_array_amd import build_suffix_array
-    if extra:
-        monkeypatch.setenv("SA_TEST_SPAN_EXTRA", str(extra))
     for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21)):
         t = oracle.gen_text(kind, n, seed=n + 5)
         t[-1] = t.max()
-        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed", span_extra=extra)
         assert st["round1"] == "bucketed" and st["round1_layout"]["compact"], (kind, st)
         assert (got == oracle.sa_c(t)).all(), (kind, extra)
 

@@ -1,6 +1,6 @@
 """The sampled lower bound of the sparse rank look-ups (interpolation-
-guided search of the round-1 key samples, then 4-ary steps over the last
-2^ksh slots; hpc_suffix_array_amd/csrc/sa_search.h) against
+guided search of the round-1 key samples, then a binary search over the
+last 2^ksh slots; hpc_suffix_array_amd/csrc/sa_search.h) against
 std::lower_bound on the host: g++ builds tests/cpp/search_check.cpp."""
 import os
 import subprocess
