@@ -313,7 +313,7 @@ class DistributedSA:
         G, r = self.G, self.r
         dev = text.device
         lo, hi = n * r // G, n * (r + 1) // G
-        self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": []}
+        self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": [], "cross_requests": []}
         self._events = []
         self._mark("alphabet", dev)
         # alphabet of the whole text: OR of the slices' masks (MAX of flags;
@@ -365,6 +365,8 @@ class DistributedSA:
                 raise RuntimeError("distributed doubling did not converge")
             recv_counts = [row[1 + r] for row in mat]
             self.stats["requests"].append(sum(sum(row[1:]) for row in mat))
+            # look-ups answered by another rank (they cross xGMI under RCCL)
+            self.stats["cross_requests"].append(sum(row[1 + q] for p, row in enumerate(mat) for q in range(G) if q != p))
             # every rank holds the whole count matrix: the slice count of both
             # exchanges needs no extra collective
             slices = max([0] + [(x + XCHUNK - 1) // XCHUNK for row in mat for x in row[1:]])

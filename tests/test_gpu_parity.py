@@ -709,3 +709,174 @@ def test_config4_partition_at_its_own_shape(gpu):
     assert sum(r["m"] for r in rows) == 1 << 32
     assert max(r["share"] for r in rows) < 1.2, rows
     assert rows[0]["bucket_bits"] == 19
+
+
+# configs[3] (4 GiB byte256 over 8 GPUs, manber_myers_mpi.c:108-144) at the
+# largest shape one MI355X holds as several ranks: n = 2^31 + 17 over 4 HIP
+# ranks (~2^29 suffixes each, 32-bit index fields, 18-19-bit buckets), with
+# copies of one 3000-byte block planted across the text so that groups survive
+# round 1 and the later rounds' rank look-ups cross ranks for several rounds.
+CFG4_N = (1 << 31) + 17
+CFG4_PLANT = (1000, 3000, 7)   # source offset, block length, copies
+
+
+def _cfg4_text(ops, torch):
+    n = CFG4_N
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    ops.b.generate_text(t, n, bytes(range(256)), seed=3)
+    src, L, copies = CFG4_PLANT
+    blk = t[src: src + L].clone()
+    for k in range(1, copies + 1):
+        p = k * (n // (copies + 1)) + 777
+        t[p: p + L] = blk
+    torch.cuda.synchronize()
+    return t
+
+
+def _cfg4_log(name):
+    import faulthandler
+    logdir = os.path.join(ROOT, "gpurun_out")
+    os.makedirs(logdir, exist_ok=True)
+    log = open(os.path.join(logdir, f"cfg4_{name}.log"), "w")
+    os.dup2(log.fileno(), 2)
+    os.environ["SA_DIST_TRACE"] = "1"
+    faulthandler.dump_traceback_later(150, exit=True, file=log)
+    return lambda *a: print(*a, file=log, flush=True)
+
+
+def _cfg4_reference(port, path, q):
+    """World-1 build of the planted text through the same driver (the path
+    test_distributed_hip_config4_shape pins), O(n)-checked, its SA written to
+    host shared memory for the ranks' slice comparison; this process exits
+    before the ranks start, so its HBM is free again."""
+    sys.path.insert(0, ROOT)
+    say = _cfg4_log("reference")
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+        ops = HipRangeOps(0, 0)
+        t = _cfg4_text(ops, torch)
+        d = DistributedSA(ops)
+        sa_local, sa_off = d.build(t, CFG4_N)
+        torch.cuda.synchronize()
+        say("built", d.stats)
+        ok = bool(ops.b.check(t, CFG4_N, sa_local))
+        say("checked", ok)
+        mm = np.memmap(path, dtype=np.int32, mode="w+", shape=(CFG4_N,))
+        step = 1 << 27
+        for a in range(0, CFG4_N, step):
+            b = min(CFG4_N, a + step)
+            mm[a:b] = sa_local[a:b].cpu().numpy()
+        mm.flush()
+        del mm
+        say("written")
+        q.put({"ok": ok, "path": d.stats["path"], "m": d.stats["m"], "rounds": d.stats["rounds"],
+               "unsorted": d.stats["unsorted"]})
+    except BaseException:
+        import traceback
+        say(traceback.format_exc())
+        q.put({"error": traceback.format_exc()})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def _cfg4_rank(rank, world, port, path, q):
+    """One of `world` HIP ranks sharing the box's GPU (collectives staged
+    through gloo): the range-partitioned build, then this rank's SA slice
+    against the same slice of the world-1 build."""
+    sys.path.insert(0, ROOT)
+    say = _cfg4_log(f"w{world}_r{rank}")
+    import torch
+    import torch.distributed as dist
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps
+    try:
+        torch.cuda.set_device(0)
+        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        ops = HipRangeOps(0, 0)
+        t = _cfg4_text(ops, torch)
+        d = DistributedSA(ops)
+        sa_local, sa_off = d.build(t, CFG4_N)
+        torch.cuda.synchronize()
+        say("built", d.stats)
+        m = sa_local.numel()
+        ref = np.memmap(path, dtype=np.int32, mode="r", shape=(CFG4_N,))
+        want = torch.from_numpy(np.array(ref[int(sa_off): int(sa_off) + m])).cuda()   # a writable host copy
+        eq = bool((want == sa_local).all().item())
+        say("compared", eq)
+        q.put({"rank": rank, "eq": eq, "m": m, "sa_off": int(sa_off), "path": d.stats["path"],
+               "rounds": d.stats["rounds"], "requests": d.stats["requests"],
+               "cross": d.stats["cross_requests"], "bucket_bits": d.stats["bucket_bits"]})
+    except BaseException:
+        import traceback
+        say(traceback.format_exc())
+        q.put({"rank": rank, "error": traceback.format_exc()})
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.slow
+def test_config4_cross_rank_rounds_four_ranks(gpu):
+    """configs[3]'s range partition end to end at n = 2^31 + 17 byte256 over
+    4 ranks on the box's GPU: round 1 per range and every later round's rank
+    requests and answers exchanged between ranks (sa_dist_req_* /
+    sa_dist_answer / sa_dist_refine and the sliced all-to-alls of
+    distributed.py), each rank's SA slice equal to the O(n)-checked world-1
+    build of the same text (manber_myers_mpi.c:108-144 is the shape
+    replaced; the 8-GPU RCCL run is the driver's)."""
+    import gc
+    import socket
+
+    import torch
+    import torch.multiprocessing as mp
+    gc.collect()
+    torch.cuda.empty_cache()   # this process's cached HBM (earlier tests) back to the device
+    shm = "/dev/shm" if os.path.isdir("/dev/shm") else "/tmp"
+    path = os.path.join(shm, f"sa_cfg4_{os.getpid()}.i32")
+
+    def port():
+        with socket.socket() as s:
+            s.bind(("127.0.0.1", 0))
+            return s.getsockname()[1]
+
+    ctx = mp.get_context("spawn")
+    try:
+        q = ctx.Queue()
+        p = ctx.Process(target=_cfg4_reference, args=(port(), path, q))
+        p.start()
+        ref = q.get(timeout=300)
+        p.join(timeout=60)
+        assert "error" not in ref, ref["error"]
+        assert p.exitcode == 0
+        assert ref["ok"] and ref["path"] == "range" and ref["m"] == CFG4_N, ref
+        world = 4
+        pt = port()
+        procs = [ctx.Process(target=_cfg4_rank, args=(r, world, pt, path, q)) for r in range(world)]
+        for pr in procs:
+            pr.start()
+        res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x["rank"])
+        for pr in procs:
+            pr.join(timeout=60)
+        errs = [x["error"] for x in res if "error" in x]
+        assert not errs, errs[0]
+        assert all(pr.exitcode == 0 for pr in procs)
+        assert all(x["path"] == "range" for x in res), res
+        assert all(x["eq"] for x in res), [(x["rank"], x["eq"]) for x in res]
+        # the ranges tile the SA in rank order
+        off = 0
+        for x in res:
+            assert x["sa_off"] == off, res
+            off += x["m"]
+        assert off == CFG4_N
+        assert max(x["m"] for x in res) < 1.2 * CFG4_N / world
+        # later rounds with look-ups answered by other ranks: at least two
+        cross = res[0]["cross"]
+        assert sum(1 for c in cross if c > 0) >= 2, res[0]
+        assert res[0]["rounds"] >= 3 and ref["rounds"] >= 3, (res[0], ref)
+    finally:
+        if os.path.exists(path):
+            os.remove(path)
