@@ -910,16 +910,17 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
                        sa_stats* st, uint64_t** sorted, uint32_t* P) {
     *sorted = nullptr;
     uint32_t* const gs = c->u_pos[uo];   // G + 1 group starts (the next set is written by segments())
+    uint32_t* const pr = gs + G + 1;     // G pivot ranks (2 G + 1 <= m / 2 + 1 words of the buffer)
     uint32_t* const gP = c->vals_alt;    // 3 (G + 1): members of each class before each group
     uint32_t* const cc = c->hist;        // 3 x chunks class counts, scanned in place
     const uint32_t Gu = (uint32_t)G;
     tm.begin(SA_K_SORT_U);
     hipLaunchKernelGGL(k_pivot_keys, dim3((uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192)), dim3(kBlock),
                        0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m, (const uint32_t*)c->rank,
-                       n, h, wr, Gu, ukb1, gs);
+                       n, h, wr, Gu, ukb1, gs, pr);
     hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
-                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs, Gu, wr, cc,
-                       gP, nullptr, nullptr, nullptr, nullptr);
+                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                       (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr);
     hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
     tm.end();
     SA_HIP(hipGetLastError());
@@ -937,8 +938,8 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     hipLaunchKernelGGL(k_pivot_gp, dim3((uint32_t)std::min<uint64_t>((G + kBlock) / kBlock, 8192)), dim3(kBlock), 0, s,
                        (const uint32_t*)gs, Gu, (const uint32_t*)cc, cu, (const uint32_t*)c->totals, gP);
     hipLaunchKernelGGL(k_pivot_pass<2>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
-                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs, Gu, wr, cc,
-                       gP, ukb0, c->vals_u, kbA, c->u_idx[uo]);
+                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                       (const uint32_t*)pr, Gu, wr, cc, gP, ukb0, c->vals_u, kbA, c->u_idx[uo]);
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SORT_U, 36 * m);

@@ -22,8 +22,10 @@
 //
 // Kernels (Chunking over U, one workgroup per chunk walking 4096-member
 // tiles; wave w owns a contiguous 1024 slice, rows of 64 lanes):
-//   k_pivot_keys    key(e) = g << wr | rank[x + h] (dense ranks) and the
-//                   group starts gs[g] (gs[G] = m)
+//   k_pivot_keys    key(e) = g << wr | rank[x + h] (dense ranks), the
+//                   group starts gs[g] (gs[G] = m) and the pivots' ranks
+//                   pr[g] (the passes read a member's pivot with one
+//                   dependent load, pr[g], instead of two, keys[gs[g]])
 //   k_pivot_pass<0> class counts per chunk (k_scan_rows then gives P_c at
 //                   each chunk start) and per group start inside its chunk
 //   k_pivot_gp      gP[c][g] = P_c(gs_g) (members of class c before g)
@@ -39,13 +41,16 @@ __global__ __launch_bounds__(kBlock) void k_pivot_keys(const uint32_t* __restric
                                                        const uint32_t* __restrict__ u_g, uint64_t m,
                                                        const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
                                                        uint32_t wr, uint32_t G, uint64_t* __restrict__ keys,
-                                                       uint32_t* __restrict__ gs) {
+                                                       uint32_t* __restrict__ gs, uint32_t* __restrict__ pr) {
     for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < m; e += (uint64_t)gridDim.x * kBlock) {
         const uint64_t x = u_idx[e];
         const uint32_t g = u_g[e];
-        const uint64_t r1 = x + h < n ? rank[x + h] : 0u;
+        const uint32_t r1 = x + h < n ? rank[x + h] : 0u;
         keys[e] = ((uint64_t)g << wr) | r1;
-        if (e == 0 || u_g[e - 1] != g) gs[g] = (uint32_t)e;
+        if (e == 0 || u_g[e - 1] != g) {
+            gs[g] = (uint32_t)e;
+            pr[g] = r1;
+        }
         if (e == m - 1) gs[G] = (uint32_t)m;
     }
 }
@@ -60,7 +65,8 @@ template <int MODE>
 __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ u_idx,
                                                        const uint32_t* __restrict__ u_g, Chunking ch,
-                                                       const uint32_t* __restrict__ gs, uint32_t G, uint32_t wr,
+                                                       const uint32_t* __restrict__ gs, const uint32_t* __restrict__ pr,
+                                                       uint32_t G, uint32_t wr,
                                                        uint32_t* __restrict__ cc, uint32_t* __restrict__ gP,
                                                        uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
                                                        uint64_t* __restrict__ rkeys, uint32_t* __restrict__ ridx) {
@@ -88,7 +94,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
 #pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t e = w0 + (uint64_t)j * kWave + lane;
-            const uint64_t p = e < e1 ? keys[gs[g[j]]] : 0ull;
+            const uint64_t p = e < e1 ? (((uint64_t)g[j] << wr) | pr[g[j]]) : 0ull;
             cls[j] = e < e1 ? (key[j] < p ? 0u : key[j] == p ? 1u : 2u) : 3u;
 #pragma unroll
             for (int k = 0; k < 3; ++k) wc[k] += (uint32_t)__popcll(__ballot(cls[j] == (uint32_t)k));

@@ -21,7 +21,13 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_split_text", "scatter_first"), ("k_split_seg", "scatter_keys"), ("k_split<sa::SrcBucketKeys", "scatter_keys"),
+KINDS = [("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0>", "pivot_count"), ("k_pivot_pass<2>", "pivot_write"),
+         ("k_pivot_place", "pivot_place"), ("k_pivot_gp", "pivot_gp"), ("k_lsd_hist", "lsd_hist"),
+         ("k_lsd_base", "lsd_base"), ("k_lsd<", "lsd"), ("k_perm_rank", "perm_rank"), ("k_perm_split", "perm_split"),
+         ("k_perm_place", "perm_place"), ("k_tile_heads", "heads"), ("k_items_to_sa", "items_to_sa"),
+         ("k_split_list", "scatter_first"), ("k_usort_small", "sort_u_small"), ("k_usort_keys", "sort_u_keys"),
+         ("k_bucket_sample", "pack"), ("k_window_split", "windows"), ("k_window_list", "windows"),
+         ("k_split_text", "scatter_first"), ("k_split_seg", "scatter_keys"), ("k_split<sa::SrcBucketKeys", "scatter_keys"),
          ("k_bucket_hist", "pack"), ("k_bucket_starts", "bucket_starts"),
          ("k_init_rank", "init"), ("k_hist<sa::SrcRank>", "hist_rank"), ("k_hist<sa::SrcText>", "hist_text"),
          ("k_hist<sa::SrcU", "hist_u"), ("k_hist<sa::SrcKeys>", "hist_keys"),
