@@ -34,7 +34,8 @@ DROPIN_SYMBOLS = ["create_suffix_array", "destroy_suffix_array", "build_suffix_a
 EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_context_set_debug", "sa_workspace_bytes", "sa_build_device",
                "sa_build_ex", "sa_check_device", "sa_check", "sa_lcp_device", "sa_lcp", "sa_generate_text_device",
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
-               "sa_gather_u64_device", "sa_running_max_i64_device",
+               "sa_gather_u64_device", "sa_running_max_i64_device", "sa_inclusive_sum_i64_device",
+               "sa_count_below_u64_device", "sa_select_u8_device",
                "sa_dist_begin", "sa_dist_cuts", "sa_dist_plan_cuts", "sa_dist_release", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
                "sa_dist_answer", "sa_dist_refine",
                "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
@@ -203,6 +204,12 @@ def lib() -> ctypes.CDLL:
     L.sa_gather_u64_device.restype = i32
     L.sa_running_max_i64_device.argtypes = [vp, u64, vp]
     L.sa_running_max_i64_device.restype = i32
+    L.sa_inclusive_sum_i64_device.argtypes = [vp, u64, vp]
+    L.sa_inclusive_sum_i64_device.restype = i32
+    L.sa_count_below_u64_device.argtypes = [vp, u64, vp, u64, i32, vp, vp]
+    L.sa_count_below_u64_device.restype = i32
+    L.sa_select_u8_device.argtypes = [vp, u64, vp, ctypes.POINTER(u64), vp]
+    L.sa_select_u8_device.restype = i32
     DI = ctypes.POINTER(SaDistInfo)
     L.sa_dist_begin.argtypes = [vp, vp, u64, i32, i32, ctypes.POINTER(ctypes.c_uint32), vp, vp, DI]
     L.sa_dist_cuts.argtypes = [vp, ctypes.POINTER(u64), DI]

@@ -1776,93 +1776,205 @@ int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n,
     return SA_OK;
 }
 
-// Inclusive running max of m int64 values, in place: per-tile maxima
-// (256 lanes x 16 contiguous values), one workgroup scans the tile maxima,
-// each tile then scans itself from its carry.
+}  // extern "C"
+
+// Inclusive scans of m int64 values in place (running max: the group-start
+// carries of the sample-sort driver; sum: its dense group ids): per-tile
+// totals (256 lanes x 16 contiguous values), one workgroup scans the tile
+// totals, each tile then scans itself from its carry.
 constexpr int kRmBlock = 256, kRmItems = 16, kRmTile = kRmBlock * kRmItems;
 
+struct ScanMax {
+    static __device__ __forceinline__ int64_t id() { return INT64_MIN; }
+    static __device__ __forceinline__ int64_t f(int64_t a, int64_t b) { return a > b ? a : b; }
+};
+struct ScanSum {
+    static __device__ __forceinline__ int64_t id() { return 0; }
+    static __device__ __forceinline__ int64_t f(int64_t a, int64_t b) { return a + b; }
+};
+
+template <class Op>
 __device__ inline int64_t rm_block_incl(int64_t v, int64_t* s_w) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const int64_t y = __shfl_up(v, o, 64);
-        if (lane >= o && y > v) v = y;
+        if (lane >= o) v = Op::f(y, v);
     }
     if (lane == 63) s_w[w] = v;
     __syncthreads();
-    for (int q = 0; q < w; ++q) v = s_w[q] > v ? s_w[q] : v;
-    return v;
+    int64_t c = Op::id();
+    for (int q = 0; q < w; ++q) c = Op::f(c, s_w[q]);
+    return Op::f(c, v);
 }
 
-// exclusive block max: the inclusive max of the previous lane
+// exclusive block scan: the inclusive value of the previous lane
+template <class Op>
 __device__ inline int64_t rm_block_excl(int64_t v, int64_t* s_w) {
-    const int64_t incl = rm_block_incl(v, s_w);
+    const int64_t incl = rm_block_incl<Op>(v, s_w);
     int64_t c = __shfl_up(incl, 1, 64);
     if ((threadIdx.x & 63) == 0) {
-        c = INT64_MIN;
-        for (int q = 0; q < (int)(threadIdx.x >> 6); ++q) c = s_w[q] > c ? s_w[q] : c;
+        c = Op::id();
+        for (int q = 0; q < (int)(threadIdx.x >> 6); ++q) c = Op::f(c, s_w[q]);
     }
     return c;
 }
 
+template <class Op>
 __global__ __launch_bounds__(kRmBlock) void k_rmax_tiles(const int64_t* __restrict__ v, uint64_t m,
                                                          int64_t* __restrict__ tmax) {
     __shared__ int64_t s_w[kRmBlock / 64];
     const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
-    int64_t x = INT64_MIN;
+    int64_t x = Op::id();
     for (int j = 0; j < kRmItems; ++j)
-        if (b0 + j < m) x = v[b0 + j] > x ? v[b0 + j] : x;
-    x = rm_block_incl(x, s_w);
+        if (b0 + j < m) x = Op::f(x, v[b0 + j]);
+    x = rm_block_incl<Op>(x, s_w);
     if (threadIdx.x == kRmBlock - 1) tmax[blockIdx.x] = x;
 }
 
-// exclusive running max of the tile maxima (one workgroup of kRmBlock lanes)
+// exclusive scan of the tile totals (one workgroup of kRmBlock lanes); the
+// grand total lands in tmax[tiles]
+template <class Op>
 __global__ __launch_bounds__(kRmBlock) void k_rmax_carry(int64_t* __restrict__ tmax, uint64_t tiles) {
     __shared__ int64_t s_w[kRmBlock / 64];
     const uint64_t per = (tiles + kRmBlock - 1) / kRmBlock;
     const uint64_t a = (uint64_t)threadIdx.x * per, e = a + per < tiles ? a + per : tiles;
-    int64_t x = INT64_MIN;
-    for (uint64_t i = a; i < e; ++i) x = tmax[i] > x ? tmax[i] : x;
-    int64_t c = rm_block_excl(x, s_w);
+    int64_t x = Op::id();
+    for (uint64_t i = a; i < e; ++i) x = Op::f(x, tmax[i]);
+    int64_t c = rm_block_excl<Op>(x, s_w);
     for (uint64_t i = a; i < e; ++i) {
         const int64_t y = tmax[i];
         tmax[i] = c;
-        c = y > c ? y : c;
+        c = Op::f(c, y);
     }
+    if (a < tiles && e == tiles) tmax[tiles] = c;
 }
 
+template <class Op>
 __global__ __launch_bounds__(kRmBlock) void k_rmax_apply(int64_t* __restrict__ v, uint64_t m,
                                                          const int64_t* __restrict__ tcarry) {
     __shared__ int64_t s_w[kRmBlock / 64];
     const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
     int64_t r[kRmItems];
-    int64_t x = INT64_MIN;
+    int64_t x = Op::id();
     for (int j = 0; j < kRmItems; ++j) {
-        r[j] = b0 + j < m ? v[b0 + j] : INT64_MIN;
-        x = r[j] > x ? r[j] : x;
+        r[j] = b0 + j < m ? v[b0 + j] : Op::id();
+        x = Op::f(x, r[j]);
     }
-    int64_t c = rm_block_excl(x, s_w);
-    const int64_t tc = tcarry[blockIdx.x];
-    c = tc > c ? tc : c;
+    int64_t c = Op::f(tcarry[blockIdx.x], rm_block_excl<Op>(x, s_w));
     for (int j = 0; j < kRmItems; ++j) {
-        c = r[j] > c ? r[j] : c;
+        c = Op::f(c, r[j]);
         if (b0 + j < m) v[b0 + j] = c;
     }
 }
 
+
+
+
+// out[i] = #{ j : sorted[j] < q[i] } (<= with RIGHT): one lane per query
+template <bool RIGHT>
+__global__ __launch_bounds__(kBlock) void k_count_below(const uint64_t* __restrict__ sorted, uint64_t m,
+                                                        const uint64_t* __restrict__ q, uint64_t nq,
+                                                        int64_t* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nq; i += (uint64_t)gridDim.x * kBlock) {
+        const uint64_t x = q[i];
+        uint64_t lo = 0, hi = m;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) / 2;
+            if (RIGHT ? sorted[mid] <= x : sorted[mid] < x) lo = mid + 1;
+            else hi = mid;
+        }
+        out[i] = (int64_t)lo;
+    }
+}
+
+
+// Stream compaction of a byte mask: per-tile counts of the non-zero bytes
+// (16 per lane), their exclusive sum (k_rmax_carry<ScanSum>), then each tile
+// writes its positions in order.
+__global__ __launch_bounds__(kRmBlock) void k_sel_count(const uint8_t* __restrict__ mask, uint64_t m,
+                                                        int64_t* __restrict__ tcnt) {
+    __shared__ int64_t s_w[kRmBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
+    int64_t c = 0;
+    for (int j = 0; j < kRmItems; ++j) c += (b0 + j < m && mask[b0 + j]) ? 1 : 0;
+    c = rm_block_incl<ScanSum>(c, s_w);
+    if (threadIdx.x == kRmBlock - 1) tcnt[blockIdx.x] = c;
+}
+
+__global__ __launch_bounds__(kRmBlock) void k_sel_write(const uint8_t* __restrict__ mask, uint64_t m,
+                                                        const int64_t* __restrict__ toff, int64_t* __restrict__ out) {
+    __shared__ int64_t s_w[kRmBlock / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * kRmTile + (uint64_t)threadIdx.x * kRmItems;
+    uint32_t bits = 0;
+    for (int j = 0; j < kRmItems; ++j) bits |= (b0 + j < m && mask[b0 + j]) ? 1u << j : 0u;
+    int64_t o = toff[blockIdx.x] + rm_block_excl<ScanSum>((int64_t)__popc(bits), s_w);
+    while (bits) {
+        const int j = __builtin_ctz(bits);
+        bits &= bits - 1u;
+        out[o++] = (int64_t)(b0 + j);
+    }
+}
+
+template <class Op>
+static int scan_i64(int64_t* d_v, uint64_t m, hipStream_t s) {
+    const uint64_t tiles = (m + kRmTile - 1) / kRmTile;
+    if (tiles > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "m too large");
+    int64_t* d_t = nullptr;
+    SA_HIP(hipMallocAsync((void**)&d_t, (tiles + 1) * 8, s));
+    hipLaunchKernelGGL(k_rmax_tiles<Op>, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
+    hipLaunchKernelGGL(k_rmax_carry<Op>, dim3(1), dim3(kRmBlock), 0, s, d_t, tiles);
+    hipLaunchKernelGGL(k_rmax_apply<Op>, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipFreeAsync(d_t, s));
+    return SA_OK;
+}
+
+extern "C" {
+
 int sa_running_max_i64_device(int64_t* d_v, uint64_t m, void* stream) {
     if (m == 0) return SA_OK;
     if (!d_v) return set_err(SA_E_INVALID, "NULL device pointer");
+    return scan_i64<ScanMax>(d_v, m, (hipStream_t)stream);
+}
+
+int sa_inclusive_sum_i64_device(int64_t* d_v, uint64_t m, void* stream) {
+    if (m == 0) return SA_OK;
+    if (!d_v) return set_err(SA_E_INVALID, "NULL device pointer");
+    return scan_i64<ScanSum>(d_v, m, (hipStream_t)stream);
+}
+
+int sa_count_below_u64_device(const uint64_t* d_sorted, uint64_t m, const uint64_t* d_q, uint64_t nq, int right,
+                              int64_t* d_out, void* stream) {
+    if (nq == 0) return SA_OK;
+    if ((!d_sorted && m) || !d_q || !d_out) return set_err(SA_E_INVALID, "NULL device pointer");
+    hipStream_t s = (hipStream_t)stream;
+    const uint32_t grid = (uint32_t)std::min<uint64_t>((nq + kBlock - 1) / kBlock, 8192);
+    if (right) hipLaunchKernelGGL(k_count_below<true>, dim3(grid), dim3(kBlock), 0, s, d_sorted, m, d_q, nq, d_out);
+    else hipLaunchKernelGGL(k_count_below<false>, dim3(grid), dim3(kBlock), 0, s, d_sorted, m, d_q, nq, d_out);
+    SA_HIP(hipGetLastError());
+    return SA_OK;
+}
+
+int sa_select_u8_device(const uint8_t* d_mask, uint64_t m, int64_t* d_out, uint64_t* count, void* stream) {
+    if (!count) return set_err(SA_E_INVALID, "count is NULL");
+    *count = 0;
+    if (m == 0) return SA_OK;
+    if (!d_mask) return set_err(SA_E_INVALID, "NULL device pointer");
     hipStream_t s = (hipStream_t)stream;
     const uint64_t tiles = (m + kRmTile - 1) / kRmTile;
     if (tiles > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "m too large");
     int64_t* d_t = nullptr;
-    SA_HIP(hipMallocAsync((void**)&d_t, tiles * 8, s));
-    hipLaunchKernelGGL(k_rmax_tiles, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
-    hipLaunchKernelGGL(k_rmax_carry, dim3(1), dim3(kRmBlock), 0, s, d_t, tiles);
-    hipLaunchKernelGGL(k_rmax_apply, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_v, m, d_t);
+    int64_t total = 0;
+    SA_HIP(hipMallocAsync((void**)&d_t, (tiles + 1) * 8, s));
+    hipLaunchKernelGGL(k_sel_count, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_mask, m, d_t);
+    hipLaunchKernelGGL(k_rmax_carry<ScanSum>, dim3(1), dim3(kRmBlock), 0, s, d_t, tiles);
+    if (d_out) hipLaunchKernelGGL(k_sel_write, dim3((uint32_t)tiles), dim3(kRmBlock), 0, s, d_mask, m, d_t, d_out);
     SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(&total, d_t + tiles, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipFreeAsync(d_t, s));
+    SA_HIP(hipStreamSynchronize(s));
+    *count = (uint64_t)total;
     return SA_OK;
 }
 

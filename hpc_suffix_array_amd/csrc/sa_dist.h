@@ -314,6 +314,10 @@ struct SrcUArr {
 // ---------------------------------------------------------------------------
 static uint32_t dist_cshift(const DistState& d) { return d.bp.bs.bb - kCoarseBits; }
 
+#ifndef SA_DIST_SHORT_K
+#define SA_DIST_SHORT_K 1
+#endif
+
 static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int world, int rank,
                       const uint32_t present[8], uint64_t* d_coarse, hipStream_t s, sa_dist_info* info) {
     std::memset(info, 0, sizeof *info);
@@ -349,6 +353,23 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     if (!planned) {
         info->status = SA_DIST_UNSUPPORTED;   // one symbol / a key layout that does not fit
         return SA_OK;
+    }
+    // one symbol fewer when that lets a range's first pass write packed
+    // 8-byte items (PK8: 8 + 12 bytes per suffix less through the two bucket
+    // passes) and sigma^K stays >= 256 n, i.e. about n / 256 suffixes left
+    // unsorted by round 1 for one more look-up round: configs[3] (byte256,
+    // n = 2^32, G = 8) K = 6 -> 5, 8 + 5 + 25 + 32 -> 8 + 5 + 17 + 32 bits.
+    // Every rank derives the same K (sigma, n and world only).
+    if (SA_DIST_SHORT_K && world > 1 && bp.K > bp.bs.s + 1) {
+        const uint32_t hb_est = range_hb((uint32_t)((3ull << bp.bs.bb) / (2ull * (uint64_t)world)));
+        unsigned __int128 pk = 1;
+        for (uint32_t t = 0; t + 1 < bp.K; ++t) pk *= sigma;
+        BucketPlan b2;
+        if (!plan_pk8(bp, hb_est, c->dbg) && pk >= (unsigned __int128)n * 256u &&
+            plan_bucketed(sigma, n, bp.K - 1, SA_ROUND1_BUCKETED, 0, &b2, world, bp.bs.cmp != 0) &&
+            (!b2.bs.cmp || !short_suffix_ties(h_tail, n, tail_n, h_code, sigma, b2.bs.s, b2.bs.R)) &&
+            plan_pk8(b2, hb_est, c->dbg))
+            bp = b2;
     }
     d->bp = bp;
     d->K = bp.K;

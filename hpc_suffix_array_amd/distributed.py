@@ -424,13 +424,6 @@ def gather_sa(sa_local: torch.Tensor, sa_off: int, n: int, group=None) -> torch.
     return full
 
 
-def mask_positions(mask: torch.Tensor) -> torch.Tensor:
-    """int64 positions of the set elements of a bool vector (torch.nonzero
-    over CHUNK-element slices)."""
-    parts = [mask[a: a + CHUNK].nonzero().squeeze(1) + a for a in range(0, mask.numel(), CHUNK)]
-    return torch.cat(parts) if parts else torch.zeros(0, dtype=I64, device=mask.device)
-
-
 def chunked_map(fn, *ts: torch.Tensor) -> torch.Tensor:
     """fn applied elementwise over CHUNK-element slices of equal-length
     vectors: torch's own kernels never see 2^30 elements here (bincount and
@@ -439,33 +432,6 @@ def chunked_map(fn, *ts: torch.Tensor) -> torch.Tensor:
     if m <= CHUNK:
         return fn(*ts)
     return torch.cat([fn(*(t[a: a + CHUNK] for t in ts)) for a in range(0, m, CHUNK)])
-
-
-def count_below(sorted_x: torch.Tensor, q: torch.Tensor, right: bool = False) -> torch.Tensor:
-    """For each q the number of elements of the sorted vector < q (<= q with
-    right): searchsorted within each CHUNK slice, summed."""
-    out = torch.zeros(q.numel(), dtype=I64, device=q.device)
-    for a in range(0, sorted_x.numel(), CHUNK):
-        out += torch.searchsorted(sorted_x[a: a + CHUNK], q, right=right)
-    return out
-
-
-def cumsum_i64(x: torch.Tensor) -> torch.Tensor:
-    """Inclusive int64 prefix sum over CHUNK slices, carrying the last sum
-    (a device scalar, no host sync) into the next slice."""
-    parts, carry = [], None
-    for a in range(0, x.numel(), CHUNK):
-        s = torch.cumsum(x[a: a + CHUNK].to(I64), 0)
-        if carry is not None:
-            s += carry
-        carry = s[-1]
-        parts.append(s)
-    return torch.cat(parts) if parts else torch.zeros(0, dtype=I64, device=x.device)
-
-
-def count_true(mask: torch.Tensor) -> int:
-    """Number of set elements of a bool vector (summed per CHUNK slice)."""
-    return int(sum(int(mask[a: a + CHUNK].sum().item()) for a in range(0, mask.numel(), CHUNK)))
 
 
 def bit_width(x: int) -> int:
@@ -556,6 +522,44 @@ class HipOps:
         N.check(self.L.sa_scatter_u64_device(dst.data_ptr(), dst.numel(), idx.data_ptr(), base, src.data_ptr(),
                                              idx.numel(), self._stream()), "sa_scatter_u64_device")
 
+    def count_below(self, sorted_x: torch.Tensor, q: torch.Tensor, right: bool = False) -> torch.Tensor:
+        """For each q the number of elements of the sorted (non-negative)
+        int64 vector below q (at most q with right): a binary search per
+        query (sa_count_below_u64_device)."""
+        sorted_x, q = sorted_x.contiguous(), q.contiguous()
+        out = torch.empty(q.numel(), dtype=I64, device=q.device)
+        if q.numel():
+            N.check(self.L.sa_count_below_u64_device(sorted_x.data_ptr() if sorted_x.numel() else None,
+                                                     sorted_x.numel(), q.data_ptr(), q.numel(), 1 if right else 0,
+                                                     out.data_ptr(), self._stream()), "sa_count_below_u64_device")
+        return out
+
+    def cumsum(self, x: torch.Tensor) -> torch.Tensor:
+        """Inclusive int64 prefix sum (sa_inclusive_sum_i64_device)."""
+        out = x.to(I64).contiguous().clone()
+        N.check(self.L.sa_inclusive_sum_i64_device(out.data_ptr(), out.numel(), self._stream()),
+                "sa_inclusive_sum_i64_device")
+        return out
+
+    def select(self, mask: torch.Tensor) -> torch.Tensor:
+        """int64 positions of the set elements of a bool vector, in order
+        (sa_select_u8_device: per-tile counts, their scan, ordered writes)."""
+        mask = mask.contiguous()
+        out = torch.empty(mask.numel(), dtype=I64, device=mask.device)
+        cnt = ctypes.c_uint64()
+        N.check(self.L.sa_select_u8_device(mask.data_ptr() if mask.numel() else None, mask.numel(),
+                                           out.data_ptr() if mask.numel() else None, ctypes.byref(cnt),
+                                           self._stream()), "sa_select_u8_device")
+        return out[: cnt.value]
+
+    def count_true(self, mask: torch.Tensor) -> int:
+        """Number of set elements of a bool vector (one device count, one sync)."""
+        mask = mask.contiguous()
+        cnt = ctypes.c_uint64()
+        N.check(self.L.sa_select_u8_device(mask.data_ptr() if mask.numel() else None, mask.numel(), None,
+                                           ctypes.byref(cnt), self._stream()), "sa_select_u8_device")
+        return int(cnt.value)
+
 
 class SampleSortSA:
     """General range-partitioned builder by sample sort (the fallback of
@@ -597,7 +601,7 @@ class SampleSortSA:
         else:
             sd, order = self.ops.argsort(dest.to(I64), bit_width(self.G - 1))
             q = torch.arange(self.G + 1, dtype=I64, device=dest.device)
-            send = torch.diff(count_below(sd, q)).tolist()
+            send = torch.diff(self.ops.count_below(sd, q)).tolist()
         outs, recv = self._alltoallv([self.ops.gather(t, order) for t in tensors], send)
         return outs, recv, order, send
 
@@ -631,8 +635,8 @@ class SampleSortSA:
                 continue
             ks, rs, ps, _ = allsamp[min(len(allsamp) - 1, j * len(allsamp) // self.G)]
             kt = torch.tensor([ks], dtype=I64, device=dev)
-            lo = int(count_below(keys, kt).item())
-            hi = int(count_below(keys, kt, right=True).item())
+            lo = int(self.ops.count_below(keys, kt).item())
+            hi = int(self.ops.count_below(keys, kt, right=True).item())
             if self.r < rs:
                 c = hi
             elif self.r > rs:
@@ -695,17 +699,19 @@ class SampleSortSA:
 
     def _carry_start(self, head: torch.Tensor, idx: torch.Tensor, dev) -> torch.Tensor:
         """For each element the value of idx at the last head at or before it
-        (scanning across ranks)."""
+        (scanning across ranks): the HIP running max of idx at the heads (-1
+        elsewhere); its last element, the largest head idx of this rank, is
+        its carry for the next ranks."""
         m = head.numel()
+        v = None
         local_last = -1
-        for a in range(0, m, CHUNK):
-            local_last = max(local_last, int(torch.where(head[a: a + CHUNK], idx[a: a + CHUNK], -1).max().item()))
+        if m:
+            v = self.ops.running_max(chunked_map(lambda hd, ix: torch.where(hd, ix, -1), head, idx))
+            local_last = int(v[-1].item())
         lasts = self._gather(torch.tensor([local_last], dtype=I64, device=dev)).reshape(-1).tolist()
         carry = max([-1] + lasts[: self.r])
         if m == 0:
             return idx
-        v = chunked_map(lambda hd, ix: torch.where(hd, ix, -1), head, idx)
-        v = self.ops.running_max(v)
         return chunked_map(lambda x: torch.where(x < 0, carry, x), v)
 
     # -- the build ----------------------------------------------------------------
@@ -717,8 +723,8 @@ class SampleSortSA:
         lo, hi = bnd[r], bnd[r + 1]
         bnd_t = torch.tensor(bnd[1:-1], dtype=I64, device=dev)
 
-        def owner(x):
-            return chunked_map(lambda y: torch.searchsorted(bnd_t, y, right=True), x)
+        def owner(x):   # the rank whose position range holds x: boundaries <= x
+            return self.ops.count_below(bnd_t, x, right=True)
 
         # alphabet: OR of the ranks' presence masks (torch's NCCL backend has
         # no BOR reduction, so gather the 8 words and OR them here)
@@ -748,12 +754,12 @@ class SampleSortSA:
         rank_local = torch.zeros(hi - lo, dtype=I64, device=dev)
         (ri, rv), _, _, _ = self._route(owner(idx), [idx, hpos + 1])
         self.ops.scatter(rank_local, ri, lo, rv)
-        sel = mask_positions(single)
+        sel = self.ops.select(single)
         fin_pos, fin_idx = [self.ops.gather(gpos, sel)], [self.ops.gather(idx, sel)]
         keep = ~single
-        sel = mask_positions(keep)
+        sel = self.ops.select(keep)
         upos, uidx, uhead = (self.ops.gather(t, sel) for t in (gpos, idx, hpos))
-        D = self._sum(count_true(head), dev)
+        D = self._sum(self.ops.count_true(head), dev)
         self.stats["rounds"] = 1
         self.stats["distinct"].append(D)
         wr = bit_width(n)
@@ -769,7 +775,7 @@ class SampleSortSA:
             q = uidx + h
             valid = q < n
             r1 = torch.zeros_like(uidx)
-            vsel = mask_positions(valid)
+            vsel = self.ops.select(valid)
             qv = self.ops.gather(q, vsel)
             (rq,), recv, order, send = self._route(owner(qv), [qv])
             (ans,), _ = self._alltoallv([self.ops.gather(rank_local, rq, lo)], recv)
@@ -778,9 +784,9 @@ class SampleSortSA:
             self.ops.scatter(r1, vsel, 0, tmp)
             # dense group id (groups are contiguous in SA order across ranks)
             ghead, _ = self._run_flags([uhead], dev)
-            gcount = count_true(ghead)
+            gcount = self.ops.count_true(ghead)
             gcounts = self._gather(torch.tensor([gcount], dtype=I64, device=dev)).reshape(-1).tolist()
-            g = cumsum_i64(ghead) + (sum(gcounts[:r]) - 1)
+            g = self.ops.cumsum(ghead) + (sum(gcounts[:r]) - 1)
             ngroups = sum(gcounts)
             wg = bit_width(max(ngroups - 1, 0))
             if wg + wr <= 63:
@@ -799,14 +805,14 @@ class SampleSortSA:
             newhead = uhead + (rstart - gstart)
             (ri, rv), _, _, _ = self._route(owner(uidx), [uidx, newhead + 1])
             self.ops.scatter(rank_local, ri, lo, rv)
-            sel = mask_positions(rsingle)
+            sel = self.ops.select(rsingle)
             fin_pos.append(self.ops.gather(pos, sel))
             fin_idx.append(self.ops.gather(uidx, sel))
             keep = ~rsingle
-            D = (n - total_u) + self._sum(count_true(rhead), dev)
+            D = (n - total_u) + self._sum(self.ops.count_true(rhead), dev)
             self.stats["rounds"] += 1
             self.stats["distinct"].append(D)
-            sel = mask_positions(keep)
+            sel = self.ops.select(keep)
             upos, uidx, uhead = (self.ops.gather(t, sel) for t in (pos, uidx, newhead))
             h *= 2
         fp = torch.cat(fin_pos)

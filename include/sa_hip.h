@@ -195,6 +195,16 @@ int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n,
 /* In-place inclusive running max of m int64 values (the group-start
  * carries of the distributed re-rank); asynchronous on `stream`. */
 int sa_running_max_i64_device(int64_t* d_v, uint64_t m, void* stream);
+/* In-place inclusive prefix sum of m int64 values; asynchronous. */
+int sa_inclusive_sum_i64_device(int64_t* d_v, uint64_t m, void* stream);
+/* d_out[i] = the number of d_sorted[0 .. m) (non-decreasing) below d_q[i]
+ * (at most d_q[i] when right != 0), for i < nq; asynchronous. */
+int sa_count_below_u64_device(const uint64_t* d_sorted, uint64_t m, const uint64_t* d_q, uint64_t nq, int right,
+                              int64_t* d_out, void* stream);
+/* Positions (int64, in order) of the non-zero bytes of d_mask[0 .. m) into
+ * d_out (capacity m; NULL: count only); *count = their number.
+ * Synchronises `stream`. */
+int sa_select_u8_device(const uint8_t* d_mask, uint64_t m, int64_t* d_out, uint64_t* count, void* stream);
 
 /* ---- range-partitioned multi-GPU build, per rank ------------------------
  * Replaces src/mpi/manber_myers_mpi.c:22-160 (and main_mpi.c:43-54).  Every

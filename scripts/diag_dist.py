@@ -11,7 +11,7 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 from hpc_suffix_array_amd import distributed as D  # noqa: E402
-from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, bit_width, choose_chars, mask_positions  # noqa: E402
+from hpc_suffix_array_amd.distributed import DistributedSA, HipOps, bit_width, choose_chars  # noqa: E402
 
 
 def say(*a):
@@ -53,7 +53,7 @@ def main():
     head, single = d._run_flags([ks], dev)
     say("heads", int(head.sum()), "singles", int(single.sum()))
     keep = ~single
-    sel = mask_positions(keep)
+    sel = ops.select(keep)
     say("unsorted", sel.numel())
     gpos = torch.arange(n, dtype=torch.int64, device=dev)
     hpos = d._carry_start(head, gpos, dev)

@@ -2,7 +2,9 @@
 driver (hpc_suffix_array_amd/distributed.py) run under gloo on CPU so its
 exchange logic is tested without a GPU.  Mirrors the three local operations
 of libsa_hip the driver calls: sa_alphabet_device, sa_pack_keys_device,
-sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device, sa_gather_u64_device, sa_running_max_i64_device."""
+sa_sort_pairs_device (stable sort by key), sa_scatter_u64_device,
+sa_gather_u64_device, sa_running_max_i64_device, sa_inclusive_sum_i64_device,
+sa_count_below_u64_device and sa_select_u8_device."""
 import torch
 
 I64 = torch.int64
@@ -44,6 +46,18 @@ class CpuOps:
 
     def running_max(self, v):
         return torch.cummax(v, 0)[0] if v.numel() else v.clone()
+
+    def count_below(self, sorted_x, q, right=False):
+        return torch.searchsorted(sorted_x, q, right=right)
+
+    def cumsum(self, x):
+        return torch.cumsum(x.to(I64), 0)
+
+    def select(self, mask):
+        return mask.nonzero().squeeze(1)
+
+    def count_true(self, mask):
+        return int(mask.sum())
 
 
 class CpuRangeOps:

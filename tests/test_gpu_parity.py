@@ -327,6 +327,20 @@ def test_distributed_hip_single_rank(gpu, oracle):
             v[torch.rand(m, generator=g) < 0.7] = -1
             got = hops.running_max(v.cuda()).cpu()
             assert torch.equal(got, torch.cummax(v, 0)[0]), m
+        # the sample-sort driver's scan / search / compaction kernels against torch
+        for m in (1, 63, 4096, 4097, 300_001):
+            mask = torch.rand(m, generator=g) < 0.3
+            x = torch.randint(0, 1 << 20, (m,), generator=g, dtype=torch.int64)
+            assert torch.equal(hops.select(mask.cuda()).cpu(), mask.nonzero().squeeze(1)), m
+            assert hops.count_true(mask.cuda()) == int(mask.sum()), m
+            assert torch.equal(hops.cumsum(mask.cuda()).cpu(), torch.cumsum(mask.to(torch.int64), 0)), m
+            assert torch.equal(hops.cumsum(x.cuda()).cpu(), torch.cumsum(x, 0)), m
+            xs = torch.sort(x).values
+            q = torch.randint(0, (1 << 20) + 5, (5000,), generator=g, dtype=torch.int64)
+            q[:3] = torch.tensor([0, int(xs[0]), int(xs[-1])])
+            for right in (False, True):
+                assert torch.equal(hops.count_below(xs.cuda(), q.cuda(), right=right).cpu(),
+                                   torch.searchsorted(xs, q, right=right)), (m, right)
         # owner-side scatter: in-range writes land, out-of-range ones are refused
         dst = torch.full((8,), -1, dtype=torch.int64, device="cuda")
         hops.scatter(dst, torch.tensor([12, 10], dtype=torch.int64, device="cuda"), 10,
@@ -343,6 +357,9 @@ def test_distributed_hip_single_rank(gpu, oracle):
         assert hops.argsort(e, 8)[0].numel() == 0 and hops.gather(e, e).numel() == 0
         assert hops.running_max(e).numel() == 0
         hops.scatter(e.clone(), e, 0, e)
+        eb = torch.empty(0, dtype=torch.bool, device="cuda")
+        assert hops.select(eb).numel() == 0 and hops.count_true(eb) == 0 and hops.cumsum(e).numel() == 0
+        assert hops.count_below(e, e).numel() == 0
     finally:
         dist.destroy_process_group()
 
