@@ -30,12 +30,7 @@
 #ifndef SA_LIST_BLOCK
 #define SA_LIST_BLOCK 1024
 #endif
-// ranges of the multi-GPU build: the first pass straight from the text with
-// an LDS record buffer (k_split_range) instead of records through HBM
-// (k_bucket_hist<.., 2> + k_split_list)
-#ifndef SA_RANGE_FUSED
-#define SA_RANGE_FUSED 0
-#endif
+
 #ifndef SA_SEG_BLOCK
 #define SA_SEG_BLOCK 1024
 #endif
@@ -45,7 +40,7 @@
 // pairs per lane of the second pass over packed items (SrcPk8: no spills;
 // 8 / 10 / 12: 5.50 / 5.17 / 4.90 ms at 2^30 DNA, profiles/r02_ai_ab_pk8.txt)
 #ifndef SA_ITEMS_PK
-#define SA_ITEMS_PK (SA_SEG_WHOLE ? 16 : 12)
+#define SA_ITEMS_PK 12
 #endif
 // the sorted key1 of every 2^kKeySample-th SA position is kept for the rank
 // look-ups of later rounds (lower_bound_sampled)
@@ -249,8 +244,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // G = 8: per-rank round 1 5.0 -> 4.0 ms against k_split_text filtering the
     // whole text; at G = 2 streaming the text through k_split_text is cheaper
     // than writing and reading 12-byte records for half of it)
+    // (the first pass straight from the text through an LDS record buffer,
+    // no records in HBM, was slower: G = 8 DNA 3.67 vs 3.29 ms per rank,
+    // profiles/r04_f_ab_range_fused.txt)
     const bool listed = m * 10 <= n * 3;   // G >= 4: every rank's ~n/G (balanced cuts are within a few %)
-    const bool fused_range = listed && SA_RANGE_FUSED;
     uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
     uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
     // one GPU, the whole bucket range: padded first-pass segments sized from a
@@ -289,7 +286,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         else if (pow2) SA_HIST(true, 0, wgcnt);
         else if (listed) SA_HIST(false, 1, wgcnt);
         else SA_HIST(false, 0, wgcnt);
-        if (listed && !fused_range) {
+        if (listed) {
             hipLaunchKernelGGL(k_exscan_u32, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)wgcnt, wgoff, g);
             if (pow2) SA_HIST(true, 2, wgoff);
             else SA_HIST(false, 2, wgoff);
@@ -297,7 +294,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_HIST
     }
     tm.end();
-    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed && !fused_range ? 12 * m : 0));
+    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? 12 * m : 0));
     // second-pass digit bits (7..10): bb - kLoBits on one GPU
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
@@ -344,21 +341,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib, \
                        stripes)
-        if (fused_range) {
-            const uint32_t gr = (uint32_t)std::max<uint64_t>(
-                1, std::min<uint64_t>((n + kRgTile - 1) / kRgTile, (uint64_t)c->cus));
-            const bool ident = bp.bs.sigma == 256;
-#define SA_RANGE(P, PK, ID)                                                                                   \
-    hipLaunchKernelGGL((k_split_range<P, PK, ID>), dim3(gr), dim3(kRgBlock), 0, s, d_text, n,                \
-                       (const uint16_t*)c->code, bp.bs, (const uint32_t*)os_base(c), c->keys[0], c->vals_alt, g_hi, \
-                       cursor, m, blo, bhi, hb, bp.ib, c->words + 4)
-            if (pk8 && ident) SA_RANGE(true, true, true);
-            else if (pk8) SA_RANGE(true, true, false);
-            else if (pow2 && ident) SA_RANGE(true, false, true);
-            else if (pow2) SA_RANGE(true, false, false);
-            else SA_RANGE(false, false, false);
-#undef SA_RANGE
-        } else if (listed) {
+        if (listed) {
             constexpr int kItemsL = SA_ITEMS_B, kListBlock = SA_LIST_BLOCK;
             const uint64_t tl = (uint64_t)kListBlock * kItemsL;
             const uint32_t gl = (uint32_t)std::max<uint64_t>(
@@ -381,7 +364,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_TEXT_PASS
     }
     tm.end();
-    add_bytes(st, SA_K_SCATTER_FIRST, listed && !fused_range ? (pk8 ? 20 : 24) * m : n + (pk8 ? 8 : 12) * m);
+    add_bytes(st, SA_K_SCATTER_FIRST, listed ? (pk8 ? 20 : 24) * m : n + (pk8 ? 8 : 12) * m);
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
@@ -411,7 +394,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             1, std::min<uint64_t>(units, (uint64_t)c->cus * (kSpBlock / sblk)));
         switch (hb) {
 #define SA_SEG_LAUNCH(S, B, SRC, SH, IT)                                                                      \
-    hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock), S::kPk8 && SA_SEG_WHOLE>), dim3(grid), \
+    hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock)>), dim3(grid),                    \
                        dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                                  \
                        (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,          \
                        c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr, \

@@ -767,268 +767,6 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
 }
 
 // ---------------------------------------------------------------------------
-// The first bucket pass of one rank's bucket range straight from the text,
-// without records in HBM: the record pass (k_bucket_hist<.., 2>) wrote
-// 12 bytes per kept suffix and k_split_list read them back -- at G = 8,
-// 1.6 GB of 1 GiB DNA and 12.9 GB of configs[3]'s 4 GiB byte256 per rank.
-// Here each workgroup streams 4096-position text tiles (4 positions per
-// lane: digits staged in LDS, D rolled, the bucket tested against the range)
-// and appends the kept suffixes' (key1, position) to an LDS buffer of kRgCap
-// records; a full buffer is flushed as one first-pass tile: ranked by the
-// low kLoBits of the local bucket (LDS atomics), places claimed from the
-// per-digit cursors, staged digit-sorted and written as runs (PK8: packed
-// 8-byte items, as k_split_list<.., PK8>).  The digit totals of the bases come
-// from the count pass (k_bucket_hist<.., 1>), the second pass's from here.
-// IDENT: sigma = 256 (every byte value present): the dense digit is the byte
-// itself, no LDS byte map.
-// ---------------------------------------------------------------------------
-constexpr int kRgBlock = 1024;
-constexpr int kRgPer = 16;                         // text positions per lane and tile (one 16-byte load)
-constexpr int kRgTile = kRgBlock * kRgPer;         // 16384
-constexpr int kRgCap = 8192;                       // LDS records per flushed tile
-constexpr int kRgItems = kRgCap / kRgBlock;        // 8 per lane at a flush
-
-template <int WAVES>
-__device__ __forceinline__ uint32_t block_exclusive_sum_w(uint32_t x, uint32_t* s_tmp, uint32_t* total) {
-    const uint32_t inc = wave_inclusive_sum(x);
-    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
-    __syncthreads();
-    uint32_t off = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < WAVES; ++w) {
-        const uint32_t v = s_tmp[w];
-        off += (w < (int)wave_id()) ? v : 0u;
-        tot += v;
-    }
-    __syncthreads();
-    if (total) *total = tot;
-    return off + inc - x;
-}
-
-template <bool POW2, bool PK8, bool IDENT>
-__global__ __launch_bounds__(kRgBlock) void k_split_range(const uint8_t* __restrict__ text, uint64_t n,
-                                                          const uint16_t* __restrict__ code, BucketSpec b,
-                                                          const uint32_t* __restrict__ digit_base,
-                                                          uint64_t* __restrict__ out_keys,
-                                                          uint32_t* __restrict__ out_vals,
-                                                          uint32_t* __restrict__ ghist_hi,
-                                                          uint32_t* __restrict__ cursor, uint64_t m, uint32_t blo,
-                                                          uint32_t bhi, uint32_t pk_hb, uint32_t pk_ib,
-                                                          uint32_t* __restrict__ err) {
-    constexpr int RADIX = kLoRadix;
-    constexpr int WAVES = kRgBlock / kWave;
-    constexpr int NW = (kRgTile + kMaxK) / 4;   // staged digit words (tile + halo)
-    static_assert(!PK8 || POW2, "packed items need a power-of-two alphabet");
-    static_assert(kRgTile / 2 <= kRgCap, "half a tile's kept suffixes fit an emptied buffer");
-    __shared__ uint64_t s_rk[kRgCap];   // key1 (flush: digit-sorted items)
-    __shared__ uint32_t s_rp[kRgCap];   // position (flush, PK8: the item's digit)
-    __shared__ __attribute__((aligned(16))) uint32_t s_dcw[NW + 8];
-    __shared__ uint8_t s_map[256];
-    __shared__ uint32_t s_cnt[RADIX];
-    __shared__ uint32_t s_start[RADIX];
-    __shared__ uint32_t s_gofs[RADIX];
-    __shared__ uint32_t s_hhi[1024];
-    __shared__ uint32_t s_tmp[WAVES];
-    const uint8_t* s_dc = reinterpret_cast<const uint8_t*>(s_dcw);
-    const uint32_t tid = threadIdx.x;
-    const uint32_t bspan = bhi - blo;
-    const uint32_t K = b.s + b.R;
-    const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(b.sigma) : 0u;
-    const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
-    const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;
-    const uint32_t kbsh = b.rb + (POW2 ? lg * b.s - b.bb : 0u);   // key1 >> kbsh = its bucket (POW2)
-    const uint64_t remmask = (1ull << kbsh) - 1ull;
-    for (uint32_t i = tid; i < 1024u; i += kRgBlock) s_hhi[i] = 0;
-    if (tid < (uint32_t)RADIX) s_cnt[tid] = 0;
-    if (tid < 256u) {
-        const uint32_t cv = code[tid];
-        s_map[tid] = (uint8_t)(cv ? cv - 1u : 0u);
-    }
-    __syncthreads();
-    auto load4 = [&](uint64_t pos) -> uint32_t {
-        if (pos + 4 <= n && (((uintptr_t)(text + pos)) & 3) == 0) return *reinterpret_cast<const uint32_t*>(text + pos);
-        uint32_t w = 0;
-        for (int q = 0; q < 4; ++q)
-            if (pos + q < n) w |= (uint32_t)text[pos + q] << (8 * q);
-        return w;
-    };
-    auto digits = [&](uint32_t raw, uint64_t pos) -> uint32_t {   // 4 bytes -> 4 dense digits (0 past n)
-        uint32_t o;
-        if (IDENT) o = raw;
-        else
-            o = (uint32_t)s_map[raw & 0xFFu] | ((uint32_t)s_map[(raw >> 8) & 0xFFu] << 8) |
-                ((uint32_t)s_map[(raw >> 16) & 0xFFu] << 16) | ((uint32_t)s_map[raw >> 24] << 24);
-        if (pos + 4 > n) {
-            for (int q = 0; q < 4; ++q)
-                if (pos + q >= n) o &= ~(0xFFu << (8 * q));
-        }
-        return o;
-    };
-    const uint64_t tiles = (n + kRgTile - 1) / kRgTile;
-    uint32_t count = 0;   // records in the buffer (uniform)
-    // one flushed tile: rank by the low digit, claim, stage sorted, write
-    auto flush = [&]() {
-        uint64_t fk[kRgItems] = {};
-        uint32_t fp[kRgItems] = {}, fr[kRgItems];
-#pragma unroll
-        for (int j = 0; j < kRgItems; ++j) {
-            const uint32_t q = j * kRgBlock + tid;
-            fr[j] = (uint32_t)RADIX << 16;
-            if (q < count) {
-                fk[j] = s_rk[q];
-                fp[j] = s_rp[q];
-                const uint32_t bk = POW2 ? (uint32_t)(fk[j] >> kbsh) : bucket_of(fk[j], b.rb, b.cmul, b.bsh);
-                const uint32_t lb = bk - blo;
-                const uint32_t d = lb & (RADIX - 1);
-                fr[j] = (d << 16) | atomicAdd(&s_cnt[d], 1u);
-                atomicAdd(&s_hhi[lb >> kLoBits], 1u);
-            }
-        }
-        __syncthreads();
-        uint32_t tc = 0;
-        if (tid < (uint32_t)RADIX) {
-            tc = s_cnt[tid];
-            s_cnt[tid] = 0;
-            s_gofs[tid] = digit_base[tid] + (tc ? atomicAdd(&cursor[tid], tc) : 0u);
-        }
-        const uint32_t st = block_exclusive_sum_w<WAVES>(tid < (uint32_t)RADIX ? tc : 0u, s_tmp, nullptr);
-        if (tid < (uint32_t)RADIX) s_start[tid] = st;
-        __syncthreads();
-#pragma unroll
-        for (int j = 0; j < kRgItems; ++j) {
-            const uint32_t d = fr[j] >> 16;
-            if (d < (uint32_t)RADIX) {
-                const uint32_t q = s_start[d] + (fr[j] & 0xFFFFu);
-                if constexpr (PK8) {
-                    const uint32_t hi = ((uint32_t)(fk[j] >> kbsh) - blo) >> kLoBits;
-                    s_rk[q] = ((uint64_t)hi << (64u - pk_hb)) | ((fk[j] & remmask) << pk_ib) | fp[j];
-                    s_rp[q] = d;
-                } else {
-                    s_rk[q] = fk[j];
-                    s_rp[q] = fp[j];
-                }
-            }
-        }
-        __syncthreads();
-        bool over = false;
-#pragma unroll
-        for (int j = 0; j < kRgItems; ++j) {
-            const uint32_t q = j * kRgBlock + tid;
-            if (q < count) {
-                const uint64_t key = s_rk[q];
-                const uint32_t dd =
-                    PK8 ? s_rp[q]
-                        : ((POW2 ? (uint32_t)(key >> kbsh) : bucket_of(key, b.rb, b.cmul, b.bsh)) - blo) & (RADIX - 1);
-                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                if (g < m) {
-                    out_keys[g] = key;
-                    if constexpr (!PK8) out_vals[g] = s_rp[q];
-                } else {
-                    over = true;
-                }
-            }
-        }
-        if (over) atomicOr(err, 1u);
-        __syncthreads();
-        count = 0;
-    };
-    // this lane's 16 text bytes of tile t (+ the 64-byte halo in lanes < 4),
-    // two tiles ahead: 32 KiB of loads in flight per workgroup
-    auto fetch = [&](uint64_t t, uint4& v, uint4& hv) {
-        const uint64_t tb = t * kRgTile;
-        auto ld16 = [&](uint64_t pos) -> uint4 {
-            if (pos + 16 <= n && (((uintptr_t)(text + pos)) & 15) == 0) return *reinterpret_cast<const uint4*>(text + pos);
-            return make_uint4(load4(pos), load4(pos + 4), load4(pos + 8), load4(pos + 12));
-        };
-        v = ld16(tb + 16ull * tid);
-        hv = tid < (uint32_t)(kMaxK / 16) ? ld16(tb + kRgTile + 16ull * tid) : make_uint4(0u, 0u, 0u, 0u);
-    };
-    uint4 r0 = make_uint4(0u, 0u, 0u, 0u), h0 = r0, r1 = r0, h1 = r0;
-    uint64_t t = blockIdx.x;
-    if (t < tiles) fetch(t, r0, h0);
-    if (t + gridDim.x < tiles) fetch(t + gridDim.x, r1, h1);
-    // append the kept positions of `kp` (bit j: position l0 + j) at count +
-    // their block offset, then key1 of the new records, one thread per record
-    // (kept positions are ~1 / G of the text: the loop over a lane's own
-    // kept positions ran as many iterations as the wave's busiest lane)
-    auto append = [&](uint32_t kp, uint32_t l0, uint32_t off, uint32_t tot, uint64_t tb) {
-        uint32_t o = count + off;
-        while (kp) {
-            const uint32_t j = (uint32_t)__builtin_ctz(kp);
-            kp &= kp - 1u;
-            s_rp[o++] = l0 + j;   // tile offset until key1 is filled in
-        }
-        __syncthreads();
-        for (uint32_t q = count + tid; q < count + tot; q += kRgBlock) {
-            const uint32_t l = s_rp[q];
-            uint32_t Dk = 0;
-            uint64_t r = 0;
-            for (uint32_t x = 0; x < b.s; ++x) Dk = POW2 ? ((Dk << lg) | s_dc[l + x]) : Dk * b.sigma + s_dc[l + x];
-            for (uint32_t x = b.s; x < K; ++x) r = POW2 ? ((r << lg) | s_dc[l + x]) : r * b.sigma + s_dc[l + x];
-            s_rk[q] = ((uint64_t)Dk << b.rb) | bucket_low(b, r, n - (tb + l));
-            s_rp[q] = (uint32_t)(tb + l);
-        }
-        count += tot;
-    };
-    for (; t < tiles; t += gridDim.x) {
-        const uint64_t tb = t * kRgTile;
-        {
-            const uint64_t p = tb + 16ull * tid;
-            uint4* const s4 = reinterpret_cast<uint4*>(s_dcw);
-            s4[tid] = make_uint4(digits(r0.x, p), digits(r0.y, p + 4), digits(r0.z, p + 8), digits(r0.w, p + 12));
-            if (tid < (uint32_t)(kMaxK / 16)) {
-                const uint64_t q = tb + kRgTile + 16ull * tid;
-                s4[kRgBlock + tid] =
-                    make_uint4(digits(h0.x, q), digits(h0.y, q + 4), digits(h0.z, q + 8), digits(h0.w, q + 12));
-            }
-        }
-        r0 = r1;
-        h0 = h1;
-        {
-            const uint64_t t2 = t + 2ull * gridDim.x;
-            fetch(t2 < tiles ? t2 : t, r1, h1);   // two tiles ahead (re-reads this tile past the end)
-        }
-        __syncthreads();
-        // D of positions 16 tid .. + 15 rolled from word reads, the range test
-        const uint32_t l0 = kRgPer * tid;
-        uint32_t D = 0;
-        for (uint32_t q = 0; q < b.s; ++q) D = POW2 ? ((D << lg) | s_dc[l0 + q]) : D * b.sigma + s_dc[l0 + q];
-        uint32_t xo[kRgPer / 4], xi[kRgPer / 4];
-        lds_bytes<kRgPer>(s_dcw, l0, xo);
-        lds_bytes<kRgPer>(s_dcw, l0 + b.s, xi);
-        uint32_t keep = 0;
-#pragma unroll
-        for (int j = 0; j < kRgPer; ++j) {
-            if (j > 0) {
-                if constexpr (POW2) D = ((D << lg) | byte_at<kRgPer>(xi, j - 1)) & dmask;
-                else D = (D - byte_at<kRgPer>(xo, j - 1) * (uint32_t)b.pow_s1) * b.sigma + byte_at<kRgPer>(xi, j - 1);
-            }
-            const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
-            if (bk - blo < bspan && tb + l0 + j < n) keep |= 1u << j;
-        }
-        uint32_t tot;
-        const uint32_t off = block_exclusive_sum_w<WAVES>((uint32_t)__popc(keep), s_tmp, &tot);
-        if (count + tot > (uint32_t)kRgCap) flush();   // uniform
-        if (tot <= (uint32_t)kRgCap) {
-            append(keep, l0, off, tot, tb);
-        } else {   // (uniform, a range holding most of a tile) in two halves
-            uint32_t t0;
-            const uint32_t o0 = block_exclusive_sum_w<WAVES>((uint32_t)__popc(keep & 0xFFu), s_tmp, &t0);
-            append(keep & 0xFFu, l0, o0, t0, tb);
-            __syncthreads();
-            flush();
-            uint32_t t1;
-            const uint32_t o1 = block_exclusive_sum_w<WAVES>((uint32_t)__popc(keep & ~0xFFu), s_tmp, &t1);
-            append(keep & ~0xFFu, l0, o1, t1, tb);
-        }
-        __syncthreads();   // s_dcw is restaged next, s_rk / s_rp complete
-    }
-    if (count) flush();   // uniform
-    for (uint32_t i = tid; i < 1024u; i += kRgBlock)
-        if (s_hhi[i]) atomicAdd(&ghist_hi[i], s_hhi[i]);
-}
-
-// ---------------------------------------------------------------------------
 // The second bucket pass without a look-back.  Its input is ordered by the
 // first pass's digit l (the bucket's low kLoBits): segment l of the input is
 // [lo_base[l], lo_base[l + 1]).  The pass must keep l's order only, and
@@ -1063,14 +801,12 @@ constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 // against 4.68 for this kernel, profiles/r04_b_ab_seg_late.txt -- the loads
 // must be in flight through the base wait and the staging, and larger units
 // do not make the 512-way writes faster.)
-// WHOLE (packed items): the item is staged whole and its digit read back
-// from its top bits at the store (no 16-bit digit array), which leaves the
-// LDS for 16-item lanes (16 K-item units: 32-item runs per digit and unit
-// instead of 24).
-#ifndef SA_SEG_WHOLE
-#define SA_SEG_WHOLE 0
-#endif
-template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock, bool WHOLE = false>
+// Also measured slower (profiles/r04_i_ab_seg_whole.txt): whole packed items
+// staged (digit from the top bits, no s_dig) with 16 / 14 / 12 items per lane
+// and the next unit's loads split around the staging: 5.72 / 4.94 / 4.89 ms
+// against 4.68-4.95 -- although 32-item runs write faster than 24-item ones
+// in isolation (microbench_runs.hip, profiles/r04_e_microbench_runs.txt).
+template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint64_t n, uint32_t shift,
                                                         const uint32_t* __restrict__ lo_base,
                                                         const uint32_t* __restrict__ digit_base,
@@ -1087,9 +823,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     static_assert(BLOCK >= RADIX && (int)kSegs <= BLOCK, "one thread per digit / segment");
     static_assert((int)(kSegs * kMaxStripes) <= 2 * BLOCK, "two sub-segments per thread in the unit numbering");
     static_assert(TILE <= 65535, "16-bit tile offsets");
-    static_assert(!WHOLE || Src::kPk8, "whole staged items carry their digit only when packed");
-    __shared__ uint64_t s_keys[TILE];   // bucket-relative items, digit-sorted (WHOLE: whole items)
-    __shared__ uint16_t s_dig[WHOLE ? 1 : TILE];
+    __shared__ uint64_t s_keys[TILE];   // bucket-relative items, digit-sorted
+    __shared__ uint16_t s_dig[TILE];
     __shared__ uint32_t s_dmin[RADIX];  // Dmin of bucket (h, l)
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
@@ -1162,22 +897,16 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     };
     uint64_t k[ITEMS];
     uint32_t v[ITEMS];
-    // items [J0, J1) of a unit into kk / vv (indexed like the items)
-    auto load = [&](uint64_t tb, uint32_t valid, uint64_t* kk, uint32_t* vv, int J0 = 0, int J1 = ITEMS) {
+    auto load = [&](uint64_t tb, uint32_t valid, uint64_t* kk, uint32_t* vv) {
         const uint32_t last = valid - 1;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
-            if (j < J0 || j >= J1) continue;
             const uint32_t le = wave * WTILE + j * kWave + lane;
             const uint64_t e = tb + (le < last ? le : last);
             kk[j] = src.key(e);
             vv[j] = Src::kPk8 ? 0u : src.val(e);
         }
     };
-    // WHOLE: the first half of the next unit is prefetched before the
-    // staging (in flight through it), the second half after it, into the
-    // registers just staged, so that 16 items per lane fit 128 VGPRs
-    constexpr int JH = WHOLE ? ITEMS / 2 : ITEMS;
     uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
     uint32_t l = 0, valid = 0;
     uint64_t tb = 0;
@@ -1278,47 +1007,35 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         if (un < units) locate(un, ln, tbn, validn);
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
-        load(tbn, validn, kn, vn, 0, JH);
+        load(tbn, validn, kn, vn);
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                if constexpr (WHOLE) {
-                    s_keys[pos] = k[j];
-                } else {
-                    if constexpr (Src::kPk8)   // the item below its digit (shift = 64 - hb)
-                        s_keys[pos] = k[j] & ((1ull << shift) - 1ull);
-                    else
-                        s_keys[pos] = ((k[j] - ((uint64_t)s_dmin[d] << src.rb)) << ib) | v[j];
-                    s_dig[pos] = (uint16_t)d;
-                }
+                if constexpr (Src::kPk8)   // the item below its digit (shift = 64 - hb)
+                    s_keys[pos] = k[j] & ((1ull << shift) - 1ull);
+                else
+                    s_keys[pos] = ((k[j] - ((uint64_t)s_dmin[d] << src.rb)) << ib) | v[j];
+                s_dig[pos] = (uint16_t)d;
             }
         }
         __syncthreads();
         SEG_STAMP(4)
-        if constexpr (WHOLE) load(tbn, validn, k, v, JH, ITEMS);
         if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
-#pragma unroll (WHOLE ? 4 : ITEMS)
+#pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t q = j * BLOCK + dg;
             if (q < valid) {
-                if constexpr (WHOLE) {
-                    const uint64_t w = s_keys[q];
-                    const uint32_t dd = (uint32_t)(w >> shift);
-                    const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                    if (g < n) out_w[g] = w & ((1ull << shift) - 1ull);
-                } else {
-                    const uint32_t dd = s_dig[q];
-                    const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                    if (g < n) out_w[g] = s_keys[q];
-                }
+                const uint32_t dd = s_dig[q];
+                const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
+                if (g < n) out_w[g] = s_keys[q];
             }
         }
         __syncthreads();
         SEG_STAMP(5)
 #pragma unroll
-        for (int j = 0; j < JH; ++j) {
+        for (int j = 0; j < ITEMS; ++j) {
             k[j] = kn[j];
             v[j] = vn[j];
         }
