@@ -165,7 +165,10 @@ constexpr uint32_t kCoarse = 1u << kCoarseBits;
 // writes each workgroup's records from its offset (no claims: a claim per
 // 4096-position tile on one counter serialised; LM = 1 keeps the plain
 // histogram's occupancy).
-template <bool POW2 = false, bool COARSE = false, int LM = 0>
+// IDENT: sigma = 256 (every byte value present), so the dense digit is the
+// byte itself: no LDS byte map (configs[3]'s byte256 text: each rank scans
+// the whole 4 GiB text twice)
+template <bool POW2 = false, bool COARSE = false, int LM = 0, bool IDENT = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
                                                         uint32_t* __restrict__ ghist, uint64_t p0, uint64_t p1,
@@ -226,12 +229,14 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 w[1] = v.y;
                 w[2] = v.z;
                 w[3] = v.w;
+                if constexpr (!IDENT) {
 #pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    uint32_t o = 0;
+                    for (int q = 0; q < 4; ++q) {
+                        uint32_t o = 0;
 #pragma unroll
-                    for (int y = 0; y < 4; ++y) o |= (uint32_t)s_map[(w[q] >> (8 * y)) & 0xFFu] << (8 * y);
-                    w[q] = o;
+                        for (int y = 0; y < 4; ++y) o |= (uint32_t)s_map[(w[q] >> (8 * y)) & 0xFFu] << (8 * y);
+                        w[q] = o;
+                    }
                 }
             } else {
 #pragma unroll
@@ -247,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
             *reinterpret_cast<uint4*>(s_dc + threadIdx.x * RUN) = make_uint4(w[0], w[1], w[2], w[3]);
             if (threadIdx.x < (uint32_t)kMaxK) {
                 const uint64_t h = tb + kTile + threadIdx.x;
-                s_dc[kTile + threadIdx.x] = (h < n) ? s_map[chv] : (uint8_t)0;
+                s_dc[kTile + threadIdx.x] = (h < n) ? (IDENT ? (uint8_t)chv : s_map[chv]) : (uint8_t)0;
             }
         }
         cv = nv;
@@ -1432,7 +1437,7 @@ __device__ __forceinline__ uint32_t slot0() {
     return (t / kWave) * (kWave * ITEMS) + (t & (kWave - 1));
 }
 
-constexpr uint32_t kSlotBits = 14;
+constexpr uint32_t kSlotBits = kBsCap > (1 << 14) ? 15 : 14;   // load slots of a window
 constexpr uint32_t kSlotMask = (1u << kSlotBits) - 1u;
 constexpr uint32_t kLowMax = 32 - kSlotBits;   // key bits below the sub-bucket
 static_assert(kBsCap <= (1 << kSlotBits), "load slots in kSlotBits");

@@ -384,7 +384,10 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
         if (hi > lo) {
             const uint64_t tiles = (hi - lo + kTile - 1) / kTile;
             const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(tiles, (uint64_t)SA_COARSE_WPC * (uint32_t)c->cus));
-            if ((sigma & (sigma - 1)) == 0)
+            if (sigma == 256)
+                hipLaunchKernelGGL((k_bucket_hist<true, true, 0, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,
+                                   (const uint16_t*)c->code, bp.bs, (uint32_t*)d_coarse, lo, hi, 0u, 1u << bp.bs.bb);
+            else if ((sigma & (sigma - 1)) == 0)
                 hipLaunchKernelGGL((k_bucket_hist<true, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,
                                    (const uint16_t*)c->code, bp.bs, (uint32_t*)d_coarse, lo, hi, 0u, 1u << bp.bs.bb);
             else

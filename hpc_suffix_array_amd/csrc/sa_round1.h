@@ -282,16 +282,23 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #define SA_HIST(P, L, W)                                                                                      \
     hipLaunchKernelGGL((k_bucket_hist<P, false, L>), dim3(g), dim3(kBlock), 0, s, d_text, n,                  \
                        (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
-        if (pow2 && listed) SA_HIST(true, 1, wgcnt);
+#define SA_HIST_ID(L, W)                                                                                      \
+    hipLaunchKernelGGL((k_bucket_hist<true, false, L, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,         \
+                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
+        const bool ident = bp.bs.sigma == 256;
+        if (ident && listed) SA_HIST_ID(1, wgcnt);
+        else if (pow2 && listed) SA_HIST(true, 1, wgcnt);
         else if (pow2) SA_HIST(true, 0, wgcnt);
         else if (listed) SA_HIST(false, 1, wgcnt);
         else SA_HIST(false, 0, wgcnt);
         if (listed) {
             hipLaunchKernelGGL(k_exscan_u32, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)wgcnt, wgoff, g);
-            if (pow2) SA_HIST(true, 2, wgoff);
+            if (ident) SA_HIST_ID(2, wgoff);
+            else if (pow2) SA_HIST(true, 2, wgoff);
             else SA_HIST(false, 2, wgoff);
         }
 #undef SA_HIST
+#undef SA_HIST_ID
     }
     tm.end();
     add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? 12 * m : 0));
