@@ -318,6 +318,12 @@ def run_single(a, torch, dev, world, rank, barrier):
         "kernels_gbs": per_kernel,
         "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
         "reference_schedule": ref_sched,
+        # the packed schedule's round 1 covers the reference's rounds h = 1 ..
+        # K/2 at once, so its ms_per_round are not per doubling: the build's
+        # time over the reference's own round count for this text
+        # (manber_myers.c:97-125, the companion schedule's rounds)
+        "ms_per_reference_round": (round(1e3 * elapsed / a.steps / ref_sched["rounds"], 3)
+                                   if ref_sched and ref_sched.get("rounds") else None),
     }
     b.close()
     return elapsed, extra

@@ -1537,6 +1537,11 @@ __device__ __forceinline__ void load_items(const uint64_t* __restrict__ w_in, ui
 }
 
 // bits: the plan's key span (br.bits1), kSubBits < bits <= kSubBits + kLowMax
+// SA_LS_WFULL: waves whose slots all lie inside the window take the
+// histogram, scatter and store loops without per-item bounds tests
+#ifndef SA_LS_WFULL
+#define SA_LS_WFULL 1
+#endif
 template <int BLOCK, int ITEMS, class Probe = NoProbe>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
@@ -1598,11 +1603,20 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         probe.mark(0);
         const uint32_t l0 = slot0<ITEMS>();
         // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
+        const bool wfull = SA_LS_WFULL && (wave + 1) * (uint32_t)(kWave * ITEMS) <= m;   // uniform per wave
+        if (wfull) {
 #pragma unroll
-        for (int i = 0; i < ITEMS; ++i) {
-            if (l0 + i * kWave < m) {
+            for (int i = 0; i < ITEMS; ++i) {
                 const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
                 atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+            }
+        } else {
+#pragma unroll
+            for (int i = 0; i < ITEMS; ++i) {
+                if (l0 + i * kWave < m) {
+                    const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                    atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                }
             }
         }
         __syncthreads();
@@ -1655,14 +1669,20 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         } else {
             // 2. scatter the 32-bit words into sub-buckets (any order inside
             // one); the indices stay by load slot
+            auto scatter1 = [&](int i, uint32_t le) {
+                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
+                const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                s_k[(old >> (16 * (sb & 1))) & 0xFFFFu] = (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
+                s_x[le] = (uint32_t)(w[i] & imask);
+            };
+            if (wfull) {
 #pragma unroll
-            for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t le = l0 + i * kWave;
-                if (le < m) {
-                    const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                    const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
-                    s_k[(old >> (16 * (sb & 1))) & 0xFFFFu] = (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
-                    s_x[le] = (uint32_t)(w[i] & imask);
+                for (int i = 0; i < ITEMS; ++i) scatter1(i, l0 + i * kWave);
+            } else {
+#pragma unroll
+                for (int i = 0; i < ITEMS; ++i) {
+                    const uint32_t le = l0 + i * kWave;
+                    if (le < m) scatter1(i, le);
                 }
             }
             // ... the window is in LDS: the next window's loads go out now (a
@@ -1770,10 +1790,18 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             probe.mark(5);
             // 4. the SA, coalesced: the index of each sorted word's load slot
             // (the U / G scan's barrier follows every thread's sort)
+            if (wfull) {
 #pragma unroll 2
-            for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t le = l0 + i * kWave;
-                if (le < m) sa_out[a + le] = s_x[s_k[le] & kSlotMask];
+                for (int i = 0; i < ITEMS; ++i) {
+                    const uint32_t le = l0 + i * kWave;
+                    sa_out[a + le] = s_x[s_k[le] & kSlotMask];
+                }
+            } else {
+#pragma unroll 2
+                for (int i = 0; i < ITEMS; ++i) {
+                    const uint32_t le = l0 + i * kWave;
+                    if (le < m) sa_out[a + le] = s_x[s_k[le] & kSlotMask];
+                }
             }
             __syncthreads();   // s_k / s_x / s_cnt reuse by the next window
             probe.mark(6);

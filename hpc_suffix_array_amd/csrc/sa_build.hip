@@ -149,6 +149,7 @@ struct sa_context {
     uint32_t dbg = 0;
     int32_t span_extra = 0;
     int32_t tune = 0;
+    bool dna = false;   // the text's alphabet is exactly {A, C, G, T} (k_split_text<.., DNA>)
 };
 
 namespace sa {
@@ -998,6 +999,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
+    c->dna = sigma == 4 && h_code['A'] && h_code['C'] && h_code['G'] && h_code['T'];
     uint32_t K = choose_chars(sigma, n, opts ? opts->init_chars : 0);
     const uint64_t base = (uint64_t)sigma + 1;
     const Chunking ch = plan_chunks(n);

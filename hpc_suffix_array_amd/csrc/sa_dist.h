@@ -336,6 +336,7 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     uint16_t* h_code = reinterpret_cast<uint16_t*>(c->host_words + 320);
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((present[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
+    c->dna = sigma == 4 && h_code['A'] && h_code['C'] && h_code['G'] && h_code['T'];
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
     // the text's tail (every rank holds the text: all take the same layout)
     const uint32_t tail_n = (uint32_t)std::min<uint64_t>(n, (uint64_t)kMaxK);

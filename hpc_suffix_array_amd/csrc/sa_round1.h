@@ -337,13 +337,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         // at 512, alnum 5.13 vs 4.90: profiles/r02_bc_ab_text_block_kinds.txt)
         constexpr int kTextBlock = SA_TEXT_BLOCK;
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
+        const bool dna = SA_DNA_SWAR && c->dna;
         auto text_grid = [&](int block) {
             const uint64_t tile = (uint64_t)block * kItemsA;
             return (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>((n + tile - 1) / tile, (uint64_t)c->cus * (kSpBlock / block)));
         };
-#define SA_TEXT_PASS(P, PK, BLK)                                                                              \
-    hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n,  \
+#define SA_TEXT_PASS(P, PK, BLK, DNA)                                                                         \
+    hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK, DNA>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n, \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib, \
@@ -361,12 +362,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                 hipLaunchKernelGGL((k_split_list<kItemsL, kListBlock, false>), dim3(gl), dim3(kListBlock), 0, s, bp.bs,
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u);
+        } else if (pk8 && dna) {
+            SA_TEXT_PASS(true, true, kTextBlock, true);
         } else if (pk8) {
-            SA_TEXT_PASS(true, true, kTextBlock);
+            SA_TEXT_PASS(true, true, kTextBlock, false);
         } else if (pow2) {
-            SA_TEXT_PASS(true, false, kTextBlock);
+            SA_TEXT_PASS(true, false, kTextBlock, false);
         } else {
-            SA_TEXT_PASS(false, false, kSpBlock);
+            SA_TEXT_PASS(false, false, kSpBlock, false);
         }
 #undef SA_TEXT_PASS
     }

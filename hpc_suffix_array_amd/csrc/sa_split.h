@@ -348,7 +348,20 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // bucket and low) and the position in the low ib bits, so the pass writes 8
 // bytes per suffix instead of 12 (key1 + position) and the second pass reads
 // 8 (SrcPk8).  Needs hb + (lg sigma^s - bb + rb) + ib <= 64 (plan_pk8).
-template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false>
+// DNA: the text's alphabet is exactly {A, C, G, T}; their dense digits
+// 0..3 are ((b >> 1) ^ (b >> 2)) & 3 of the byte b (0x41 0x43 0x47 0x54 ->
+// 0 1 2 3), four bytes of a word at once, instead of four LDS byte-map reads
+#ifndef SA_DNA_SWAR
+#define SA_DNA_SWAR 1
+#endif
+// SA_TEXT_FULL: whole tiles of the whole bucket range take the key loop
+// without per-item tests (its LDS atomics unpredicated): 3.54 -> 3.27-3.37
+// ms at 1 GiB DNA; the staging and write loops alone made no difference
+// (profiles/r04_n_ab_full_tiles.txt)
+#ifndef SA_TEXT_FULL
+#define SA_TEXT_FULL 1
+#endif
+template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false, bool DNA = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -459,8 +472,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             if (w < (uint32_t)NW) {
                 uint32_t o = 0;
                 if (whole) {
-                    o = (uint32_t)s_map[raw[i] & 0xFFu] | ((uint32_t)s_map[(raw[i] >> 8) & 0xFFu] << 8) |
-                        ((uint32_t)s_map[(raw[i] >> 16) & 0xFFu] << 16) | ((uint32_t)s_map[raw[i] >> 24] << 24);
+                    if constexpr (DNA)
+                        o = ((raw[i] >> 1) ^ (raw[i] >> 2)) & 0x03030303u;
+                    else
+                        o = (uint32_t)s_map[raw[i] & 0xFFu] | ((uint32_t)s_map[(raw[i] >> 8) & 0xFFu] << 8) |
+                            ((uint32_t)s_map[(raw[i] >> 16) & 0xFFu] << 16) | ((uint32_t)s_map[raw[i] >> 24] << 24);
                 } else {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
@@ -479,6 +495,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         TEXT_STAMP(0)
         // key1 of positions tb + ITEMS dg + j (D < 64 sigma 2^bb <= 2^32 rolls
         // in 32 bits; the remainder in 64)
+        const bool full = SA_TEXT_FULL && valid == (uint32_t)TILE && blo == 0 && bspan == (1u << b.bb);   // uniform
         uint64_t k[ITEMS];
         uint32_t dr[ITEMS];
         {
@@ -506,6 +523,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             lds_bytes<ITEMS>(s_dcw, l0, xo);
             lds_bytes<ITEMS>(s_dcw, l0 + b.s, xm);
             lds_bytes<ITEMS>(s_dcw, l0 + K, xn);
+            // FULL: a whole tile of the whole bucket range, every position
+            // kept (no per-item tests)
+            auto keyloop = [&](auto fullc) {
+            constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
                 if (j > 0) {
@@ -523,11 +544,20 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 const uint32_t lb = bk - blo;
-                const bool ok = l0 + j < valid && lb < bspan;
-                const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
-                dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
-                if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
+                if constexpr (FULL) {
+                    const uint32_t d = lb & (RADIX - 1);
+                    dr[j] = (d << 16) | atomicAdd(&s_cnt[d], 1u);
+                    atomicAdd(&s_hhi[lb >> kLoBits], 1u);
+                } else {
+                    const bool ok = l0 + j < valid && lb < bspan;
+                    const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
+                    dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
+                    if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
+                }
             }
+            };
+            if (full) keyloop(std::true_type{});
+            else keyloop(std::false_type{});
         }
         __syncthreads();
         TEXT_STAMP(1)
@@ -932,6 +962,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         // claims (read after the claims' barrier)
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         // ranks within the unit (any order: one segment, one value of l)
+        // (full units without per-item bounds tests: no faster,
+        // profiles/r04_n_ab_full_tiles.txt)
         uint32_t dr[ITEMS];
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
