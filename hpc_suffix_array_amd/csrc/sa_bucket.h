@@ -269,25 +269,31 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         lds_bytes<RUN>(s_dcw, l0, xo);
         lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
         uint32_t keep = 0;   // LIST: bit j = position l0 + j is in the range
+        // whole tiles inside [p0, p1) take the loop without the position test
+        auto count = [&](auto wholec) {
+            constexpr bool WHOLE = decltype(wholec)::value;
 #pragma unroll
-        for (int j = 0; j < RUN; ++j) {
-            if (j > 0) {
-                if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
-                else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
-            }
-            if (tb + l0 + j < p1) {
-                const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
-                if constexpr (COARSE) {
-                    atomicAdd(&s_hlo[bk >> cshift], 1u);
-                } else {
-                    const uint32_t lb = bk - blo;
-                    if (lb < bspan) {
-                        if (LM != 2) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
-                        keep |= 1u << j;
+            for (int j = 0; j < RUN; ++j) {
+                if (j > 0) {
+                    if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
+                    else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
+                }
+                if (WHOLE || tb + l0 + j < p1) {
+                    const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
+                    if constexpr (COARSE) {
+                        atomicAdd(&s_hlo[bk >> cshift], 1u);
+                    } else {
+                        const uint32_t lb = bk - blo;
+                        if (lb < bspan) {
+                            if (LM != 2) atomicAdd(&s_hlo[lb & (kLoRadix - 1)], 1u);
+                            keep |= 1u << j;
+                        }
                     }
                 }
             }
-        }
+        };
+        if (tb + kTile <= p1) count(std::true_type{});   // uniform
+        else count(std::false_type{});
         if (LM == 1) kept_lane += (uint32_t)__popc(keep);
         if (LM == 2) {
             // the tile's kept positions compacted into LDS in order, then one
@@ -1727,9 +1733,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 // the sorted key1 of this sub-bucket's every-2^ksh-th SA
                 // positions, from the sorted words (a global load here would
                 // make the store phase wait for the next window's loads)
-                for (uint64_t p = ((a + lo + smask) >> so.ksh) << so.ksh; p < a + hi; p += smask + 1)
-                    keys_out[p >> so.ksh] =
-                        mn + (((uint64_t)sb << low_bits) | (s_k[(uint32_t)(p - a)] >> kSlotBits));
+                // (32-bit positions: a window lies below 2^32)
+                const uint32_t a32 = (uint32_t)a, sm32 = (uint32_t)smask;
+                for (uint32_t p = ((a32 + lo + sm32) >> so.ksh) << so.ksh; p < a32 + hi; p += sm32 + 1)
+                    keys_out[p >> so.ksh] = mn + (((uint64_t)sb << low_bits) | (s_k[p - a32] >> kSlotBits));
             }
             probe.mark(4);
             // 3. U / U-group offsets (one scan of both; heads = m - U + G)

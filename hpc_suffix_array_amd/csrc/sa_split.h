@@ -495,7 +495,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         TEXT_STAMP(0)
         // key1 of positions tb + ITEMS dg + j (D < 64 sigma 2^bb <= 2^32 rolls
         // in 32 bits; the remainder in 64)
-        const bool full = SA_TEXT_FULL && valid == (uint32_t)TILE && blo == 0 && bspan == (1u << b.bb);   // uniform
+        const bool full0 = SA_TEXT_FULL && valid == (uint32_t)TILE && blo == 0 && bspan == (1u << b.bb);
         uint64_t k[ITEMS];
         uint32_t dr[ITEMS];
         {
@@ -517,6 +517,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
             }
             const bool interior = tb + TILE + K <= n;   // every suffix of the tile has >= K symbols
+            const bool full = full0 && interior;        // uniform
             // the digits leaving D (l0 ..), moving from the remainder into D
             // (l0 + s ..) and entering the remainder (l0 + K ..)
             uint32_t xo[ITEMS / 4], xm[ITEMS / 4], xn[ITEMS / 4];
@@ -539,8 +540,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                         r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
                     }
                 }
-                // (past the end L wraps: never ranked)
-                const uint64_t low = interior ? r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
+                // (past the end L wraps: never ranked; FULL tiles are interior)
+                const uint64_t low = (FULL || interior) ? r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 const uint32_t lb = bk - blo;
@@ -719,15 +720,21 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
         const uint64_t tb = t * TILE;
         const uint32_t valid = (uint32_t)((m - tb) < (uint64_t)TILE ? (m - tb) : (uint64_t)TILE);
         uint32_t dr[ITEMS];
+        // whole tiles take the ranking without per-item tests
+        auto rank = [&](auto wholec) {
+            constexpr bool WHOLE = decltype(wholec)::value;
 #pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const uint32_t le = wave * WTILE + j * kWave + lane;
-            const bool ok = le < valid;
-            const uint32_t lb = bucket_of(k[j], b.rb, b.cmul, b.bsh) - blo;
-            const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
-            dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
-            if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
-        }
+            for (int j = 0; j < ITEMS; ++j) {
+                const uint32_t le = wave * WTILE + j * kWave + lane;
+                const bool ok = WHOLE || le < valid;
+                const uint32_t lb = bucket_of(k[j], b.rb, b.cmul, b.bsh) - blo;
+                const uint32_t d = ok ? (lb & (RADIX - 1)) : (uint32_t)RADIX;
+                dr[j] = (d << 16) | (ok ? atomicAdd(&s_cnt[d], 1u) : 0u);
+                if (ok) atomicAdd(&s_hhi[lb >> kLoBits], 1u);
+            }
+        };
+        if (valid == (uint32_t)TILE) rank(std::true_type{});   // uniform
+        else rank(std::false_type{});
         __syncthreads();
         uint32_t tile_cnt = 0;
         if (dg < (uint32_t)RADIX) {
