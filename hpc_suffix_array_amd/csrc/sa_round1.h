@@ -31,6 +31,7 @@
 #define SA_LIST_BLOCK 1024
 #endif
 
+
 #ifndef SA_SEG_BLOCK
 #define SA_SEG_BLOCK 1024
 #endif
@@ -286,6 +287,9 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     hipLaunchKernelGGL((k_bucket_hist<true, false, L, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,         \
                        (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
         const bool ident = bp.bs.sigma == 256;
+        // (the records in one pass with offsets by a decoupled look-back over
+        // the 4096-position tiles was 2.3x slower: the chain over 2^18 - 2^20
+        // tiles serialises, profiles/r04_q_ab_range_lookback.txt)
         if (ident && listed) SA_HIST_ID(1, wgcnt);
         else if (pow2 && listed) SA_HIST(true, 1, wgcnt);
         else if (pow2) SA_HIST(true, 0, wgcnt);
@@ -301,7 +305,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
 #undef SA_HIST_ID
     }
     tm.end();
-    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? 12 * m : 0));
+    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? n + 12 * m : 0));
     // second-pass digit bits (7..10): bb - kLoBits on one GPU
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
