@@ -110,7 +110,8 @@ class SaStats(ctypes.Structure):
             "sparse_ranks": bool(self.sparse_ranks),
             "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed"}.get(self.round1, "lsd"),
             "largest_window": self.largest_window,
-            "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow"}.get(self.round1_segments, "exact"),
+            "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow", 3: "striped-records",
+                                4: "striped-records-overflow"}.get(self.round1_segments, "exact"),
             "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2)},
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),

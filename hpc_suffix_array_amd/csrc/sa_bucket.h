@@ -165,9 +165,21 @@ constexpr uint32_t kCoarse = 1u << kCoarseBits;
 // writes each workgroup's records from its offset (no claims: a claim per
 // 4096-position tile on one counter serialised; LM = 1 keeps the plain
 // histogram's occupancy).
+// LM = 3: one launch instead of LM = 1 + LM = 2 -- the records of a tile go
+// to one of kRecStripes regions of rcap records (stripe = workgroup mod
+// kRecStripes; the grid a multiple of it, so a stripe takes every
+// kRecStripes-th tile of the text), their place claimed per tile from the
+// stripe's cursor wg[stripe]; the low-digit histogram as LM = 1.  A stripe
+// whose records outgrow rcap sets *rovf and writes none past it (the caller
+// re-runs with LM = 1 + 2).
 // IDENT: sigma = 256 (every byte value present), so the dense digit is the
 // byte itself: no LDS byte map (configs[3]'s byte256 text: each rank scans
 // the whole 4 GiB text twice)
+constexpr uint32_t kRecStripes = 64;
+constexpr uint32_t kRecCurStride = 64;   // words between stripe cursors (atomics on one line serialise)
+// record slots of a range of m suffixes: the striped regions' 1/8 margin and
+// two tiles of slack per stripe
+constexpr uint64_t rec_capacity(uint64_t m) { return m + m / 8 + kRecStripes * (2ull * kTile + 1); }
 template <bool POW2 = false, bool COARSE = false, int LM = 0, bool IDENT = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
@@ -175,12 +187,15 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                                                         uint32_t blo, uint32_t bhi,
                                                         uint64_t* __restrict__ lkeys = nullptr,
                                                         uint32_t* __restrict__ lpos = nullptr,
-                                                        uint32_t* __restrict__ wg = nullptr) {
+                                                        uint32_t* __restrict__ wg = nullptr, uint32_t rcap = 0,
+                                                        uint32_t* __restrict__ rovf = nullptr) {
+    constexpr bool REC = LM == 2 || LM == 3;   // records written
     constexpr int RUN = kTile / kBlock;   // 16
     constexpr uint32_t NB = COARSE ? kCoarse : kLoRadix;
     __shared__ uint32_t s_tmp[kWaves];
     // LM = 2: the tile's kept positions (tile offsets), compacted
-    __shared__ uint16_t s_rp[LM == 2 ? kTile : 1];
+    __shared__ uint16_t s_rp[REC ? kTile : 1];
+    __shared__ uint32_t s_claim;
     __shared__ uint8_t s_map[256];
     __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
     uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
@@ -198,6 +213,8 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     const uint64_t tiles = (p1 - p0 + kTile - 1) / kTile;
     uint32_t kept_lane = 0;                        // LM = 1: this lane's kept positions
     uint32_t run = LM == 2 ? wg[blockIdx.x] : 0u;  // LM = 2: the workgroup's next record slot
+    const uint32_t stripe = blockIdx.x % kRecStripes;  // LM = 3
+    const uint64_t rbase = (uint64_t)stripe * rcap;
     // the next tile's 16 text bytes per lane (and the halo byte of lanes <
     // kMaxK) are loaded while the current tile is counted: clamped to the
     // last tile, unconditional (a conditional load is waited for at the join)
@@ -216,10 +233,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         const uint64_t tb = p0 + tt * kTile;
         uint4 nv;
         uint32_t nhv;
-        {
-            const uint64_t tn = tt + gridDim.x;
-            fetch(tn < tiles ? tn : tiles - 1, nv, nhv);
-        }
+        const uint64_t tn = tt + gridDim.x;
+        // LM = 3 issues the prefetch after its claim: a claim issued behind
+        // the prefetch could only be waited for together with it
+        if constexpr (LM != 3) fetch(tn < tiles ? tn : tiles - 1, nv, nhv);
         {
             const uint64_t i = tb + (uint64_t)threadIdx.x * RUN;
             uint32_t w[4];
@@ -255,8 +272,6 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 s_dc[kTile + threadIdx.x] = (h < n) ? (IDENT ? (uint8_t)chv : s_map[chv]) : (uint8_t)0;
             }
         }
-        cv = nv;
-        chv = nhv;
         __syncthreads();
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
@@ -295,18 +310,31 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         if (tb + kTile <= p1) count(std::true_type{});   // uniform
         else count(std::false_type{});
         if (LM == 1) kept_lane += (uint32_t)__popc(keep);
-        if (LM == 2) {
+        if constexpr (REC) {
             // the tile's kept positions compacted into LDS in order, then one
             // thread per record computes key1 from the staged digits (only
             // ~1/G of the positions) and writes it coalesced
             uint32_t tot;
             uint32_t off = block_exclusive_sum((uint32_t)__popc(keep), s_tmp, &tot);
+            // (the claim's round trip overlaps the compaction)
+            uint32_t clm = 0;
+            if (LM == 3 && threadIdx.x == 0 && tot) clm = atomicAdd(&wg[stripe * kRecCurStride], tot);
+            if constexpr (LM == 3) fetch(tn < tiles ? tn : tiles - 1, nv, nhv);
             while (keep) {
                 const int j = __builtin_ctz(keep);
                 keep &= keep - 1;
                 s_rp[off++] = (uint16_t)(l0 + j);
             }
+            if (LM == 3 && threadIdx.x == 0) s_claim = clm;
             __syncthreads();
+            if constexpr (LM == 3) {
+                const uint32_t cl = s_claim;
+                if (cl + tot > rcap) {   // uniform: the stripe is full
+                    if (threadIdx.x == 0) atomicOr(rovf, 1u);
+                    tot = 0;
+                }
+            }
+            const uint64_t rb = LM == 3 ? rbase + s_claim : (uint64_t)run;
             const uint32_t K = b.s + b.R;
             for (uint32_t t = threadIdx.x; t < tot; t += kBlock) {
                 const uint32_t l = s_rp[t];
@@ -314,11 +342,13 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 uint64_t r = 0;
                 for (uint32_t q = 0; q < b.s; ++q) Dk = POW2 ? ((Dk << lg) | s_dc[l + q]) : Dk * sig + s_dc[l + q];
                 for (uint32_t q = b.s; q < K; ++q) r = POW2 ? ((r << lg) | s_dc[l + q]) : r * sig + s_dc[l + q];
-                lkeys[run + t] = ((uint64_t)Dk << b.rb) | bucket_low(b, r, n - (tb + l));
-                lpos[run + t] = (uint32_t)(tb + l);
+                lkeys[rb + t] = ((uint64_t)Dk << b.rb) | bucket_low(b, r, n - (tb + l));
+                lpos[rb + t] = (uint32_t)(tb + l);
             }
-            run += tot;
+            if (LM == 2) run += tot;
         }
+        cv = nv;
+        chv = nhv;
         __syncthreads();
     }
     if (LM == 1) {

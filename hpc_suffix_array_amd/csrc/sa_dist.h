@@ -130,7 +130,7 @@ static int ensure_dist_m(sa_context* c, uint64_t m) {
     DistState* d = dist_of(c);
     int rc = ensure_capacity(c, m);
     if (rc) return rc;
-    rc = ensure_u_capacity(c, m);
+    rc = ensure_u_capacity(c, rec_capacity(m));   // round 1's striped records (sa_round1.h)
     if (rc) return rc;
     if (d->r1 && d->cap_m >= m) return SA_OK;
     hipFree(d->r1);

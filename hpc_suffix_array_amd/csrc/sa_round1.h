@@ -15,6 +15,10 @@
 #ifndef SA_HIST_WPC
 #define SA_HIST_WPC 64
 #endif
+// range builds: records in one striped scan of the text (k_bucket_hist<.., 3>)
+#ifndef SA_REC_STRIPED
+#define SA_REC_STRIPED 1
+#endif
 // Extra bucket bits over the size-based default (+1 at 2^30: windows of
 // ~4 K suffixes, local sort 7.3 -> 11.3 ms, second pass 5.9 -> 7.1 ms).
 #ifndef SA_BB_EXTRA
@@ -251,6 +255,23 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const bool listed = m * 10 <= n * 3;   // G >= 4: every rank's ~n/G (balanced cuts are within a few %)
     uint64_t* const lkeys = c->keys_u;   // m records (free until the second pass writes keys_u)
     uint32_t* const lpos = c->vals_u;    // (free until the later rounds)
+    // striped records (k_bucket_hist<.., LM = 3>): one scan of the text
+    // writes the records into kRecStripes regions of rcap, each tile's place
+    // claimed from its stripe's cursor, instead of a counting scan + an
+    // exclusive scan + a record scan; a stripe that overflows (a text whose
+    // kept suffixes cluster on every kRecStripes-th tile) re-runs the round
+    // with the counting scan.  SA_DEBUG_PAD_OVERFLOW: regions of half the
+    // expected share (tests).
+    const uint64_t rtiles = (n + kTile - 1) / kTile;
+    const uint32_t rgrid = (uint32_t)(std::min<uint64_t>(rtiles, (uint64_t)SA_HIST_WPC * (uint32_t)c->cus) /
+                                      kRecStripes * kRecStripes);
+    const uint64_t rcap64 = (c->dbg & SA_DEBUG_PAD_OVERFLOW) ? m / kRecStripes / 2 + 1
+                                                             : (m + m / 8) / kRecStripes + 2 * (uint64_t)kTile;
+    const bool striped = SA_REC_STRIPED && listed && allow_pad && !(c->dbg & SA_DEBUG_NO_PAD) &&
+                         rtiles >= 4ull * kRecStripes && rgrid >= kRecStripes && kRecStripes * rcap64 <= c->ucap;
+    const uint32_t rcap = (uint32_t)std::min<uint64_t>(rcap64, UINT32_MAX);
+    uint32_t* const rcur = c->hist;   // the stripes' cursors (the chunk histograms are free here)
+    // (the regions live in keys_u / vals_u: ucap entries, rec_capacity(m) in range builds)
     // one GPU, the whole bucket range: padded first-pass segments sized from a
     // sample instead of the exact totals (k_bucket_sample, sa_bucket.h)
     const bool padded = allow_pad && !listed && blo == 0 && bhi == (1u << bp.bs.bb) && n >= kPadMinN &&
@@ -258,7 +279,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint32_t ssh = std::max<uint32_t>(6u, bit_width(n) > 21 ? bit_width(n) - 21 : 0u);
     uint32_t* const pstart = os_base(c) + kPadStartOff;   // kLoRadix + 1 padded segment starts
     uint32_t* const dlo = os_base(c) + kPadDenseOff;      // kLoRadix dense segment starts
-    if (st) st->round1_segments = padded ? 1 : 0;
+    if (st) st->round1_segments = padded ? 1 : striped ? 3 : 0;
     tm.begin(SA_K_PACK);
     if (padded) {
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
@@ -280,22 +301,41 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
         uint32_t* const wgcnt = c->hist;       // per-workgroup kept counts, then offsets (the
         uint32_t* const wgoff = c->hist + g;   // chunk histograms are free in the bucketed round)
-#define SA_HIST(P, L, W)                                                                                      \
-    hipLaunchKernelGGL((k_bucket_hist<P, false, L>), dim3(g), dim3(kBlock), 0, s, d_text, n,                  \
-                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
-#define SA_HIST_ID(L, W)                                                                                      \
-    hipLaunchKernelGGL((k_bucket_hist<true, false, L, true>), dim3(g), dim3(kBlock), 0, s, d_text, n,         \
-                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W)
+#define SA_HIST_G(G, P, L, W)                                                                                 \
+    hipLaunchKernelGGL((k_bucket_hist<P, false, L>), dim3(G), dim3(kBlock), 0, s, d_text, n,                  \
+                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W, rcap,  \
+                       c->words + 11)
+#define SA_HIST_ID_G(G, L, W)                                                                                 \
+    hipLaunchKernelGGL((k_bucket_hist<true, false, L, true>), dim3(G), dim3(kBlock), 0, s, d_text, n,         \
+                       (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, W, rcap,  \
+                       c->words + 11)
+#define SA_HIST(P, L, W) SA_HIST_G(g, P, L, W)
+#define SA_HIST_ID(L, W) SA_HIST_ID_G(g, L, W)
         const bool ident = bp.bs.sigma == 256;
         // (the records in one pass with offsets by a decoupled look-back over
         // the 4096-position tiles was 2.3x slower: the chain over 2^18 - 2^20
         // tiles serialises, profiles/r04_q_ab_range_lookback.txt)
-        if (ident && listed) SA_HIST_ID(1, wgcnt);
+        if (striped) {
+            SA_HIP(hipMemsetAsync(rcur, 0, kRecStripes * kRecCurStride * 4, s));
+            if (ident) SA_HIST_ID_G(rgrid, 3, rcur);
+            else if (pow2) SA_HIST_G(rgrid, true, 3, rcur);
+            else SA_HIST_G(rgrid, false, 3, rcur);
+            // an overflowed stripe dropped records: stop before any pass reads them
+            SA_HIP(hipMemcpyAsync(c->host_words + 11, c->words + 11, 4, hipMemcpyDeviceToHost, s));
+            SA_HIP(hipStreamSynchronize(s));
+            if (c->host_words[11]) {
+                SA_TRACE("  bucketed round 1: a record stripe overflowed, again with the counting scan");
+                tm.end();
+                const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false);
+                if (st) st->round1_segments = 4;
+                return rc;
+            }
+        } else if (ident && listed) SA_HIST_ID(1, wgcnt);
         else if (pow2 && listed) SA_HIST(true, 1, wgcnt);
         else if (pow2) SA_HIST(true, 0, wgcnt);
         else if (listed) SA_HIST(false, 1, wgcnt);
         else SA_HIST(false, 0, wgcnt);
-        if (listed) {
+        if (listed && !striped) {
             hipLaunchKernelGGL(k_exscan_u32, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)wgcnt, wgoff, g);
             if (ident) SA_HIST_ID(2, wgoff);
             else if (pow2) SA_HIST(true, 2, wgoff);
@@ -303,9 +343,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         }
 #undef SA_HIST
 #undef SA_HIST_ID
+#undef SA_HIST_G
+#undef SA_HIST_ID_G
     }
     tm.end();
-    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (listed ? n + 12 * m : 0));
+    add_bytes(st, SA_K_PACK, padded ? (n >> ssh) * 64 : n + (striped ? 12 * m : listed ? n + 12 * m : 0));
     // second-pass digit bits (7..10): bb - kLoBits on one GPU
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
@@ -361,11 +403,13 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             if (pk8)
                 hipLaunchKernelGGL((k_split_list<kItemsL, kListBlock, true>), dim3(gl), dim3(kListBlock), 0, s, bp.bs,
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
-                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, hb, bp.ib);
+                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, hb, bp.ib,
+                                   striped ? (const uint32_t*)rcur : nullptr, rcap);
             else
                 hipLaunchKernelGGL((k_split_list<kItemsL, kListBlock, false>), dim3(gl), dim3(kListBlock), 0, s, bp.bs,
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
-                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u);
+                                   os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u,
+                                   striped ? (const uint32_t*)rcur : nullptr, rcap);
         } else if (pk8 && dna) {
             SA_TEXT_PASS(true, true, kTextBlock, true);
         } else if (pk8) {

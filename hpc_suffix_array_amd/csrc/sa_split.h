@@ -678,7 +678,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
                                                          uint32_t* __restrict__ ticket, uint64_t* __restrict__ out_keys,
                                                          uint32_t* __restrict__ out_vals,
                                                          uint32_t* __restrict__ ghist_hi, uint32_t* __restrict__ cursor,
-                                                         uint32_t pk_hb = 0, uint32_t pk_ib = 0) {
+                                                         uint32_t pk_hb = 0, uint32_t pk_ib = 0,
+                                                         const uint32_t* __restrict__ reg_cnt = nullptr,
+                                                         uint32_t reg_cap = 0) {
+    // reg_cnt (k_bucket_hist<.., LM = 3>'s records): kRecStripes regions of
+    // reg_cap records, region r holding reg_cnt[r kRecCurStride] from r reg_cap; the
+    // units are cut per region.  Else m records from 0.
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
@@ -692,20 +697,46 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_hhi[1024];   // the second pass's digit totals (local bucket >> kLoBits)
+    __shared__ uint32_t s_ubase[kRecStripes + 1];   // regions: units before region r
+    static_assert(BLOCK >= (int)kRecStripes && kRecStripes == kWave, "one wave numbers the regions");
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
-    const uint64_t tiles = (m + TILE - 1) / TILE;
     for (uint32_t i = dg; i < 1024u; i += BLOCK) s_hhi[i] = 0;
     if (dg < (uint32_t)RADIX) s_cnt[dg] = 0;
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
+    if (reg_cnt && wave == 0) {
+        const uint32_t c = min(reg_cnt[lane * kRecCurStride], reg_cap);
+        const uint32_t x = (c + TILE - 1) / TILE;
+        const uint32_t inc = wave_inclusive_sum(x);
+        s_ubase[lane] = inc - x;
+        if (lane == kWave - 1) s_ubase[kRecStripes] = inc;
+    }
     __syncthreads();
+    const uint64_t tiles = reg_cnt ? (uint64_t)s_ubase[kRecStripes] : (m + TILE - 1) / TILE;
+    // unit -> its first record and size
+    auto locate = [&](uint64_t u, uint64_t& tb, uint32_t& valid) {
+        if (!reg_cnt) {
+            tb = u * TILE;
+            valid = (uint32_t)((m - tb) < (uint64_t)TILE ? (m - tb) : (uint64_t)TILE);
+            return;
+        }
+        uint32_t a = 0, z = kRecStripes;   // last region r with s_ubase[r] <= u
+        while (z - a > 1) {
+            const uint32_t mid = (a + z) / 2;
+            if (s_ubase[mid] <= (uint32_t)u) a = mid;
+            else z = mid;
+        }
+        const uint32_t i0 = ((uint32_t)u - s_ubase[a]) * TILE;
+        tb = (uint64_t)a * reg_cap + i0;
+        const uint32_t c = min(reg_cnt[a * kRecCurStride], reg_cap) - i0;
+        valid = c < (uint32_t)TILE ? c : (uint32_t)TILE;
+    };
     uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
     uint64_t k[ITEMS];
     uint32_t v[ITEMS];
-    auto load = [&](uint64_t tt, uint64_t* kk, uint32_t* vv) {   // clamped, unpredicated (see k_split)
-        const uint64_t tb = tt * TILE;
-        const uint32_t last = (uint32_t)min(m - 1 - tb, (uint64_t)(TILE - 1));
+    auto load = [&](uint64_t tb, uint32_t valid, uint64_t* kk, uint32_t* vv) {   // clamped, unpredicated (see k_split)
+        const uint32_t last = valid - 1;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t le = wave * WTILE + j * kWave + lane;
@@ -714,11 +745,14 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
             vv[j] = lpos[e];
         }
     };
-    if (t < tiles) load(t, k, v);
+    uint64_t tb = 0;
+    uint32_t valid = 1;
+    if (t < tiles) {
+        locate(t, tb, valid);
+        load(tb, valid, k, v);
+    }
     uint32_t par = 0;
     while (t < tiles) {
-        const uint64_t tb = t * TILE;
-        const uint32_t valid = (uint32_t)((m - tb) < (uint64_t)TILE ? (m - tb) : (uint64_t)TILE);
         uint32_t dr[ITEMS];
         // whole tiles take the ranking without per-item tests
         auto rank = [&](auto wholec) {
@@ -757,7 +791,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
         const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
-        load(tn < tiles ? tn : tiles - 1, kn, vn);
+        uint64_t tbn;
+        uint32_t validn;
+        locate(tn < tiles ? tn : tiles - 1, tbn, validn);
+        load(tbn, validn, kn, vn);
         const uint32_t kbsh = b.rb + (PK8 ? (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb : 0u);
         const uint64_t remmask = PK8 ? (1ull << kbsh) - 1ull : 0ull;
 #pragma unroll
@@ -797,6 +834,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_list(BucketSpec b
             v[j] = vn[j];
         }
         t = tn;
+        tb = tbn;
+        valid = validn;
         par ^= 1u;
     }
     for (uint32_t i = dg; i < 1024u; i += BLOCK)

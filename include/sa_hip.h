@@ -115,7 +115,9 @@ typedef struct {
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */
     uint64_t kern_bytes[SA_K_COUNT];     /* algorithmic bytes moved per kind */
     int32_t round1_segments;             /* bucketed round 1: 0 exact digit totals, 1 sampled padded segments,
-                                            2 padded segments overflowed and the round ran again exactly */
+                                            2 padded segments overflowed and the round ran again exactly;
+                                            range builds: 3 records by one striped text scan, 4 a record
+                                            stripe overflowed and the round ran again with the counting scan */
     int32_t round1_layout;               /* bucketed round 1: bit 0 compact key1 low (BucketSpec.cmp),
                                             bit 1 packed 8-byte first-pass items (PK8) */
 } sa_stats;

@@ -394,6 +394,7 @@ def _multi_rank_worker(rank, world, port, q, large=False):
     say("group up")
     try:
         ops = HipRangeOps(0, 0)
+        ops.profile = True   # round 1's sa_stats: which record path ran
         res = {}
         if large:
             from hpc_suffix_array_amd import DeviceBuilder
@@ -427,7 +428,11 @@ def _multi_rank_worker(rank, world, port, q, large=False):
             return
         for name, kind, n, seed in (("dna", "dna", 3_000_017, 8), ("byte256", "byte256", 2_000_003, 2),
                                     ("alnum", "alnum", 1_048_576, 1), ("binary", "binary", 1_000_003, 4),
-                                    ("periodic", None, 300_000, 11), ("degenerate", None, 70_001, 0)):
+                                    ("periodic", None, 300_000, 11), ("degenerate", None, 70_001, 0),
+                                    ("dna_overflow", "dna", 2_000_003, 9), ("dna_counted", "dna", 2_000_003, 9)):
+            # dna_overflow: record stripes of half their share (the round runs
+            # again with the counting scan); dna_counted: the counting scan
+            ops.b.set_debug({"dna_overflow": ("pad_overflow",), "dna_counted": ("no_pad",)}.get(name, ()))
             if name == "periodic":
                 t = np.tile(O.gen_text("alnum", 1000, seed=seed), 300)
             elif name == "degenerate":
@@ -442,7 +447,9 @@ def _multi_rank_worker(rank, world, port, q, large=False):
             say("gathered", name)
             if rank == 0:
                 want = O.sa_c(t).astype(np.int64)
-                res[name] = (bool((sa.cpu().numpy() == want).all()), d.stats["path"], len(d.stats["unsorted"]))
+                res[name] = (bool((sa.cpu().numpy() == want).all()), d.stats["path"], len(d.stats["unsorted"]),
+                             ops.round1_stats.to_dict()["round1_segments"])
+        ops.b.set_debug(())
         if rank == 0:
             q.put(res)
     except BaseException:
@@ -461,8 +468,9 @@ def test_distributed_hip_multi_rank(gpu, world):
     unequal ranges, rank requests answered by other ranks, several doubling
     rounds (periodic text), the sample-sort fallback (one symbol) -- every SA
     equal to the oracle's.  From 4 ranks a range holds <= 0.3 n suffixes and
-    round 1 sorts records counted and emitted by k_bucket_hist<.., 1 / 2>
-    (k_split_list) instead of filtering the text in k_split_text."""
+    round 1 sorts records emitted by k_bucket_hist<.., 3> into striped
+    regions (or, forced / overflowed, counted and emitted by <.., 1 / 2>;
+    k_split_list) instead of filtering the text in k_split_text."""
     _multi_rank(world)
 
 
@@ -494,10 +502,16 @@ def _multi_rank(world, large=False):
         assert p.exitcode == 0
     if large:
         return res
-    for name, (ok, path, rounds) in res.items():
+    for name, (ok, path, rounds, seg) in res.items():
         assert ok, (name, world)
         assert path == ("sample-sort" if name == "degenerate" else "range"), (name, path)
     assert res["periodic"][2] >= 4, res["periodic"]
+    # ranges of <= 0.3 n (world >= 4) take the records; one striped scan of
+    # the text unless forced off or overflowed
+    listed = world >= 4
+    assert res["dna"][3] == ("striped-records" if listed else "exact"), (world, res["dna"])
+    assert res["dna_overflow"][3] == ("striped-records-overflow" if listed else "exact"), (world, res["dna_overflow"])
+    assert res["dna_counted"][3] == "exact", (world, res["dna_counted"])
 
 
 @pytest.mark.slow
