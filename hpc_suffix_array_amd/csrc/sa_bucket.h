@@ -175,12 +175,14 @@ constexpr uint32_t kCoarse = 1u << kCoarseBits;
 // IDENT: sigma = 256 (every byte value present), so the dense digit is the
 // byte itself: no LDS byte map (configs[3]'s byte256 text: each rank scans
 // the whole 4 GiB text twice)
+// DNA (POW2): the text's alphabet is exactly {A, C, G, T}: dense digits by
+// ((b >> 1) ^ (b >> 2)) & 3 per byte, four at once (as k_split_text)
 constexpr uint32_t kRecStripes = 64;
 constexpr uint32_t kRecCurStride = 64;   // words between stripe cursors (atomics on one line serialise)
 // record slots of a range of m suffixes: the striped regions' 1/8 margin and
 // two tiles of slack per stripe
 constexpr uint64_t rec_capacity(uint64_t m) { return m + m / 8 + kRecStripes * (2ull * kTile + 1); }
-template <bool POW2 = false, bool COARSE = false, int LM = 0, bool IDENT = false>
+template <bool POW2 = false, bool COARSE = false, int LM = 0, bool IDENT = false, bool DNA = false>
 __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restrict__ text, uint64_t n,
                                                         const uint16_t* __restrict__ code, BucketSpec b,
                                                         uint32_t* __restrict__ ghist, uint64_t p0, uint64_t p1,
@@ -246,7 +248,10 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 w[1] = v.y;
                 w[2] = v.z;
                 w[3] = v.w;
-                if constexpr (!IDENT) {
+                if constexpr (DNA) {
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) w[q] = ((w[q] >> 1) ^ (w[q] >> 2)) & 0x03030303u;
+                } else if constexpr (!IDENT) {
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         uint32_t o = 0;
@@ -1016,7 +1021,7 @@ __global__ __launch_bounds__(kBlock) void k_u_gather(const uint32_t* __restrict_
 // Exclusive popcount scan of a bitmap of nw words (the compact rank map's
 // prefix, RankMap): k_popc_reduce (per-block popcount sums) -> k_popc_top
 // (their exclusive scan, one workgroup) -> k_popc_apply (each block's words
-// rescanned from its offset).  kPcPer consecutive words per thread, moved as
+// rescanned from its offset; one prefix word per 8 bitmap words).  kPcPer consecutive words per thread, moved as
 // 16-byte vectors (bits and prefix are hipMalloc bases); kPcBlock words per
 // block.  (8 scalar words per thread and a top scan of 256 sums per step:
 // 0.24 ms for the 2^25 words of 1 GiB.)
@@ -1060,6 +1065,7 @@ __global__ __launch_bounds__(kPcTop) void k_popc_top(uint32_t* __restrict__ part
     const uint32_t per = (blocks + kPcTop - 1) / kPcTop;
     const uint32_t b0 = threadIdx.x * per, b1 = b0 + per < blocks ? b0 + per : blocks;
     uint32_t sum = 0;
+#pragma unroll 8
     for (uint32_t b = b0; b < b1; ++b) sum += part[b];
     const uint32_t inc = wave_inclusive_sum(sum);
     if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
@@ -1067,6 +1073,7 @@ __global__ __launch_bounds__(kPcTop) void k_popc_top(uint32_t* __restrict__ part
     uint32_t run = inc - sum;
 #pragma unroll
     for (int w = 0; w < kPcTop / kWave; ++w) run += w < (int)wave_id() ? s_tmp[w] : 0u;
+#pragma unroll 8
     for (uint32_t b = b0; b < b1; ++b) {
         const uint32_t v = part[b];
         part[b] = run;
@@ -1084,20 +1091,13 @@ __global__ __launch_bounds__(kBlock) void k_popc_apply(const uint32_t* __restric
 #pragma unroll
     for (int k = 0; k < kPcPer; ++k) sum += c[k];
     uint32_t run = block_exclusive_sum(sum, s_tmp, nullptr) + part[blockIdx.x];
-    uint32_t o[kPcPer];
+    // one prefix word per 8-word block (RankMap)
+    static_assert(kPcPer % 8 == 0, "whole 8-word blocks per thread");
 #pragma unroll
-    for (int k = 0; k < kPcPer; ++k) {
-        o[k] = run;
-        run += c[k];
-    }
-    if (b0 + kPcPer <= nw) {
+    for (int q = 0; q < kPcPer / 8; ++q) {
+        if (b0 + 8 * q < nw) prefix[(b0 >> 3) + q] = run;
 #pragma unroll
-        for (int q = 0; q < kPcPer / 4; ++q)
-            reinterpret_cast<uint4*>(prefix + b0)[q] = make_uint4(o[4 * q], o[4 * q + 1], o[4 * q + 2], o[4 * q + 3]);
-    } else {
-#pragma unroll
-        for (int k = 0; k < kPcPer; ++k)
-            if (b0 + k < nw) prefix[b0 + k] = o[k];
+        for (int k = 0; k < 8; ++k) run += c[8 * q + k];
     }
 }
 

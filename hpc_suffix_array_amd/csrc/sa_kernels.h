@@ -1091,15 +1091,25 @@ __global__ __launch_bounds__(kBlock) void k_seg_scan(uint32_t* __restrict__ c_he
 // Where rank[x] lives: rank[x] itself (prefix == nullptr: the n-entry rank
 // array of one GPU), or the range-partitioned build's compact map -- only
 // the members of this rank's round-1 unsorted set have ranks, in text order:
-// rank[prefix[x >> 5] + popc(member[x >> 5] below bit x & 31)], prefix the
-// exclusive popcount scan of the member bitmap (sa_dist.h).  8 + 4 |U| bytes
-// per suffix range instead of 4 n.
+// rank[prefix[x >> 8] + the members of x's 256-bit block below x], prefix
+// the exclusive popcount scan of the member bitmap per 8-word block
+// (sa_dist.h; one word per 256 positions: the scan writes n / 64 bytes, not
+// n / 8).  The block's 32 bytes share one cache line.  n / 8 + n / 64 +
+// 4 |U| bytes per rank instead of 4 n.
 struct RankMap {
-    const uint32_t* __restrict__ member = nullptr;
+    const uint32_t* __restrict__ member = nullptr;   // 32-byte aligned, whole blocks
     const uint32_t* __restrict__ prefix = nullptr;
     __device__ __forceinline__ uint64_t slot(uint32_t x) const {
         if (!prefix) return x;
-        return (uint64_t)prefix[x >> 5] + (uint32_t)__popc(member[x >> 5] & ((1u << (x & 31u)) - 1u));
+        const uint32_t g = x >> 8, k = (x >> 5) & 7u;
+        const uint4* p = reinterpret_cast<const uint4*>(member) + 2 * (uint64_t)g;
+        const uint4 a = p[0], c = p[1];
+        const uint32_t w[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+        uint32_t cnt = prefix[g];
+#pragma unroll
+        for (uint32_t q = 0; q < 8; ++q)
+            cnt += (uint32_t)__popc(q < k ? w[q] : q == k ? (w[q] & ((1u << (x & 31u)) - 1u)) : 0u);
+        return cnt;
     }
 };
 

@@ -318,6 +318,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         if (striped) {
             SA_HIP(hipMemsetAsync(rcur, 0, kRecStripes * kRecCurStride * 4, s));
             if (ident) SA_HIST_ID_G(rgrid, 3, rcur);
+            else if (pow2 && SA_DNA_SWAR && c->dna)
+                hipLaunchKernelGGL((k_bucket_hist<true, false, 3, false, true>), dim3(rgrid), dim3(kBlock), 0, s, d_text,
+                                   n, (const uint16_t*)c->code, bp.bs, os_ghist(c), 0ull, n, blo, bhi, lkeys, lpos, rcur,
+                                   rcap, c->words + 11);
             else if (pow2) SA_HIST_G(rgrid, true, 3, rcur);
             else SA_HIST_G(rgrid, false, 3, rcur);
             // an overflowed stripe dropped records: stop before any pass reads them
