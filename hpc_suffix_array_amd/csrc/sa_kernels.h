@@ -378,13 +378,32 @@ struct Chunking {
 // ---------------------------------------------------------------------------
 // scans
 // ---------------------------------------------------------------------------
+// Inclusive sum over the wave by DPP: row_shr 1 / 2 / 4 / 8 inside each
+// 16-lane row, then row_bcast 15 / 31 across rows (lanes without a source
+// add 0).  The __shfl_up form took six ds_bpermute lane addresses and six
+// lane masks that the compiler hoisted out of the kernels' loops: in the
+// first bucket pass and the LSD passes they spilled to scratch, and each
+// reload waited for every store in flight.
+#ifndef SA_DPP_SCAN
+#define SA_DPP_SCAN 1
+#endif
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t x) {
+#if SA_DPP_SCAN
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xf, 0xf, false);   // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xf, 0xf, false);   // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xf, 0xf, false);   // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xa, 0xf, false);   // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xc, 0xf, false);   // row_bcast:31
+    return x;
+#else
 #pragma unroll
     for (int o = 1; o < kWave; o <<= 1) {
         const uint32_t y = __shfl_up(x, o, kWave);
         if ((int)lane_id() >= o) x += y;
     }
     return x;
+#endif
 }
 
 // exclusive sum over the 256 threads of the block; s_tmp holds kWaves words.

@@ -447,6 +447,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     };
     if (t < tiles) load(t);
     uint32_t par = 0;
+    // tile-level range tests as 32-bit tile-index compares (scalar): in 64
+    // bits they went to VALU with a hoisted 64-bit constant that spilled to
+    // scratch, and every reload waited for the previous tile's stores
+    const uint32_t t_whole = n >= 4ull * NW ? (uint32_t)((n - 4ull * NW) / TILE + 1) : 0u;   // tb + 4 NW <= n
+    const uint32_t t_int = n >= (uint64_t)TILE + K ? (uint32_t)((n - TILE - K) / TILE + 1) : 0u;   // tb + TILE + K <= n
+    const uint32_t t_last = (uint32_t)(tiles - 1);
 #if SA_TEXT_PROF
     // diagnostic build (-DSA_TEXT_PROF=1): clock64 spans of thread 0 per phase
     uint64_t pacc[5] = {0, 0, 0, 0, 0}, plast = clock64();
@@ -461,11 +467,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
 #endif
     while (t < tiles) {
         const uint64_t tb = t * TILE;
-        const uint32_t valid = (uint32_t)((n - tb) < (uint64_t)TILE ? (n - tb) : (uint64_t)TILE);
+        const uint32_t valid = (uint32_t)t < t_last ? (uint32_t)TILE : (uint32_t)(n - tb);
         // dense digits (0 past the end); a tile whose staged words lie inside
         // the text maps its four bytes with four independent LDS reads (the
         // per-byte bounds test made them a chain of branches and waits)
-        const bool whole = tb + 4ull * NW <= n;   // uniform
+        const bool whole = (uint32_t)t < t_whole;   // uniform
 #pragma unroll
         for (int i = 0; i < WPT; ++i) {
             const uint32_t w = dg + i * BLOCK;
@@ -516,7 +522,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
                 for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
             }
-            const bool interior = tb + TILE + K <= n;   // every suffix of the tile has >= K symbols
+            const bool interior = (uint32_t)t < t_int;   // every suffix of the tile has >= K symbols
             const bool full = full0 && interior;        // uniform
             // the digits leaving D (l0 ..), moving from the remainder into D
             // (l0 + s ..) and entering the remainder (l0 + K ..)
@@ -569,13 +575,18 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         // memory operation for it)
         uint32_t clm, dbase;
         if (dg < (uint32_t)RADIX) {
-            tile_cnt = s_cnt[dg];
-            s_cnt[dg] = 0;
+            // (the lane's addresses rebuilt here from an opaque copy of dg: hoisted
+            // out of the loop they spilled to scratch, and each reload waited
+            // for every store of the previous tile)
+            uint32_t dgo = dg;
+            asm volatile("" : "+v"(dgo));
+            tile_cnt = s_cnt[dgo];
+            s_cnt[dgo] = 0;
             // the pass need not be stable, so a tile's place in each digit
             // is claimed from a cursor (one atomic round trip, whatever the
             // other tiles do) instead of a look-back
-            dbase = seg_end ? sbase : digit_base[dg];
-            clm = tile_cnt ? atomicAdd(&cursor[dg], tile_cnt) : 0u;
+            dbase = seg_end ? sbase : digit_base[dgo];
+            clm = tile_cnt ? atomicAdd(&cursor[dgo], tile_cnt) : 0u;
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
