@@ -202,6 +202,11 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
     __shared__ __attribute__((aligned(16))) uint32_t s_dcw[(kTile + kMaxK) / 4 + 8];   // dense digits, 4 per word (+ slack)
     uint8_t* s_dc = reinterpret_cast<uint8_t*>(s_dcw);
     __shared__ uint32_t s_hlo[NB];
+    // DNA records: the tile's digits packed 2 bits each, 16 per word (the
+    // first on top) + the halo, so a record's K <= 32 symbols are three word
+    // reads instead of K byte reads
+    constexpr bool PKD = DNA && REC;
+    __shared__ uint32_t s_pk[PKD ? kBlock + kMaxK / 16 + 2 : 1];
     {
         const uint32_t cv = code[threadIdx.x];
         s_map[threadIdx.x] = (uint8_t)(cv ? cv - 1u : 0u);
@@ -272,12 +277,32 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 }
             }
             *reinterpret_cast<uint4*>(s_dc + threadIdx.x * RUN) = make_uint4(w[0], w[1], w[2], w[3]);
+            if constexpr (PKD) {
+                uint32_t pk = 0;
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const uint32_t x = w[q];   // four digits 0..3, the first in the low byte
+                    const uint32_t v = ((x & 3u) << 6) | ((x >> 4) & 0x30u) | ((x >> 14) & 0xCu) | (x >> 24);
+                    pk |= v << (24 - 8 * q);
+                }
+                s_pk[threadIdx.x] = pk;
+            }
             if (threadIdx.x < (uint32_t)kMaxK) {
                 const uint64_t h = tb + kTile + threadIdx.x;
                 s_dc[kTile + threadIdx.x] = (h < n) ? (IDENT ? (uint8_t)chv : s_map[chv]) : (uint8_t)0;
             }
         }
         __syncthreads();
+        if constexpr (PKD) {
+            // the halo's packed words (read after the compaction's barrier)
+            if (threadIdx.x < (uint32_t)kMaxK / 16) {
+                uint32_t pk = 0;
+                for (int y = 0; y < 16; ++y) pk |= (uint32_t)s_dc[kTile + 16 * threadIdx.x + y] << (30 - 2 * y);
+                s_pk[kBlock + threadIdx.x] = pk;
+            } else if (threadIdx.x < (uint32_t)kMaxK / 16 + 2) {
+                s_pk[kBlock + threadIdx.x] = 0;
+            }
+        }
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
         const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(sig) : 0u;
@@ -345,8 +370,17 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 const uint32_t l = s_rp[t];
                 uint32_t Dk = 0;
                 uint64_t r = 0;
-                for (uint32_t q = 0; q < b.s; ++q) Dk = POW2 ? ((Dk << lg) | s_dc[l + q]) : Dk * sig + s_dc[l + q];
-                for (uint32_t q = b.s; q < K; ++q) r = POW2 ? ((r << lg) | s_dc[l + q]) : r * sig + s_dc[l + q];
+                if (PKD && K <= 32) {   // uniform
+                    const uint32_t wi = l >> 4, off = 2u * (l & 15u);
+                    const uint64_t a = s_pk[wi], bw = s_pk[wi + 1], cw = s_pk[wi + 2];
+                    uint64_t win = ((a << 32) | bw) << off;
+                    if (off) win |= cw >> (32u - off);
+                    Dk = (uint32_t)(win >> (64u - 2u * b.s));
+                    r = (win >> (64u - 2u * K)) & ((1ull << (2u * b.R)) - 1ull);
+                } else {
+                    for (uint32_t q = 0; q < b.s; ++q) Dk = POW2 ? ((Dk << lg) | s_dc[l + q]) : Dk * sig + s_dc[l + q];
+                    for (uint32_t q = b.s; q < K; ++q) r = POW2 ? ((r << lg) | s_dc[l + q]) : r * sig + s_dc[l + q];
+                }
                 lkeys[rb + t] = ((uint64_t)Dk << b.rb) | bucket_low(b, r, n - (tb + l));
                 lpos[rb + t] = (uint32_t)(tb + l);
             }
