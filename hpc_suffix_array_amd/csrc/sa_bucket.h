@@ -287,44 +287,55 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
                 }
                 s_pk[threadIdx.x] = pk;
             }
-            if (threadIdx.x < (uint32_t)kMaxK) {
+            if (threadIdx.x < (uint32_t)kMaxK) {   // wave 0, every lane
                 const uint64_t h = tb + kTile + threadIdx.x;
-                s_dc[kTile + threadIdx.x] = (h < n) ? (IDENT ? (uint8_t)chv : s_map[chv]) : (uint8_t)0;
+                const uint32_t hd = (h < n) ? (IDENT ? chv : (uint32_t)s_map[chv]) : 0u;
+                s_dc[kTile + threadIdx.x] = (uint8_t)hd;
+                if constexpr (PKD) {
+                    // the halo's packed words: 16 lanes' digits OR-ed together
+                    static_assert(kMaxK == kWave, "the halo is wave 0's");
+                    uint32_t v = hd << (30 - 2 * (threadIdx.x & 15u));
+#pragma unroll
+                    for (int o = 1; o < 16; o <<= 1) v |= (uint32_t)__shfl_xor((int)v, o, kWave);
+                    if ((threadIdx.x & 15u) == 0) s_pk[kBlock + threadIdx.x / 16] = v;
+                    if (threadIdx.x < 2) s_pk[kBlock + kMaxK / 16 + threadIdx.x] = 0;
+                }
             }
         }
         __syncthreads();
-        if constexpr (PKD) {
-            // the halo's packed words (read after the compaction's barrier)
-            if (threadIdx.x < (uint32_t)kMaxK / 16) {
-                uint32_t pk = 0;
-                for (int y = 0; y < 16; ++y) pk |= (uint32_t)s_dc[kTile + 16 * threadIdx.x + y] << (30 - 2 * y);
-                s_pk[kBlock + threadIdx.x] = pk;
-            } else if (threadIdx.x < (uint32_t)kMaxK / 16 + 2) {
-                s_pk[kBlock + threadIdx.x] = 0;
-            }
-        }
         const uint32_t l0 = threadIdx.x * RUN;
         uint32_t D = 0;
         const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(sig) : 0u;
         const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
         const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;
-        for (uint32_t q = 0; q < b.s; ++q) D = POW2 ? ((D << lg) | s_dc[l0 + q]) : D * sig + s_dc[l0 + q];
         // the digits leaving (positions l0 .. l0 + 15) and entering (l0 + s ..)
         uint32_t xo[RUN / 4], xi[RUN / 4];
-        lds_bytes<RUN>(s_dcw, l0, xo);
-        lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
+        // PKD: the lane's 32 symbols from l0 as one 64-bit word (its packed
+        // word and the next); position l0 + j's bucket is bits [2j, 2j + bb)
+        // from the top (bb <= 2s: the bucket is a bit field of D)
+        uint64_t wpk = 0;
+        if constexpr (PKD) {
+            wpk = ((uint64_t)s_pk[threadIdx.x] << 32) | s_pk[threadIdx.x + 1];
+        } else {
+            for (uint32_t q = 0; q < b.s; ++q) D = POW2 ? ((D << lg) | s_dc[l0 + q]) : D * sig + s_dc[l0 + q];
+            lds_bytes<RUN>(s_dcw, l0, xo);
+            lds_bytes<RUN>(s_dcw, l0 + b.s, xi);
+        }
+        const uint32_t pksh = 64u - b.bb;
         uint32_t keep = 0;   // LIST: bit j = position l0 + j is in the range
         // whole tiles inside [p0, p1) take the loop without the position test
         auto count = [&](auto wholec) {
             constexpr bool WHOLE = decltype(wholec)::value;
 #pragma unroll
             for (int j = 0; j < RUN; ++j) {
-                if (j > 0) {
+                if (!PKD && j > 0) {
                     if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
                     else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
                 }
                 if (WHOLE || tb + l0 + j < p1) {
-                    const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
+                    const uint32_t bk = PKD    ? (uint32_t)((wpk << (2 * j)) >> pksh)
+                                        : POW2 ? (D >> bksh)
+                                               : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
                     if constexpr (COARSE) {
                         atomicAdd(&s_hlo[bk >> cshift], 1u);
                     } else {
