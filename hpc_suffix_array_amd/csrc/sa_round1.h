@@ -387,7 +387,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         // at 512, alnum 5.13 vs 4.90: profiles/r02_bc_ab_text_block_kinds.txt)
         constexpr int kTextBlock = SA_TEXT_BLOCK;
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
-        const bool dna = SA_DNA_SWAR && c->dna;
+        // (the DNA kernel keys each position from a 32-symbol window)
+        const bool dna = SA_DNA_SWAR && c->dna && bp.bs.s + bp.bs.R + kItemsA - 1 <= 32 && 2 * bp.bs.s <= 32;
         auto text_grid = [&](int block) {
             const uint64_t tile = (uint64_t)block * kItemsA;
             return (uint32_t)std::max<uint64_t>(

@@ -391,6 +391,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     __shared__ uint64_t s_keys[TILE];
     __shared__ uint16_t s_idx[TILE];                    // tile offset; PK8: the pair's digit
     __shared__ uint32_t s_dcw[NW + 8];                  // dense digits, 4 per word (0 past the end; + slack)
+    // DNA: the digits packed 2 bits each, one byte per staged word (the first
+    // digit on top), so a lane's 32 symbols from l0 are three word reads and
+    // each position's key1 a shift of that window (no Horner start, no
+    // per-position byte extraction); the host launches it when K + ITEMS - 1 <= 32
+    __shared__ uint32_t s_pkw[DNA ? (NW + 3) / 4 + 4 : 1];
     __shared__ uint8_t s_map[256];
     __shared__ uint32_t s_cnt[RADIX];
     __shared__ uint16_t s_start[RADIX];
@@ -491,6 +496,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                     }
                 }
                 s_dcw[w] = o;
+                if constexpr (DNA)
+                    reinterpret_cast<uint8_t*>(s_pkw)[w] =
+                        (uint8_t)(((o & 3u) << 6) | ((o >> 4) & 0x30u) | ((o >> 14) & 0xCu) | (o >> 24));
             }
         }
         // the next tile's ticket now: its round trip overlaps this tile's key
@@ -515,7 +523,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;   // bucket = D >> (lg s - bb)
             // interior low = r mulR + addR (BucketSpec: compact or not)
             const uint64_t mulR = b.cmp ? 2u : b.R + 1u, addR = b.cmp ? 1u : b.s + b.R;
-            if constexpr (POW2) {
+            uint64_t win = 0;   // DNA: symbols l0 .. l0 + 31, the first on top
+            if constexpr (DNA) {
+                const uint32_t bo = l0 / 4, sh = bo & 3u;   // l0 % 4 == 0: one packed byte per 4 symbols
+                const uint32_t w0 = s_pkw[bo >> 2], w1 = s_pkw[(bo >> 2) + 1], w2 = s_pkw[(bo >> 2) + 2];
+                win = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh)) << 32) |
+                      __builtin_bswap32(__builtin_amdgcn_alignbyte(w2, w1, sh));
+            } else if constexpr (POW2) {
                 for (uint32_t q = 0; q < b.s; ++q) D = (D << lg) | s_dc[l0 + q];
                 for (uint32_t q = 0; q < b.R; ++q) r = (r << lg) | s_dc[l0 + b.s + q];
             } else {
@@ -527,16 +541,23 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             // the digits leaving D (l0 ..), moving from the remainder into D
             // (l0 + s ..) and entering the remainder (l0 + K ..)
             uint32_t xo[ITEMS / 4], xm[ITEMS / 4], xn[ITEMS / 4];
-            lds_bytes<ITEMS>(s_dcw, l0, xo);
-            lds_bytes<ITEMS>(s_dcw, l0 + b.s, xm);
-            lds_bytes<ITEMS>(s_dcw, l0 + K, xn);
+            if constexpr (!DNA) {
+                lds_bytes<ITEMS>(s_dcw, l0, xo);
+                lds_bytes<ITEMS>(s_dcw, l0 + b.s, xm);
+                lds_bytes<ITEMS>(s_dcw, l0 + K, xn);
+            }
+            const uint32_t dsh = 64u - 2u * b.s, rsh = 64u - 2u * K;
             // FULL: a whole tile of the whole bucket range, every position
             // kept (no per-item tests)
             auto keyloop = [&](auto fullc) {
             constexpr bool FULL = decltype(fullc)::value;
 #pragma unroll
             for (int j = 0; j < ITEMS; ++j) {
-                if (j > 0) {
+                if constexpr (DNA) {
+                    const uint64_t x = win << (2 * j);
+                    D = (uint32_t)(x >> dsh);
+                    r = (x >> rsh) & rmask;
+                } else if (j > 0) {
                     const uint32_t xi = byte_at<ITEMS>(xm, j - 1);
                     if constexpr (POW2) {
                         D = ((D << lg) | xi) & dmask;
