@@ -314,7 +314,14 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
         // word and the next); position l0 + j's bucket is bits [2j, 2j + bb)
         // from the top (bb <= 2s: the bucket is a bit field of D)
         uint64_t wpk = 0;
-        if constexpr (PKD) {
+        // IDENT (sigma = 256, digit = byte): the lane's 20 bytes from l0 as
+        // five aligned words; position l0 + j's bucket is the top bb bits of
+        // the big-endian word at byte j (bb <= 32, a bit field of D)
+        uint32_t wid[IDENT ? 5 : 1];
+        if constexpr (IDENT) {
+#pragma unroll
+            for (int q = 0; q < 5; ++q) wid[q] = s_dcw[l0 / 4 + q];
+        } else if constexpr (PKD) {
             wpk = ((uint64_t)s_pk[threadIdx.x] << 32) | s_pk[threadIdx.x + 1];
         } else {
             for (uint32_t q = 0; q < b.s; ++q) D = POW2 ? ((D << lg) | s_dc[l0 + q]) : D * sig + s_dc[l0 + q];
@@ -328,14 +335,18 @@ __global__ __launch_bounds__(kBlock) void k_bucket_hist(const uint8_t* __restric
             constexpr bool WHOLE = decltype(wholec)::value;
 #pragma unroll
             for (int j = 0; j < RUN; ++j) {
-                if (!PKD && j > 0) {
+                if (!PKD && !IDENT && j > 0) {
                     if constexpr (POW2) D = ((D << lg) | byte_at<RUN>(xi, j - 1)) & dmask;
                     else D = (D - byte_at<RUN>(xo, j - 1) * ps1) * sig + byte_at<RUN>(xi, j - 1);
                 }
                 if (WHOLE || tb + l0 + j < p1) {
-                    const uint32_t bk = PKD    ? (uint32_t)((wpk << (2 * j)) >> pksh)
-                                        : POW2 ? (D >> bksh)
-                                               : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
+                    uint32_t bk;
+                    if constexpr (IDENT)
+                        bk = __builtin_bswap32(__builtin_amdgcn_alignbyte(wid[j / 4 + 1], wid[j / 4], j % 4)) >> (32u - b.bb);
+                    else
+                        bk = PKD ? (uint32_t)((wpk << (2 * j)) >> pksh)
+                             : POW2 ? (D >> bksh)
+                                    : (uint32_t)(((uint64_t)D * b.cmul) >> shh);
                     if constexpr (COARSE) {
                         atomicAdd(&s_hlo[bk >> cshift], 1u);
                     } else {
