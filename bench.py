@@ -300,7 +300,10 @@ def run_single(a, torch, dev, world, rank, barrier):
                           "bytes_per_suffix": round(build_bytes / n, 2), "t_sa_ms": round(1e3 * t_sa, 3)}
     extra = {
         "build_roofline": build_roofline,
-        "ms_per_round": [round(x, 3) for x in round_ms],
+        # the packed schedule's rounds: round 1 sorts by the first K symbols
+        # at once (the reference's rounds h = 1 .. K/2), so these are not per
+        # doubling; ms_per_doubling_round is the reference schedule's
+        "ms_per_packed_round": [round(x, 3) for x in round_ms],
         "rounds": rounds,
         "distinct_per_round": stats[-1]["distinct"],
         "passes_per_round": stats[-1]["passes"],
@@ -324,9 +327,81 @@ def run_single(a, torch, dev, world, rank, barrier):
         # (manber_myers.c:97-125, the companion schedule's rounds)
         "ms_per_reference_round": (round(1e3 * elapsed / a.steps / ref_sched["rounds"], 3)
                                    if ref_sched and ref_sched.get("rounds") else None),
+        # ms per doubling round as the metric reads it (manber_myers.c:97-125):
+        # the north-star schedule's measured rounds, one LSD sort per h
+        "ms_per_doubling_round": ref_sched["ms_per_round"] if ref_sched else None,
     }
     b.close()
     return elapsed, extra
+
+
+XGMI_BYTES_PER_REQUEST = 4 + 8   # a request is a u32 position, its answer an i64 rank (distributed.py)
+
+
+def rank_record(rank: int, stats: list, round1_kernels: dict | None) -> dict:
+    """One rank's measurements of the timed steps, for distributed_summary:
+    its range, the mean HIP-event time of each phase of DistributedSA.build
+    and the round-1 kernels of its last build (sa_dist_round1's sa_stats)."""
+    st = stats[-1]
+    phase = {}
+    for x in stats:
+        for k, v in (x.get("phase_ms") or {}).items():
+            phase[k] = phase.get(k, 0.0) + v / len(stats)
+    return {"rank": rank, "m": st.get("m"), "sa_off": st.get("sa_off"), "phase_ms": phase,
+            "round1_kernels": round1_kernels or {}, "requests": st.get("requests") or [],
+            "cross_requests": st.get("cross_requests") or []}
+
+
+def distributed_summary(recs: list, n: int) -> dict:
+    """The N > 1 line's per-rank figures (every rank's record, rank order):
+    - "roofline": the round-1 kernel with the most time on the rank whose
+      round 1 is slowest -- its algorithmic bytes per launch (the range's m
+      suffixes times the kernel's bytes per suffix, sa_round1.h add_bytes)
+      over its mean HIP-event launch duration, against the 8 TB/s peak;
+    - "round1_per_rank": each rank's round-1 time, algorithmic bytes and GB/s;
+    - "kernels_ms_per_step": each phase's time, max over ranks, and the
+      round-1 kernels of the slowest rank;
+    - "xgmi_bytes_per_round": the bytes of the rank look-ups answered by
+      another rank, per later doubling round (requests out + answers back),
+      which cross xGMI under RCCL (look-ups a rank answers itself stay in HBM);
+    - "largest_rank_share": the largest range over n / G."""
+    G = len(recs)
+    per_rank = []
+    for r in recs:
+        kb = sum(v["bytes"] for v in r["round1_kernels"].values())
+        t = r["phase_ms"].get("round1")
+        gbs = kb / (t / 1e3) / 1e9 if kb and t else None
+        per_rank.append({"rank": r["rank"], "m": r["m"], "round1_ms": t and round(t, 3), "round1_bytes": kb,
+                         "gbs": gbs and round(gbs, 1), "frac": gbs and round(gbs / HBM_PEAK_GBS, 4)})
+    timed = [x for x in per_rank if x["round1_ms"]]
+    slow = max(timed, key=lambda x: x["round1_ms"]) if timed else None
+    roofline = None
+    if slow:
+        kern = recs[slow["rank"]]["round1_kernels"]
+        cand = {k: v for k, v in kern.items() if k != "scan" and v["launches"] and v["bytes"] and v["ms"] > 0}
+        if cand:
+            dom = max(cand, key=lambda k: cand[k]["ms"])
+            v = cand[dom]
+            per_launch = v["bytes"] / v["launches"]
+            avg_s = v["ms"] / v["launches"] / 1e3
+            ach = per_launch / avg_s / 1e9
+            roofline = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "traffic_source": None,
+                        "kernel": KERNEL_NAMES.get(dom, dom) + " [range build, round 1]", "kind": dom,
+                        "rank": slow["rank"], "bytes_per_launch": int(per_launch),
+                        "avg_launch_ms": round(avg_s * 1e3, 4),
+                        "scope": "the slowest rank's round-1 kernel with the most time"}
+    phases = sorted({k for r in recs for k in r["phase_ms"]})
+    kms = {k: round(max(r["phase_ms"].get(k, 0.0) for r in recs), 3) for k in phases}
+    if slow:
+        kms["round1_kernels_slowest_rank"] = {k: round(v["ms"], 3) for k, v in
+                                              recs[slow["rank"]]["round1_kernels"].items() if v["launches"]}
+    cross = recs[0]["cross_requests"]
+    m_max = max((r["m"] or 0) for r in recs)
+    return {"roofline": roofline, "round1_per_rank": per_rank, "kernels_ms_per_step": kms,
+            "requests_per_round": recs[0]["requests"], "cross_requests_per_round": cross,
+            "xgmi_bytes_per_round": [int(c) * XGMI_BYTES_PER_REQUEST for c in cross],
+            "largest_rank_share": round(m_max / (n / G), 4) if m_max else None}
 
 
 def run_distributed(a, torch, dev, world, rank, barrier):
@@ -338,6 +413,7 @@ def run_distributed(a, torch, dev, world, rank, barrier):
     from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa
     n = a.n
     ops = HipRangeOps(n, dev.index)
+    ops.profile = not a.no_profile   # round 1's per-kernel HIP events (sa_dist_round1 sa_stats)
     sptr = torch.cuda.current_stream(dev).cuda_stream
     d_text = torch.empty(n, dtype=torch.uint8, device=dev)
     if a.kind == "degenerate":
@@ -365,6 +441,13 @@ def run_distributed(a, torch, dev, world, rank, barrier):
         return d.stats
 
     elapsed, stats = timed(a.steps, a.warmup, step, barrier)
+    r1k = ops.round1_stats.to_dict()["kernels"] if ops.profile and stats[-1].get("path") == "range" else None
+    rec = rank_record(rank, stats, r1k)
+    recs = [None] * world
+    if world > 1:
+        dist.all_gather_object(recs, rec)
+    else:
+        recs = [rec]
     sa_local, sa_off = holder["sa"]
     # verification: the full SA gathered to every rank, O(n) check on rank 0
     verified = None
@@ -378,19 +461,16 @@ def run_distributed(a, torch, dev, world, rank, barrier):
         dist.broadcast(v, 0)
         verified = bool(v.item()) if n <= 0xFFFFFFFF else None
     st = stats[-1]
-    m_max = st.get("m_max")
-    phase = {}
-    for x in stats:
-        for k, v in (x.get("phase_ms") or {}).items():
-            phase[k] = phase.get(k, 0.0) + v / len(stats)
+    summ = distributed_summary(recs, n)
     extra = {"rounds": st["rounds"], "unsorted_per_round": st.get("unsorted"),
-             "requests_per_round": st.get("requests"), "init_chars": st.get("K"), "sigma": st.get("sigma"),
-             "bucket_bits": st.get("bucket_bits"), "path": st.get("path"), "largest_rank_share": (
-                 round(m_max / (n / world), 4) if m_max else None),
-             "phase_ms": {k: round(v, 3) for k, v in phase.items()},
-             "text_broadcast_ms": round(bcast_ms, 3) if bcast_ms else None, "verified": verified, "roofline": None,
+             "init_chars": st.get("K"), "sigma": st.get("sigma"), "bucket_bits": st.get("bucket_bits"),
+             "path": st.get("path"),
+             "phase_ms": {k: round(v, 3) for k, v in rec["phase_ms"].items()},
+             "text_broadcast_ms": round(bcast_ms, 3) if bcast_ms else None, "verified": verified,
              "note": "range-partitioned build: each rank sorts the suffixes of its bucket range from its text "
-                     "copy; rank requests/answers by RCCL all_to_all between doubling rounds"}
+                     "copy; rank requests/answers by RCCL all_to_all between doubling rounds; roofline = the "
+                     "slowest rank's dominant round-1 kernel"}
+    extra.update(summ)
     return elapsed, extra
 
 

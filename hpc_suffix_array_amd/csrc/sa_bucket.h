@@ -1661,7 +1661,6 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     const uint32_t dsh = ib + low_bits;
     const uint32_t lmask = (1u << low_bits) - 1u;
     const uint64_t imask = (1ull << ib) - 1ull;
-    const uint64_t smask = (1ull << so.ksh) - 1ull;
     auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
     Probe probe;
     if (threadIdx.x == 0) {
@@ -1819,10 +1818,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 // the sorted key1 of this sub-bucket's every-2^ksh-th SA
                 // positions, from the sorted words (a global load here would
                 // make the store phase wait for the next window's loads)
-                // (32-bit positions: a window lies below 2^32)
-                const uint32_t a32 = (uint32_t)a, sm32 = (uint32_t)smask;
-                for (uint32_t p = ((a32 + lo + sm32) >> so.ksh) << so.ksh; p < a32 + hi; p += sm32 + 1)
-                    keys_out[p >> so.ksh] = mn + (((uint64_t)sb << low_bits) | (s_k[p - a32] >> kSlotBits));
+                // (sa_search.h for_each_sample: exact up to a + hi = 2^32)
+                for_each_sample(a, lo, hi, so.ksh, [&](uint32_t q) {
+                    keys_out[(a + q) >> so.ksh] = mn + (((uint64_t)sb << low_bits) | (s_k[q] >> kSlotBits));
+                });
             }
             probe.mark(4);
             // 3. U / U-group offsets (one scan of both; heads = m - U + G)

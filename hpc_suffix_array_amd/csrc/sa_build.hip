@@ -1596,7 +1596,12 @@ int sa_context_set_debug(sa_context* ctx, const sa_opts* opts) {
 int sa_build_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, void* stream,
                     const sa_opts* opts, sa_stats* stats) {
     if (!ctx) return set_err(SA_E_INVALID, "context is NULL");
-    return build_device(ctx, d_text, n, d_sa, (hipStream_t)stream, opts, stats);
+    const int rc = build_device(ctx, d_text, n, d_sa, (hipStream_t)stream, opts, stats);
+    // this build's debug flags, span and launch shapes do not outlive it: a
+    // later sa_dist_* build on the same context sees the defaults unless
+    // sa_context_set_debug sets them again
+    set_debug(ctx, nullptr);
+    return rc;
 }
 
 int sa_check_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, void* stream) {

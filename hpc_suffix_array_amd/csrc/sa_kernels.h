@@ -387,6 +387,12 @@ struct Chunking {
 #ifndef SA_DPP_SCAN
 #define SA_DPP_SCAN 1
 #endif
+// row_bcast:15 / :31 exist on the wave64 GFX9 family only (gfx950 is one);
+// the library is built for gfx950 alone, so another target is an error here
+// rather than a silently wrong scan.
+#if SA_DPP_SCAN && defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "wave_inclusive_sum: DPP row_bcast needs a GFX9-family target (build with -DSA_DPP_SCAN=0 otherwise)"
+#endif
 __device__ __forceinline__ uint32_t wave_inclusive_sum(uint32_t x) {
 #if SA_DPP_SCAN
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xf, 0xf, false);   // row_shr:1

@@ -120,4 +120,17 @@ SA_HD uint64_t lower_bound_sampled(const uint64_t* __restrict__ keys, uint32_t k
     return l;
 }
 
+// Every 2^ksh-th SA position inside [a + lo, a + hi) (the key samples a
+// window's sub-bucket writes, sa_bucket.h k_bucket_sort): f(q) with q
+// window-relative.  The first sample is found in 64 bits (a + hi reaches 2^32
+// when n = 2^32); the steps stay 32-bit and window-relative, where q < hi
+// (a window's size) cannot wrap.  Host-checked at the 2^32 boundary by
+// tests/cpp/search_check.cpp.
+template <class F>
+SA_HD void for_each_sample(uint64_t a, uint32_t lo, uint32_t hi, uint32_t ksh, const F& f) {
+    const uint64_t smask = (1ull << ksh) - 1ull;
+    const uint64_t p0 = ((a + lo + smask) >> ksh) << ksh;
+    for (uint32_t q = (uint32_t)(p0 - a); q < hi; q += (uint32_t)smask + 1u) f(q);
+}
+
 }  // namespace sa

@@ -334,14 +334,17 @@ class DistributedSA:
             return self._fallback(text, n, "unsupported alphabet / size")
         ch = None
         if G > 1:
+            self._mark("coarse_allreduce", dev)
             _all_reduce(coarse, group=self.group)
             ch = coarse.cpu()
         _trace("cuts")
+        self._mark("cuts", dev)   # the cut plan and the range's workspace (first build: allocation)
         info = self._phase("cuts", dev, self.ops.cuts, ch)
         _trace("cut", info)
         self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
         if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
             return self._fallback(text, n, "unbalanced bucket ranges")
+        self._mark("sa_local", dev)
         sa_local = self._phase("sa_local", dev, self.ops.empty, info["m"], I32)
         self._mark("round1", dev)
         info = self._phase("round1", dev, self.ops.round1, sa_local)
@@ -543,14 +546,21 @@ class HipOps:
 
     def select(self, mask: torch.Tensor) -> torch.Tensor:
         """int64 positions of the set elements of a bool vector, in order
-        (sa_select_u8_device: per-tile counts, their scan, ordered writes)."""
+        (sa_select_u8_device: per-tile counts, their scan, ordered writes).
+        The output is sized by a counting call first, so the result holds
+        exactly its elements (an m-entry buffer behind a view would keep 8m
+        bytes alive while the caller holds the selection)."""
         mask = mask.contiguous()
-        out = torch.empty(mask.numel(), dtype=I64, device=mask.device)
+        total = self.count_true(mask)
+        out = torch.empty(total, dtype=I64, device=mask.device)
+        if total == 0:
+            return out
         cnt = ctypes.c_uint64()
         N.check(self.L.sa_select_u8_device(mask.data_ptr() if mask.numel() else None, mask.numel(),
-                                           out.data_ptr() if mask.numel() else None, ctypes.byref(cnt),
-                                           self._stream()), "sa_select_u8_device")
-        return out[: cnt.value]
+                                           out.data_ptr(), ctypes.byref(cnt), self._stream()), "sa_select_u8_device")
+        if cnt.value != total:
+            raise N.SAError(f"sa_select_u8_device: {cnt.value} selected after a count of {total}")
+        return out
 
     def count_true(self, mask: torch.Tensor) -> int:
         """Number of set elements of a bool vector (one device count, one sync)."""

@@ -74,7 +74,10 @@ enum sa_kernel_kind {
 #define SA_DEBUG_NO_CMP 0x1u            /* bucketed round 1: original key1 low, not the compact one */
 #define SA_DEBUG_NO_PK8 0x2u            /* bucketed round 1: key1 + position, not packed 8-byte items */
 #define SA_DEBUG_NO_PAD 0x4u            /* bucketed round 1: exact digit totals, not sampled padded segments */
-#define SA_DEBUG_PAD_OVERFLOW 0x8u      /* padded segments with no slack: the round overflows and re-runs exactly */
+#define SA_DEBUG_PAD_OVERFLOW 0x8u      /* forced overflow of the padded round-1 layouts, which then re-run exactly:
+                                           one GPU: padded first-pass segments with no slack; range builds
+                                           (sa_dist_round1): striped record regions of half their share, the
+                                           round re-runs with the counting record scan */
 #define SA_DEBUG_NO_FAST32 0x10u        /* local sort: measured-span kernel, not the fixed-span 32-bit one */
 #define SA_DEBUG_NO_PIVOT 0x20u         /* later rounds: full sorts, never the three-way pivot split */
 #define SA_DEBUG_PERM_ALWAYS 0x40u      /* reference schedule: permutation re-rank at every n */

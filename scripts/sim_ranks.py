@@ -34,35 +34,52 @@ CHUNK = 1 << 25   # torch elementwise / index ops over slices of at most this ma
 
 
 def prefix_keys(torch, text, n, sa, K):
-    """int64 key of the first K symbols of each suffix sa[i] (K <= 7): digits
-    byte + 1 in base 257, 0 past the end, so key order = the order of the
-    K-prefixes with the end smallest (equal keys: equal K-prefixes)."""
-    assert K <= 7, "257^K must fit int64"
+    """The first K symbols of each suffix sa[i] as int64 words of up to 7
+    symbols each (digits byte + 1 in base 257, 0 past the end): the order of
+    the K-prefixes (end smallest) is the lexicographic order of the word
+    lists, and equal lists are equal K-prefixes.  Any K (DNA ranges: K = 20)."""
     pos = sa.to(torch.int64) & 0xFFFFFFFF
-    key = torch.zeros(pos.numel(), dtype=torch.int64, device=pos.device)
-    for t in range(K):
-        p = pos + t
-        inside = p < n
-        d = torch.where(inside, text[torch.where(inside, p, 0)].to(torch.int64) + 1, 0)
-        key = key * 257 + d
-    return key
+    words = []
+    for t0 in range(0, K, 7):
+        key = torch.zeros(pos.numel(), dtype=torch.int64, device=pos.device)
+        for t in range(t0, min(K, t0 + 7)):
+            p = pos + t
+            inside = p < n
+            d = torch.where(inside, text[torch.where(inside, p, 0)].to(torch.int64) + 1, 0)
+            key = key * 257 + d
+        words.append(key)
+    return words
+
+
+def lex_le(a, b):
+    """Elementwise a <= b for word lists a, b (lexicographic)."""
+    lt = None
+    eq = None
+    for x, y in zip(a, b):
+        l, e = x < y, x == y
+        lt = l if lt is None else lt | (eq & l)
+        eq = e if eq is None else eq & e
+    return lt | eq
 
 
 def check_rank(torch, text, n, sa_local, K, flags):
     """Sortedness of one rank's slice on its first K symbols, its positions
-    counted in flags (int32 per text position); returns (first, last) key."""
+    counted in flags (int32 per text position); returns (first, last) key
+    (tuples of the words)."""
     m = sa_local.numel()
     first = last = None
     prev = None
     for a in range(0, m, CHUNK):
         k = prefix_keys(torch, text, n, sa_local[a: a + CHUNK], K)
-        if k.numel() > 1:
-            assert bool((k[1:] >= k[:-1]).all()), f"slice not sorted on its first {K} symbols near {a}"
+        if k[0].numel() > 1:
+            assert bool(lex_le([w[:-1] for w in k], [w[1:] for w in k]).all()), \
+                f"slice not sorted on its first {K} symbols near {a}"
+        head = tuple(int(w[0]) for w in k)
         if prev is not None:
-            assert int(k[0]) >= prev, f"slice not sorted across {a}"
-        prev = int(k[-1])
+            assert head >= prev, f"slice not sorted across {a}"
+        prev = tuple(int(w[-1]) for w in k)
         if first is None:
-            first = int(k[0])
+            first = head
         last = prev
         pos = sa_local[a: a + CHUNK].to(torch.int64) & 0xFFFFFFFF
         flags.index_put_((pos,), torch.ones_like(pos, dtype=flags.dtype), accumulate=True)
@@ -134,6 +151,132 @@ def simulate(n, kind, worlds, ranks="ends", reps=5, check=False, seed=1, log=pri
     return out
 
 
+def simulate_full(n, kind, G, reps=2, seed=1, log=print, check=True):
+    """The whole range-partitioned build of G ranks played on ONE GPU, every
+    rank's phases in turn on its own context (G HipRangeOps in this
+    process), the collectives played in-process: the count matrix of each
+    later round, the requests routed to their owners (what all_to_all moves),
+    the answers routed back.  Per rank and round: the HIP-event time of its
+    own kernels (as on its own GPU), its unsorted suffixes, the requests it
+    sends and how many of them another rank answers (the look-ups that cross
+    xGMI: 4 B out + 8 B back each).  One build's SA (all slices) is O(n)-
+    checked.  Memory: G contexts of ~90 B per range suffix + one text."""
+    import torch
+
+    from bench import ALPHABETS
+    from hpc_suffix_array_amd.distributed import HipRangeOps
+    dev = torch.device("cuda", 0)
+    ops = [HipRangeOps(0, 0) for _ in range(G)]
+    text = torch.empty(n, dtype=torch.uint8, device=dev)
+    ops[0].b.generate_text(text, n, ALPHABETS[kind], seed=seed)
+    torch.cuda.synchronize()
+
+    def timed(fn, *a):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn(*a)
+        e1.record()
+        e1.synchronize()
+        return r, e0.elapsed_time(e1)
+
+    builds = []
+    for rep in range(reps + 1):
+        words = [0] * 8
+        for q in range(G):
+            w = ops[q].alphabet(text[n * q // G: n * (q + 1) // G])
+            words = [x | y for x, y in zip(words, w)]
+        total = torch.zeros(4096, dtype=torch.int64, device=dev)
+        for q in range(G):
+            info, coarse = ops[q].begin(text, n, G, q, words)
+            assert info["status"] == 0, info
+            if G > 1:
+                total += coarse
+        ch = total.cpu() if G > 1 else None
+        cut = [ops[q].cuts(ch) for q in range(G)]
+        sa = [torch.empty(c["m"], dtype=torch.int32, device=dev) for c in cut]
+        rows = [{"rank": q, "m": cut[q]["m"], "sa_off": cut[q]["sa_off"], "round_ms": [], "unsorted": [],
+                 "sent": [], "sent_cross": []} for q in range(G)]
+        for q in range(G):
+            r1, ms = timed(ops[q].round1, sa[q])
+            assert r1["round1_ok"] == 1, (q, r1)
+            rows[q]["round_ms"].append(ms)
+        h = cut[0]["K"]
+        exch = []
+        req = got = ans = back = None
+        while True:
+            cnt, ms_c, uns = [], [], []
+            for q in range(G):
+                (c, info), ms = timed(ops[q].req_count, h, G)
+                cnt.append(c)
+                ms_c.append(ms)
+                uns.append(info["unsorted"])
+            if sum(uns) == 0:
+                break
+            req, ms_f = [], []
+            for q in range(G):
+                r, ms = timed(ops[q].req_fill, h, sum(cnt[q]))
+                req.append(r)
+                ms_f.append(ms)
+            offs = [[sum(cnt[q][:p]) for p in range(G + 1)] for q in range(G)]
+            got = [torch.cat([req[q][offs[q][p]: offs[q][p + 1]] for q in range(G)]) for p in range(G)]
+            ans, ms_a = [], []
+            for p in range(G):
+                a, ms = timed(ops[p].answer, got[p])
+                ans.append(a)
+                ms_a.append(ms)
+            back = []
+            for q in range(G):   # answers to q, in the order of q's requests (owner by owner)
+                parts = []
+                for p in range(G):
+                    a0 = sum(cnt[x][p] for x in range(q))
+                    parts.append(ans[p][a0: a0 + cnt[q][p]])
+                back.append(torch.cat(parts))
+            ms_r = []
+            for q in range(G):
+                _, ms = timed(ops[q].refine, h, back[q], sa[q])
+                ms_r.append(ms)
+            for q in range(G):
+                rows[q]["round_ms"].append(ms_c[q] + ms_f[q] + ms_a[q] + ms_r[q])
+                rows[q]["unsorted"].append(uns[q])
+                rows[q]["sent"].append(sum(cnt[q]))
+                rows[q]["sent_cross"].append(sum(cnt[q][p] for p in range(G) if p != q))
+            pair = max((cnt[q][p] for q in range(G) for p in range(G) if p != q), default=0)
+            exch.append({"h": h, "requests": sum(sum(c) for c in cnt),
+                         "cross": sum(cnt[q][p] for q in range(G) for p in range(G) if p != q),
+                         "max_pair_bytes": 12 * pair})
+            h *= 2
+        builds.append((rows, exch))
+        if rep < reps:
+            del sa, req, got, ans, back
+            torch.cuda.empty_cache()
+    rows, exch = builds[-1]
+    verified = None
+    if check and n <= 0xFFFFFFFF:
+        full = torch.cat(sa)
+        verified = bool(ops[0].b.check(text, n, full))
+        del full
+    # per round: the slowest rank's compute (each on its own GPU); medians
+    # over the timed builds
+    nr = len(rows[0]["round_ms"])
+    per_round = []
+    for j in range(nr):
+        vals = sorted(max(b[0][q]["round_ms"][j] for q in range(G)) for b in builds[1:] or builds)
+        per_round.append(round(vals[len(vals) // 2], 3))
+    out = {"world": G, "n": n, "kind": kind, "rounds": nr, "verified": verified,
+           "m": [r["m"] for r in rows], "share_max": round(max(r["m"] for r in rows) / (n / G), 4),
+           "slowest_rank_ms_per_round": per_round, "compute_ms": round(sum(per_round), 3),
+           "unsorted_per_round": [sum(r["unsorted"][j] for r in rows) for j in range(nr - 1)],
+           "requests_per_round": [e["requests"] for e in exch],
+           "cross_requests_per_round": [e["cross"] for e in exch],
+           "xgmi_bytes_per_round": [12 * e["cross"] for e in exch],
+           "max_pair_bytes_per_round": [e["max_pair_bytes"] for e in exch],
+           "per_rank_round1_ms": [round(r["round_ms"][0], 3) for r in rows]}
+    log(json.dumps(out))
+    for o in ops:
+        o.b.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 30)
@@ -142,8 +285,17 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--all-ranks", action="store_true", help="every rank, not only the first, middle and last")
     ap.add_argument("--check", action="store_true", help="verify the partition and the slices' order")
+    ap.add_argument("--full", action="store_true",
+                    help="play the whole build (later rounds and their exchanges) of every rank per world size")
     ap.add_argument("--json-out", default=None)
     a = ap.parse_args()
+    if a.full:
+        out = [simulate_full(a.n, a.kind, int(G), max(a.reps, 1), log=lambda s: print(s, flush=True))
+               for G in a.worlds.split(",")]
+        if a.json_out:
+            with open(a.json_out, "w") as f:
+                json.dump(out, f, indent=1)
+        return
     out = simulate(a.n, a.kind, [int(x) for x in a.worlds.split(",")], "all" if a.all_ranks else "ends", a.reps,
                    a.check, log=lambda s: print(s, flush=True))
     if a.json_out:

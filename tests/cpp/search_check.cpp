@@ -58,6 +58,43 @@ int main() {
             }
         }
     }
+    // sa::for_each_sample (the local sort's key samples) against a 64-bit
+    // scan, windows ending at and just below 2^32 (n = 2^32, world 1 or a
+    // range build's last range) and random windows
+    {
+        auto check = [&](uint64_t a, uint32_t lo, uint32_t hi, uint32_t ksh) {
+            std::vector<uint64_t> got, want;
+            sa::for_each_sample(a, lo, hi, ksh, [&](uint32_t q) {
+                got.push_back(a + q);
+                if (got.size() > hi - lo + 1) return;
+            });
+            for (uint64_t p = a + lo; p < a + hi; ++p)
+                if ((p & ((1ull << ksh) - 1)) == 0) want.push_back(p);
+            ++cases;
+            if (got != want) {
+                std::printf("for_each_sample mismatch a %llu lo %u hi %u ksh %u: %zu vs %zu samples\n",
+                            (unsigned long long)a, lo, hi, ksh, got.size(), want.size());
+                return false;
+            }
+            return true;
+        };
+        for (uint32_t ksh : {0u, 1u, 4u}) {
+            for (uint32_t w : {1u, 7u, 16u, 17u, 9216u}) {
+                for (uint64_t end : {1ull << 32, (1ull << 32) - 1, (1ull << 32) - 16, (1ull << 32) + 0x1234}) {
+                    for (uint32_t lo : {0u, 1u, w / 2}) {
+                        if (!check(end - w, lo, w, ksh)) return 1;
+                        if (lo < w && !check(end - w, lo, w - 1, ksh)) return 1;
+                    }
+                }
+            }
+            for (int rep = 0; rep < 2000; ++rep) {
+                const uint32_t w = 1 + (uint32_t)(rng() % 9216);
+                const uint64_t a = rng() % ((1ull << 33) - w);
+                const uint32_t lo = (uint32_t)(rng() % (w + 1)), hi = lo + (uint32_t)(rng() % (w - lo + 1));
+                if (!check(a, lo, hi, ksh)) return 1;
+            }
+        }
+    }
     std::printf("ok %ld\n", cases);
     return 0;
 }

@@ -199,3 +199,75 @@ def test_exchange_slice_limit():
     # and the sample-sort fallback's bucket exchange at 2^30 / 8 ranks (2^27
     # int64 per peer) are sliced into 1 and 4 collectives
     assert -(-(1 << 19) // D.XCHUNK) == 1 and -(-(1 << 27) // D.XCHUNK) == 4
+
+
+def _summary_worker(rank, world, port, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    import bench
+    from dist_cpu_ops import CpuRangeOps
+    from hpc_suffix_array_amd.distributed import DistributedSA
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = _texts()["periodic"]
+        d = DistributedSA(CpuRangeOps())
+        d.build(torch.from_numpy(t.copy()), len(t))
+        st = dict(d.stats)
+        # CPU stand-ins have no HIP events: per-rank phase and round-1 kernel
+        # times as a GPU rank would report them (rank 1 the slower)
+        st["phase_ms"] = {"alphabet": 0.1, "round1": 2.0 + rank, "requests": 0.5, "exchange": 0.2}
+        m = st["m"]
+        kern = {"scatter_keys": {"ms": 1.0 + rank, "launches": 1, "bytes": 16 * m},
+                "local_sort": {"ms": 0.5, "launches": 1, "bytes": 12 * m},
+                "scan": {"ms": 5.0, "launches": 3, "bytes": 0}}
+        rec = bench.rank_record(rank, [st], kern)
+        recs = [None] * world
+        dist.all_gather_object(recs, rec)
+        if rank == 0:
+            q.put((recs, bench.distributed_summary(recs, len(t)), len(t)))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bench_distributed_summary_gloo():
+    """bench.py's N > 1 fields (per-rank roofline of the slowest rank's
+    dominant round-1 kernel, per-rank round-1 GB/s, phase times max over
+    ranks, xGMI bytes per later round) from the records of a world-2 gloo
+    build of the range-partitioned driver (the RCCL run gathers the same
+    records with all_gather_object)."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_summary_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    recs, s, n = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert [r["rank"] for r in recs] == [0, 1]
+    assert sum(r["m"] for r in recs) == n and recs[1]["sa_off"] == recs[0]["m"]
+    roof = s["roofline"]
+    m1 = recs[1]["m"]
+    # rank 1 has the slower round 1; its dominant kernel (scan excluded) is
+    # scatter_keys: 16 m bytes in 2.0 ms
+    assert roof["rank"] == 1 and roof["kind"] == "scatter_keys", roof
+    assert roof["bytes_per_launch"] == 16 * m1 and roof["avg_launch_ms"] == 2.0
+    assert abs(roof["achieved"] - 16 * m1 / 2e-3 / 1e9) < 0.1
+    assert abs(roof["frac"] - roof["achieved"] / 8000.0) < 1e-4
+    assert roof["unit"] == "GB/s" and roof["bound"] == "hbm" and roof["peak"] == 8000.0
+    pr = s["round1_per_rank"]
+    assert [x["round1_ms"] for x in pr] == [2.0, 3.0]
+    assert pr[0]["round1_bytes"] == 28 * recs[0]["m"]
+    assert s["kernels_ms_per_step"]["round1"] == 3.0 and s["kernels_ms_per_step"]["requests"] == 0.5
+    assert s["kernels_ms_per_step"]["round1_kernels_slowest_rank"]["scatter_keys"] == 2.0
+    # the periodic text needs later rounds; some look-ups cross ranks
+    cross = s["cross_requests_per_round"]
+    assert len(cross) >= 2 and any(c > 0 for c in cross)
+    assert s["xgmi_bytes_per_round"] == [12 * c for c in cross]
+    assert s["requests_per_round"] == recs[0]["requests"]
+    assert abs(s["largest_rank_share"] - max(r["m"] for r in recs) / (n / 2)) < 1e-3

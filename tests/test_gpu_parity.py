@@ -429,10 +429,15 @@ def _multi_rank_worker(rank, world, port, q, large=False):
         for name, kind, n, seed in (("dna", "dna", 3_000_017, 8), ("byte256", "byte256", 2_000_003, 2),
                                     ("alnum", "alnum", 1_048_576, 1), ("binary", "binary", 1_000_003, 4),
                                     ("periodic", None, 300_000, 11), ("degenerate", None, 70_001, 0),
-                                    ("dna_overflow", "dna", 2_000_003, 9), ("dna_counted", "dna", 2_000_003, 9)):
-            # dna_overflow: record stripes of half their share (the round runs
-            # again with the counting scan); dna_counted: the counting scan
-            ops.b.set_debug({"dna_overflow": ("pad_overflow",), "dna_counted": ("no_pad",)}.get(name, ()))
+                                    ("dna_overflow", "dna", 2_000_003, 9), ("dna_counted", "dna", 2_000_003, 9),
+                                    ("byte256_overflow", "byte256", 2_000_003, 3),
+                                    ("alnum_overflow", "alnum", 1_048_576, 5)):
+            # *_overflow: record stripes of half their share (the round runs
+            # again with the counting scan) -- the packed DNA, the IDENT
+            # (byte256) and the non-power-of-two record kernels; dna_counted:
+            # the counting scan
+            ops.b.set_debug(("pad_overflow",) if name.endswith("_overflow") else
+                            ("no_pad",) if name == "dna_counted" else ())
             if name == "periodic":
                 t = np.tile(O.gen_text("alnum", 1000, seed=seed), 300)
             elif name == "degenerate":
@@ -510,7 +515,8 @@ def _multi_rank(world, large=False):
     # the text unless forced off or overflowed
     listed = world >= 4
     assert res["dna"][3] == ("striped-records" if listed else "exact"), (world, res["dna"])
-    assert res["dna_overflow"][3] == ("striped-records-overflow" if listed else "exact"), (world, res["dna_overflow"])
+    for name in ("dna_overflow", "byte256_overflow", "alnum_overflow"):
+        assert res[name][3] == ("striped-records-overflow" if listed else "exact"), (world, name, res[name])
     assert res["dna_counted"][3] == "exact", (world, res["dna_counted"])
 
 
@@ -838,7 +844,9 @@ def _cfg4_rank(rank, world, port, path, q):
         want = torch.from_numpy(np.array(ref[int(sa_off): int(sa_off) + m])).cuda()   # a writable host copy
         eq = bool((want == sa_local).all().item())
         say("compared", eq)
+        free, _ = torch.cuda.mem_get_info()
         q.put({"rank": rank, "eq": eq, "m": m, "sa_off": int(sa_off), "path": d.stats["path"],
+               "free_gib": free / (1 << 30), "round1_ms": d.stats["phase_ms"].get("round1"),
                "rounds": d.stats["rounds"], "requests": d.stats["requests"],
                "cross": d.stats["cross_requests"], "bucket_bits": d.stats["bucket_bits"]})
     except BaseException:
@@ -851,14 +859,17 @@ def _cfg4_rank(rank, world, port, path, q):
 
 
 @pytest.mark.slow
-def test_config4_cross_rank_rounds_four_ranks(gpu):
+def test_config4_cross_rank_rounds_eight_and_four_ranks(gpu):
     """configs[3]'s range partition end to end at n = 2^31 + 17 byte256 over
-    4 ranks on the box's GPU: round 1 per range and every later round's rank
-    requests and answers exchanged between ranks (sa_dist_req_* /
-    sa_dist_answer / sa_dist_refine and the sliced all-to-alls of
-    distributed.py), each rank's SA slice equal to the O(n)-checked world-1
-    build of the same text (manber_myers_mpi.c:108-144 is the shape
-    replaced; the 8-GPU RCCL run is the driver's)."""
+    8 ranks (configs[3]'s own world size) and then 4 ranks, all on the box's
+    GPU: round 1 per range and every later round's rank requests and answers
+    exchanged between ranks (sa_dist_req_* / sa_dist_answer / sa_dist_refine
+    and the sliced all-to-alls of distributed.py), each rank's SA slice equal
+    to the O(n)-checked world-1 build of the same text
+    (manber_myers_mpi.c:108-144 is the shape replaced; the 8-GPU RCCL run is
+    the driver's).  HBM: ~26 GiB per rank at 8 ranks (text 2 GiB, the
+    n-bit member map and its prefix 0.5 GiB, ~90 B per suffix of the
+    ~2^28-suffix range), ~210 GiB in all."""
     import gc
     import socket
 
@@ -884,30 +895,33 @@ def test_config4_cross_rank_rounds_four_ranks(gpu):
         assert "error" not in ref, ref["error"]
         assert p.exitcode == 0
         assert ref["ok"] and ref["path"] == "range" and ref["m"] == CFG4_N, ref
-        world = 4
-        pt = port()
-        procs = [ctx.Process(target=_cfg4_rank, args=(r, world, pt, path, q)) for r in range(world)]
-        for pr in procs:
-            pr.start()
-        res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x["rank"])
-        for pr in procs:
-            pr.join(timeout=60)
-        errs = [x["error"] for x in res if "error" in x]
-        assert not errs, errs[0]
-        assert all(pr.exitcode == 0 for pr in procs)
-        assert all(x["path"] == "range" for x in res), res
-        assert all(x["eq"] for x in res), [(x["rank"], x["eq"]) for x in res]
-        # the ranges tile the SA in rank order
-        off = 0
-        for x in res:
-            assert x["sa_off"] == off, res
-            off += x["m"]
-        assert off == CFG4_N
-        assert max(x["m"] for x in res) < 1.2 * CFG4_N / world
-        # later rounds with look-ups answered by other ranks: at least two
-        cross = res[0]["cross"]
-        assert sum(1 for c in cross if c > 0) >= 2, res[0]
-        assert res[0]["rounds"] >= 3 and ref["rounds"] >= 3, (res[0], ref)
+        for world in (8, 4):
+            pt = port()
+            procs = [ctx.Process(target=_cfg4_rank, args=(r, world, pt, path, q)) for r in range(world)]
+            for pr in procs:
+                pr.start()
+            res = sorted((q.get(timeout=300) for _ in range(world)), key=lambda x: x["rank"])
+            for pr in procs:
+                pr.join(timeout=60)
+            errs = [x["error"] for x in res if "error" in x]
+            assert not errs, (world, errs[0])
+            assert all(pr.exitcode == 0 for pr in procs)
+            assert all(x["path"] == "range" for x in res), res
+            assert all(x["eq"] for x in res), (world, [(x["rank"], x["eq"]) for x in res])
+            # the ranges tile the SA in rank order
+            off = 0
+            for x in res:
+                assert x["sa_off"] == off, res
+                off += x["m"]
+            assert off == CFG4_N
+            assert max(x["m"] for x in res) < 1.2 * CFG4_N / world, (world, [x["m"] for x in res])
+            # later rounds with look-ups answered by other ranks: at least two
+            cross = res[0]["cross"]
+            assert sum(1 for c in cross if c > 0) >= 2, res[0]
+            assert res[0]["rounds"] >= 3 and ref["rounds"] >= 3, (res[0], ref)
+            print(f"world {world}: m {[x['m'] for x in res]}, rounds {res[0]['rounds']}, cross {cross}, "
+                  f"HBM free after the builds {min(x['free_gib'] for x in res):.1f} GiB, "
+                  f"round1 ms {[x['round1_ms'] for x in res]}", flush=True)
     finally:
         if os.path.exists(path):
             os.remove(path)
