@@ -48,7 +48,7 @@ class SAError(RuntimeError):
 # sa_opts.debug flags (include/sa_hip.h SA_DEBUG_*): alternative paths the
 # tests force; every combination gives the same suffix array
 DEBUG_FLAGS = {"no_cmp": 0x1, "no_pk8": 0x2, "no_pad": 0x4, "pad_overflow": 0x8, "no_fast32": 0x10,
-               "no_pivot": 0x20, "perm_always": 0x40}
+               "no_pivot": 0x20, "perm_always": 0x40, "no_xq": 0x80, "xq_overflow": 0x100}
 
 
 def debug_bits(names) -> int:
@@ -112,7 +112,8 @@ class SaStats(ctypes.Structure):
             "largest_window": self.largest_window,
             "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow", 3: "striped-records",
                                 4: "striped-records-overflow"}.get(self.round1_segments, "exact"),
-            "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2)},
+            "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2),
+                              "xq": bool(self.round1_layout & 4)},
             "model_bytes": int(self.model_bytes),
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},

@@ -178,6 +178,7 @@ constexpr uint32_t kCoarse = 1u << kCoarseBits;
 // DNA (POW2): the text's alphabet is exactly {A, C, G, T}: dense digits by
 // ((b >> 1) ^ (b >> 2)) & 3 per byte, four at once (as k_split_text)
 constexpr uint32_t kRecStripes = 64;
+constexpr uint32_t kXq = 8;   // second-pass queues = XCDs (sa_split.h SegXq, XqWin below)
 constexpr uint32_t kRecCurStride = 64;   // words between stripe cursors (atomics on one line serialise)
 // record slots of a range of m suffixes: the striped regions' 1/8 margin and
 // two tiles of slack per stripe
@@ -1538,10 +1539,15 @@ constexpr int kTicketWord = 15;                // words[]: k_bucket_sort's windo
 
 // listed windows -> one-bucket windows with headers {j, a, m, Dmin} (fast:
 // the fixed-span kernel runs) or the retry list (k_bucket_sort_wide)
+// XQ (pc / pn: the per-region chunk starts and counts of k_bucket_starts_xq,
+// [kXq][nb]): each one-bucket window's chunk header hx (load_items_xq).
 __global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restrict__ list,
                                                          const uint32_t* __restrict__ ws, BucketRel br,
                                                          uint32_t* __restrict__ words, uint4* __restrict__ hdr,
-                                                         uint32_t* __restrict__ retry, uint32_t fast) {
+                                                         uint32_t* __restrict__ retry, uint32_t fast,
+                                                         const uint32_t* __restrict__ pc = nullptr,
+                                                         const uint32_t* __restrict__ pn = nullptr, uint32_t nb = 0,
+                                                         uint32_t* __restrict__ hx = nullptr) {
     const uint32_t nlist = words[7];
     const uint32_t lane = lane_id();
     for (uint64_t q0 = (uint64_t)blockIdx.x * kBlock; q0 < nlist; q0 += (uint64_t)gridDim.x * kBlock) {
@@ -1564,9 +1570,47 @@ __global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restr
         base2 = (uint32_t)__shfl((int)base2, 0, kWave);
         if (ok && one) {
             const uint32_t a = ws[j];
-            hdr[base1 + (uint32_t)__popcll(m1 & lanemask_lt())] = make_uint4(j, a, ws[j + 1] - a, br.bdmin[b0]);
+            const uint32_t qi = base1 + (uint32_t)__popcll(m1 & lanemask_lt());
+            hdr[qi] = make_uint4(j, a, ws[j + 1] - a, br.bdmin[b0]);
+            if (hx) {
+                uint32_t P = 0;
+                for (uint32_t k = 0; k < kXq; ++k) {
+                    const uint32_t c = pc[(uint64_t)k * nb + b0];
+                    hx[(uint64_t)qi * 16 + k] = c - P;
+                    if (k) hx[(uint64_t)qi * 16 + kXq - 1 + k] = P;
+                    P += pn[(uint64_t)k * nb + b0];
+                }
+            }
         } else if (ok) {
             retry[base2 + (uint32_t)__popcll(m2 & lanemask_lt())] = j;
+        }
+    }
+}
+
+// XQ: the windows listed for k_bucket_sort_wide (by k_window_split: more
+// than one bucket; by k_bucket_sort: keys that cluster) copied from their
+// chunks in the per-XCD regions to their SA positions in `out` (which the
+// wide / LSD window kernels then read), one workgroup per window; the chunks
+// of bucket b in region k are [pc[k][b], pc[k][b] + pn[k][b]).
+__global__ __launch_bounds__(kBlock) void k_window_gather(const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ words,
+                                                          const uint32_t* __restrict__ ws,
+                                                          const uint32_t* __restrict__ wb,
+                                                          const uint32_t* __restrict__ pc,
+                                                          const uint32_t* __restrict__ pn, uint32_t nb,
+                                                          const uint64_t* __restrict__ in,
+                                                          uint64_t* __restrict__ out) {
+    const uint32_t nlist = words[kRetryWord];
+    for (uint32_t qi = blockIdx.x; qi < nlist; qi += gridDim.x) {
+        const uint32_t j = list[qi];
+        uint64_t dst = ws[j];
+        for (uint32_t b = wb[j]; b < wb[j + 1]; ++b) {
+            for (uint32_t k = 0; k < kXq; ++k) {
+                const uint32_t c = pn[(uint64_t)k * nb + b];
+                const uint64_t src = pc[(uint64_t)k * nb + b];
+                for (uint32_t t = threadIdx.x; t < c; t += kBlock) out[dst + t] = in[src + t];
+                dst += c;
+            }
         }
     }
 }
@@ -1628,18 +1672,98 @@ __device__ __forceinline__ void load_items(const uint64_t* __restrict__ w_in, ui
     }
 }
 
+// XQ windows (sa_split.h k_split_seg<.., XQ>): a one-bucket window's items
+// are its bucket's chunks in the 8 per-XCD regions of the second pass's
+// output.  Its header hx (16 words, k_window_split) holds, for chunk k,
+// d[k] = (chunk start) - P_k and P_1..P_7 (P_k: the window slots before
+// chunk k), so slot le reads w_in[d[k] + le] for the last k with P_k <= le.
+// Its row table (k_window_rows) holds one word per row r of 64 slots (wave
+// r / ITEMS, item r % ITEMS): d[k] of the row's chunk, or kXqCross when the
+// row crosses a chunk boundary (at most 7 of a window's rows; those lanes
+// search hx).  The local sort copies the next window's row table and header
+// into LDS while it sorts the current one, so the next window's loads (the
+// prefetch) cost an LDS read and an add per item, as contiguous items do.
+// (Reading the table from memory at the prefetch point put a round trip in
+// front of every load: local sort 3.5 -> 6.1 ms.)
+struct XqWin {
+    const uint32_t* __restrict__ hx = nullptr;     // [hdr index][16]
+    const uint32_t* __restrict__ rows = nullptr;   // [hdr index][rows per window]
+};
+constexpr uint32_t kXqCross = 0xFFFFFFFFu;   // (an offset is C_k - P_k with C_k >= P_k, never ~0)
+
+// window slot le of chunk k: the last k with P_k <= le (P_0 = 0)
+__device__ __forceinline__ uint32_t xq_offset(const uint32_t* __restrict__ hx, uint32_t le) {
+    uint32_t off = hx[0];
+#pragma unroll
+    for (int k = 1; k < (int)kXq; ++k) off = hx[kXq - 1 + k] <= le ? hx[k] : off;
+    return off;
+}
+
+// a row that crosses a chunk boundary (rare: at most 7 of a window's 144
+// rows), out of line so that its header reads do not stay live across the
+// inlined loads of the other rows
+__device__ __noinline__ uint64_t xq_cross_load(const uint64_t* __restrict__ w_in, const uint32_t* s_h, uint32_t lc) {
+    return w_in[(uint32_t)(xq_offset(s_h, lc) + lc)];
+}
+
+// s_rw: this wave's ITEMS row words, s_h: the window's header (both LDS)
+template <int ITEMS>
+__device__ __forceinline__ void load_items_xq(const uint64_t* __restrict__ w_in, const uint32_t* s_rw,
+                                              const uint32_t* s_h, uint32_t m, uint64_t (&x)[ITEMS]) {
+    const uint32_t l0 = slot0<ITEMS>();
+    const uint32_t last = m - 1;
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t le = l0 + i * kWave;
+        const uint32_t lc = le < m ? le : last;
+        // the row's offset is uniform: a scalar base and the lane's slot
+        const uint32_t off = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_rw[i]);
+        if (off == kXqCross)   // uniform: the row crosses a chunk boundary
+            x[i] = xq_cross_load(w_in, s_h, lc);
+        else
+            x[i] = (w_in + off)[lc];
+    }
+}
+
+// The row tables of the XQ one-bucket windows (k_window_split's headers
+// words[kHdrWord], hx), one wave per window: row r covers slots [64 r,
+// min(64 r + 63, m - 1)] (slots past m re-read item m - 1).
+__global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restrict__ words, const uint4* __restrict__ hdr,
+                                                        const uint32_t* __restrict__ hx, uint32_t nrows,
+                                                        uint32_t* __restrict__ rows) {
+    const uint32_t nh = words[kHdrWord];
+    const uint32_t lane = lane_id();
+    for (uint64_t q = (uint64_t)blockIdx.x * kWaves + wave_id(); q < nh; q += (uint64_t)gridDim.x * kWaves) {
+        const uint32_t m = hdr[q].z;
+        const uint32_t* const h = hx + q * 16;
+        uint32_t hv[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k) hv[k] = h[k];
+        for (uint32_t r = lane; r < nrows; r += kWave) {
+            const uint32_t lo = std::min(r * kWave, m - 1), hi = std::min(r * kWave + (kWave - 1), m - 1);
+            uint32_t klo = 0, khi = 0;
+#pragma unroll
+            for (int k = 1; k < (int)kXq; ++k) {
+                klo += hv[kXq - 1 + k] <= lo ? 1u : 0u;
+                khi += hv[kXq - 1 + k] <= hi ? 1u : 0u;
+            }
+            rows[q * nrows + r] = klo == khi ? xq_offset(hv, lo) : kXqCross;
+        }
+    }
+}
+
 // bits: the plan's key span (br.bits1), kSubBits < bits <= kSubBits + kLowMax
 // SA_LS_WFULL: waves whose slots all lie inside the window take the
 // histogram, scatter and store loops without per-item bounds tests
 #ifndef SA_LS_WFULL
 #define SA_LS_WFULL 1
 #endif
-template <int BLOCK, int ITEMS, class Probe = NoProbe>
+template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
                                                        uint32_t ib, uint32_t* __restrict__ words,
                                                        uint64_t* __restrict__ keys_out, uint32_t* __restrict__ sa_out,
-                                                       uint32_t* __restrict__ retry, SegOut so) {
+                                                       uint32_t* __restrict__ retry, SegOut so, XqWin xw = XqWin{}) {
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     static_assert(CAP <= (1 << kSlotBits), "load slots");
@@ -1653,6 +1777,11 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     __shared__ unsigned long long s_tot[3];   // heads, U, U groups of the workgroup's windows (thread 0)
     constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
     static_assert(WPT * 2 == 4 && WPT * 2 * BLOCK == kSubBuckets, "four sub-buckets per thread");
+    // XQ: row tables + headers of the current and the next window (load_items_xq)
+    constexpr int ROWS = WAVES * ITEMS;
+    constexpr int XRW = ROWS + 16;
+    static_assert(!XQ || XRW <= BLOCK, "one thread per row word");
+    __shared__ uint32_t s_xr[XQ ? 2 * XRW : 1];
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -1673,7 +1802,14 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     if (q >= nwin) return;   // uniform
     uint4 h = hdr[q];
     uint64_t w[ITEMS];
-    load_items<ITEMS>(keys_in, h.y, h.z, w);
+    if constexpr (XQ) {
+        if (dg < (uint32_t)XRW)
+            s_xr[dg] = dg < (uint32_t)ROWS ? xw.rows[(uint64_t)q * ROWS + dg] : xw.hx[(uint64_t)q * 16 + dg - ROWS];
+        __syncthreads();
+        load_items_xq<ITEMS>(keys_in, s_xr + wave * ITEMS, s_xr + ROWS, h.z, w);
+    } else {
+        load_items<ITEMS>(keys_in, h.y, h.z, w);
+    }
     uint32_t par = 0;
     for (;;) {
         probe.mark(-1);
@@ -1691,6 +1827,16 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         // the scatter (a conditional one kept them live through the sort)
         uint4 hn = make_uint4(0u, 0u, 1u, 0u);
         if (more) hn = hdr[qn];
+        // XQ: the next window's row table and header word of this thread
+        // (past the last window: the current one's), into LDS after the
+        // histogram, read at the prefetch point
+        uint32_t xr_next = 0;
+        if constexpr (XQ) {
+            const uint64_t qx = more ? qn : q;
+            if (dg < (uint32_t)XRW)
+                xr_next = dg < (uint32_t)ROWS ? xw.rows[qx * ROWS + dg] : xw.hx[qx * 16 + dg - ROWS];
+        }
+        const uint32_t* const s_xn = s_xr + (par ^ 1u) * XRW;
         probe.mark(0);
         const uint32_t l0 = slot0<ITEMS>();
         // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
@@ -1709,6 +1855,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                     atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
                 }
             }
+        }
+        if constexpr (XQ) {
+            if (dg < (uint32_t)XRW) s_xr[(par ^ 1u) * XRW + dg] = xr_next;
         }
         __syncthreads();
         probe.mark(1);
@@ -1753,9 +1902,12 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         __syncthreads();
         probe.mark(2);
         if (big > kMaxSub) {   // uniform: clustered keys -> the measured-span kernel
+            // (XQ: k_window_gather copies the retried windows to their SA
+            // positions for it; storing the items here made this kernel spill)
             if (threadIdx.x == 0) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
             __builtin_amdgcn_sched_barrier(0);
-            load_items<ITEMS>(keys_in, hn.y, hn.z, w);
+            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, s_xn + wave * ITEMS, s_xn + ROWS, hn.z, w);
+            else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
         } else {
             // 2. scatter the 32-bit words into sub-buckets (any order inside
@@ -1780,7 +1932,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // scheduling barrier: hoisted above the scatter, they would hold
             // a second window of registers)
             __builtin_amdgcn_sched_barrier(0);
-            load_items<ITEMS>(keys_in, hn.y, hn.z, w);
+            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, s_xn + wave * ITEMS, s_xn + ROWS, hn.z, w);
+            else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
             probe.mark(3);
             // ... then each thread sorts its four consecutive sub-buckets,

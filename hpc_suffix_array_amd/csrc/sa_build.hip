@@ -125,6 +125,9 @@ struct sa_context {
     uint32_t* u_idx[2] = {nullptr, nullptr};
     uint32_t* u_g[2] = {nullptr, nullptr};
     uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
+    uint64_t kucap = 0;                         // keys_u capacity (items): ucap + the XQ regions' slack
+    uint32_t* segx = nullptr;                   // second bucket pass, per-XCD queues (sa_split.h SegXq) + tables
+    uint64_t segx_words = 0;
     uint32_t* os = nullptr;                     // onesweep ghist / digit bases / tickets
     uint32_t* lsd = nullptr;                    // k_lsd ghist [8][1024] | bases [8][1024] | tickets [8]
     uint32_t* segw = nullptr;                   // second bucket pass: per-segment cursors / bases / flags
@@ -206,6 +209,7 @@ static void free_u_buffers(sa_context* c) {
         c->u_pos[i] = c->u_idx[i] = c->u_g[i] = nullptr;
     }
     c->ucap = 0;
+    c->kucap = 0;
 }
 
 // sa_opts debug / tune fields -> the context (NULL: production defaults)
@@ -244,7 +248,12 @@ static int ensure_u_capacity(sa_context* c, uint64_t n) {
     SA_HIP(hipSetDevice(c->device));
     free_u_buffers(c);
     const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64) * 4;
-    bool ok = hipMalloc(&c->vals_u, m) == hipSuccess && hipMalloc(&c->keys_u, 2 * m) == hipSuccess &&
+    // keys_u also holds the second bucket pass's per-XCD regions (sa_split.h
+    // SegXq): n items plus each (queue, digit) sub-region's slack, at most
+    // n / 16 + 8 * 1024 * kXqSlack items (padded first-pass sizes only)
+    const uint64_t ku = align_up(std::max<uint64_t>(n, 1), 64) +
+                        (n >= (1ull << 26) ? n / 16 + 8ull * 1024 * kXqSlack + 64 : 0);
+    bool ok = hipMalloc(&c->vals_u, m) == hipSuccess && hipMalloc(&c->keys_u, 8 * ku) == hipSuccess &&
               hipMalloc(&c->member, align_up(n, 1024) / 8) == hipSuccess;
     for (int i = 0; i < 2 && ok; ++i)
         ok = hipMalloc(&c->u_pos[i], m) == hipSuccess && hipMalloc(&c->u_idx[i], m) == hipSuccess &&
@@ -255,6 +264,7 @@ static int ensure_u_capacity(sa_context* c, uint64_t n) {
         return set_err(SA_E_NOMEM, "device allocation of the unsorted-set buffers failed");
     }
     c->ucap = n;
+    c->kucap = ku;
     SA_TRACE("unsorted-set buffers: vals_u %p keys_u %p", (void*)c->vals_u, (void*)c->keys_u);
     return SA_OK;
 }
@@ -1578,6 +1588,7 @@ void sa_context_destroy(sa_context* c) {
     hipFree(c->os);
     hipFree(c->lsd);
     hipFree(c->segw);
+    hipFree(c->segx);
     hipFree(c->hist);
     hipFree(c->totals);
     hipFree(c->counts);

@@ -39,6 +39,10 @@
 #ifndef SA_SEG_BLOCK
 #define SA_SEG_BLOCK 1024
 #endif
+// second bucket pass by per-XCD queues and regions (sa_split.h SegXq)
+#ifndef SA_SEG_XQ
+#define SA_SEG_XQ 1
+#endif
 #ifndef SA_ITEMS_B
 #define SA_ITEMS_B 10
 #endif
@@ -228,7 +232,7 @@ static uint32_t range_hb(uint32_t nb) {
 // segments() on keys[0].
 static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, const BucketPlan& bp,
                            const BucketRange& br_, hipStream_t s, Timer& tm, sa_stats* st, bool* done, bool* fused,
-                           uint64_t seg[3], uint32_t* ksh, bool allow_pad = true) {
+                           uint64_t seg[3], uint32_t* ksh, bool allow_pad = true, bool allow_xq = true) {
     *done = false;
     *fused = false;
     *ksh = 0;
@@ -330,7 +334,8 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             if (c->host_words[11]) {
                 SA_TRACE("  bucketed round 1: a record stripe overflowed, again with the counting scan");
                 tm.end();
-                const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false);
+                const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false,
+                                               allow_xq);
                 if (st) st->round1_segments = 4;
                 return rc;
             }
@@ -357,7 +362,52 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
     const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
     const bool pk8 = plan_pk8(bp, hb, c->dbg);
-    if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0);
+    // the local sort's key span: a one-bucket window's keys fill bits1 bits
+    // (compact layout); 0 = measured per window
+    uint32_t bits1 = 0;
+    if (bp.bs.cmp) {
+        const uint64_t ps = bp.bs.pow_s1 * bp.bs.sigma, per = (ps + (1ull << bp.bs.bb) - 1) >> bp.bs.bb;
+        bits1 = bit_width(per - 1) + bp.bs.rb;
+        // tests: a span wider than the keys' (they cluster in the low
+        // sub-buckets), so every window takes the measured-span recount
+        if (c->span_extra > 0) bits1 = std::min<uint32_t>(bits1 + (uint32_t)c->span_extra, 64u - bp.ib);
+    }
+    // the fixed-span 32-bit local sort (k_bucket_sort): the key bits below a
+    // sub-bucket fit beside the load slot, and buckets are large enough that
+    // windows hold one bucket each (suffixes per bucket of the range >= 4
+    // window strides; a rank's range holds m suffixes in bhi - blo buckets --
+    // m >> bb undercounted them by G, and ranges took k_bucket_sort_wide)
+    const bool fast32 = bits1 > (uint32_t)kSubBits && bits1 - kSubBits <= kLowMax &&
+                        m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !(c->dbg & SA_DEBUG_NO_FAST32);
+    // the second pass by per-XCD queues and regions (sa_split.h SegXq): one
+    // GPU's padded round (n >= 2^26: the regions' slack is in keys_u), the
+    // fixed-span local sort (which loads a one-bucket window's 8 chunks), a
+    // grid of whole XCDs
+    const bool xq = SA_SEG_XQ && allow_xq && padded && fast32 && c->cus % (int)kXq == 0 &&
+                    !(c->dbg & SA_DEBUG_NO_XQ) && c->kucap >= n + n / 16 + 8ull * 1024 * kXqSlack;
+    if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0);
+    // XQ workspace: queue cursors / bases / claim counts / tickets, the digit
+    // sub-region starts, the per-region chunk starts and counts per bucket
+    const uint64_t xqw = xq_words(1u << hb);
+    uint32_t* xq_dh = nullptr;
+    uint32_t* xq_pc = nullptr;
+    uint32_t* xq_pn = nullptr;
+    if (xq) {
+        const uint64_t need = xqw + 1032 + 2ull * kXq * nb_tab;
+        if (c->segx_words < need) {
+            hipFree(c->segx);
+            c->segx = nullptr;
+            c->segx_words = 0;
+            if (hipMalloc(&c->segx, need * 4) != hipSuccess) {
+                (void)hipGetLastError();
+                return set_err(SA_E_NOMEM, "second-pass queue workspace (%llu words)", (unsigned long long)need);
+            }
+            c->segx_words = need;
+        }
+        xq_dh = c->segx + xqw;
+        xq_pc = xq_dh + 1032;
+        xq_pn = xq_pc + (uint64_t)kXq * nb_tab;
+    }
     // os layout: ghist [0, kLoRadix) low totals, [kLoRadix, +2^hb) high
     // totals, [1280, +kLoRadix) the first pass's cursors; base [0, kLoRadix)
     // low, [kLoRadix, +2^hb) high
@@ -431,6 +481,9 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_SCAN);   // the second pass's digit totals came from the first
     hipLaunchKernelGGL(k_digit_base_wide, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
                        os_base(c) + kLoRadix);
+    if (xq)   // the digits' sub-regions of each queue's region
+        hipLaunchKernelGGL(k_xq_dh, dim3(1), dim3(1024), 0, s, (const uint32_t*)g_hi, 1u << hb,
+                           (c->dbg & SA_DEBUG_XQ_OVERFLOW) ? 1u : 0u, xq_dh);
     // padded: the dense segment starts from the first pass's final cursors
     if (padded) {
         if (stripes > 1)
@@ -448,20 +501,38 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         uint32_t* tk = os_tickets(c) + 1;
         const uint32_t* hbase = os_base(c) + kLoRadix;
         SA_HIP(hipMemsetAsync(c->segw, 0, segw_words(1u << hb) * 4, s));   // <= 3 MiB
+        SegXq sx;
+        if (xq) {
+            SA_HIP(hipMemsetAsync(c->segx, 0, xqw * 4, s));   // <= 25 MiB
+            sx.cur = c->segx;
+            sx.sbase = reinterpret_cast<uint64_t*>(c->segx + (uint64_t)kXq * kSegs * (1u << hb));
+            sx.done = c->segx + 3ull * kXq * kSegs * (1u << hb);
+            sx.tickets = sx.done + kXq * kSegs;
+            sx.dh = xq_dh;
+            sx.err2 = c->words + 9;
+            sx.cap = (uint32_t)std::min<uint64_t>(c->kucap, UINT32_MAX);
+        }
         // workgroups of kSegBlock threads (1024 / kSegBlock per CU) for radices up to 512
         constexpr int kSegBlock = SA_SEG_BLOCK;
         const int sblk = hb <= 9 ? kSegBlock : kSpBlock;
         const uint64_t ut = (uint64_t)sblk * (pk8 ? kItemsPk : kItemsB);
         const uint64_t units = (m + ut - 1) / ut + kSegs;
-        const uint32_t grid = (uint32_t)std::max<uint64_t>(
-            1, std::min<uint64_t>(units, (uint64_t)c->cus * (kSpBlock / sblk)));
+        const uint32_t grid = xq ? (uint32_t)c->cus * (kSpBlock / sblk)   // whole XCDs
+                                 : (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(units, (uint64_t)c->cus * (kSpBlock / sblk)));
         switch (hb) {
 #define SA_SEG_LAUNCH(S, B, SRC, SH, IT)                                                                      \
-    hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock)>), dim3(grid),                    \
-                       dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                                  \
-                       (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,          \
-                       c->words + 4, padded ? (const uint32_t*)cursor : nullptr, padded ? (const uint32_t*)dlo : nullptr, \
-                       stripes)
+    if (xq)                                                                                                   \
+        hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock), true>), dim3(grid),        \
+                           dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                              \
+                           (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,      \
+                           c->words + 4, padded ? (const uint32_t*)cursor : nullptr,                           \
+                           padded ? (const uint32_t*)dlo : nullptr, stripes, sx);                              \
+    else                                                                                                      \
+        hipLaunchKernelGGL((k_split_seg<S, B, IT, (B <= 9 ? kSegBlock : kSpBlock)>), dim3(grid),                \
+                           dim3(B <= 9 ? kSegBlock : kSpBlock), 0, s, SRC, m, SH,                              \
+                           (const uint32_t*)(padded ? pstart : os_base(c)), hbase, c->segw, tk, bp.ib, c->keys_u,      \
+                           c->words + 4, padded ? (const uint32_t*)cursor : nullptr,                           \
+                           padded ? (const uint32_t*)dlo : nullptr, stripes)
 #define SA_SEG_PASS(B)                                                                                        \
     case B:                                                                                                   \
         if (pk8) SA_SEG_LAUNCH(SrcPk8, B, sp, 64u - B, kItemsPk);                                             \
@@ -481,8 +552,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         uint32_t* bstart = c->segw + kBstartOff;
         uint32_t* bdmin = bstart + kBstartWords;
 #define SA_BSTARTS(R)                                                                                         \
-    hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)(padded ? dlo : os_base(c)), hbase, \
-                       (const uint32_t*)c->segw, m, bp.bs.cmul, bp.bs.bsh, bstart, bdmin, blo)
+    if (xq)                                                                                                   \
+        hipLaunchKernelGGL(k_bucket_starts_xq<R>, dim3(R), dim3(kLoRadix), 0, s, hbase, (const uint32_t*)sx.cur, \
+                           (const uint32_t*)xq_dh, m, bp.bs.cmul, bp.bs.bsh, bstart, bdmin, xq_pc, xq_pn, blo); \
+    else                                                                                                      \
+        hipLaunchKernelGGL(k_bucket_starts<R>, dim3(gb), dim3(kBlock), 0, s, (const uint32_t*)(padded ? dlo : os_base(c)), \
+                           hbase, (const uint32_t*)c->segw, m, bp.bs.cmul, bp.bs.bsh, bstart, bdmin, blo)
         switch (hb) {
             case 7: SA_BSTARTS(128); break;
             case 8: SA_BSTARTS(256); break;
@@ -514,9 +589,13 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
     if (padded && c->host_words[11]) {   // a digit outgrew its sampled segment: exact totals
         SA_TRACE("  bucketed round 1: padded segment overflow, again with exact digit totals");
-        const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false);
+        const int rc = round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, false, allow_xq);
         if (st) st->round1_segments = 2;
         return rc;
+    }
+    if (xq && c->host_words[9]) {   // a queue's digit outgrew its sub-region: one region
+        SA_TRACE("  bucketed round 1: second-pass queue overflow, again with one region");
+        return round1_bucketed(c, d_text, n, d_sa, bp, br_, s, tm, st, done, fused, seg, ksh, allow_pad, false);
     }
     if (st) st->largest_window = (int32_t)std::min<uint32_t>(c->host_words[5], INT32_MAX);
     if (c->host_words[5] > (uint32_t)kBsCap) {
@@ -535,13 +614,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // alphabets whose buckets fill ~80 % of that span (1 GiB alnum / ascii127
     // local sort 7.05 / 6.85 ms with measured spans, 4.75 / 4.56 with the
     // fixed one: profiles/r02_av_ab_kinds_fixed_span_pow2_only.txt)
-    if (bp.bs.cmp) {
-        const uint64_t ps = bp.bs.pow_s1 * bp.bs.sigma, per = (ps + (1ull << bp.bs.bb) - 1) >> bp.bs.bb;
-        br.bits1 = bit_width(per - 1) + bp.bs.rb;
-        // tests: a span wider than the keys' (they cluster in the low
-        // sub-buckets), so every window takes the measured-span recount
-        if (c->span_extra > 0) br.bits1 = std::min<uint32_t>(br.bits1 + (uint32_t)c->span_extra, 64u - bp.ib);
-    }
+    br.bits1 = bits1;
     SA_HIP(hipMemsetAsync(cnt_u, 0, (2 * nw + 2) * 4, s));
     uint32_t* const rank_arr = br_.rank ? br_.rank : c->rank;
     uint32_t* const member = br_.member ? br_.member : c->member;
@@ -556,15 +629,15 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t* const retry = cnt_g + 2 * nw + 2;
     BucketRel br_measured = br;
     br_measured.bits1 = 0;
-    // the fixed-span 32-bit local sort (k_bucket_sort): the key bits below a
-    // sub-bucket fit beside the load slot, and buckets are large enough that
-    // windows hold one bucket each (suffixes per bucket of the range >= 4
-    // window strides; a rank's range holds m suffixes in bhi - blo buckets --
-    // m >> bb undercounted them by G, and ranges took k_bucket_sort_wide)
-    const bool fast32 = br.bits1 > (uint32_t)kSubBits && br.bits1 - kSubBits <= kLowMax &&
-                        m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !(c->dbg & SA_DEBUG_NO_FAST32);
     // one-bucket window headers after the retry list (16-byte aligned; 11 nw + 8 <= capacity)
     uint4* const hdr = reinterpret_cast<uint4*>(((uintptr_t)(retry + nw + 4) + 15) & ~(uintptr_t)15);
+    // XQ: the one-bucket windows' chunk headers after them (16 words each; 27 nw + 8 <= capacity), and the
+    // windows for the measured-span / LSD kernels at their SA positions in keys[1] (free in the bucketed round)
+    uint32_t* const hx = xq ? reinterpret_cast<uint32_t*>(hdr + nw + 1) : nullptr;
+    // and their row tables (3 kBsRows words each; 27 nw + 432 (nw + 1) + 24 <= capacity)
+    constexpr uint32_t kBsRows = (kBsBlock / kWave) * kBsItems;
+    uint32_t* const xrows = xq ? hx + 16 * (nw + 1) : nullptr;
+    const uint64_t* const wide_in = xq ? c->keys[1] : c->keys_u;
     auto local_sort = [&](const SegOut& o) {
         const uint32_t g = std::max<uint32_t>(1, std::min(c->host_words[7], kBsGrid));
         // (no SA_HIP here: its error return would make the lambda non-void)
@@ -572,10 +645,27 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         if (fast32) {
             const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024));
             hipLaunchKernelGGL(k_window_split, dim3(gs), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)ws,
-                               br, c->words, hdr, retry, 1u);
-            hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(kBsWpc * (uint32_t)c->cus), dim3(kBsBlock), 0, s,
-                               (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1, bp.ib, c->words,
-                               c->keys[0], d_sa, retry, o);
+                               br, c->words, hdr, retry, 1u, (const uint32_t*)xq_pc, (const uint32_t*)xq_pn, nb_tab, hx);
+            if (xq) {
+                hipLaunchKernelGGL(k_window_rows, dim3(2048), dim3(kBlock), 0, s, (const uint32_t*)c->words,
+                                   (const uint4*)hdr, (const uint32_t*)hx, kBsRows, xrows);
+                XqWin xw;
+                xw.hx = hx;
+                xw.rows = xrows;
+                hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, true>), dim3(kBsWpc * (uint32_t)c->cus),
+                                   dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb,
+                                   br.bits1, bp.ib, c->words, c->keys[0], d_sa, retry, o, xw);
+                // the windows for the measured-span kernel (several buckets, or
+                // clustered keys), from their chunks to their SA positions
+                hipLaunchKernelGGL(k_window_gather, dim3(1024), dim3(kBlock), 0, s, (const uint32_t*)retry,
+                                   (const uint32_t*)c->words, (const uint32_t*)ws, (const uint32_t*)br.wb,
+                                   (const uint32_t*)xq_pc, (const uint32_t*)xq_pn, nb_tab, (const uint64_t*)c->keys_u,
+                                   c->keys[1]);
+            } else {
+                hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(kBsWpc * (uint32_t)c->cus), dim3(kBsBlock),
+                                   0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1, bp.ib,
+                                   c->words, c->keys[0], d_sa, retry, o);
+            }
         } else {
             hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,
                                (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)list, c->words,
@@ -583,14 +673,14 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         }
         if (br.bits1)   // rare: a small grid loops over the retried windows (measured span)
             hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(std::min<uint32_t>(g, 1024)),
-                               dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, br_measured, (const uint32_t*)ws,
+                               dim3(kBsBlock), 0, s, wide_in, br_measured, (const uint32_t*)ws,
                                (const uint32_t*)retry, c->words, bp.ib, c->keys[0], d_sa, skew, o, (uint32_t*)nullptr,
                                (uint32_t)kRetryWord);
         // skewed windows are rare: a small grid loops over them (one
         // workgroup per listed window spent 0.1 ms on empty workgroups)
         const uint32_t gl = std::min<uint32_t>(g, 1024);
         hipLaunchKernelGGL((k_bucket_sort_lsd<kBsBlock, kBsItems>), dim3(gl), dim3(kBsBlock), 0, s,
-                           (const uint64_t*)c->keys_u, br, (const uint32_t*)ws, (const uint32_t*)skew, c->words, bp.ib,
+                           wide_in, br, (const uint32_t*)ws, (const uint32_t*)skew, c->words, bp.ib,
                            c->keys[0], d_sa, o);
     };
     tm.begin(SA_K_LOCAL_SORT);

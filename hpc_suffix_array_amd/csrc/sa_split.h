@@ -914,7 +914,41 @@ constexpr uint64_t kBstartWords = (1ull << 18) + 1;
 // and the next unit's loads split around the staging: 5.72 / 4.94 / 4.89 ms
 // against 4.68-4.95 -- although 32-item runs write faster than 24-item ones
 // in isolation (microbench_runs.hip, profiles/r04_e_microbench_runs.txt).
-template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock>
+// ---------------------------------------------------------------------------
+// XQ: per-XCD queues and output regions (round 5).  Workgroup w runs on XCD
+// w mod 8 (workgroups are dealt to the 8 XCDs round robin), so queue q =
+// w mod 8 takes the units u = 8 t + q from its own ticket, and its units'
+// items go to region q of the output: region q is in bucket order (h, l)
+// over queue q's items only, each digit h in a sub-region of capacity
+// cap(h) = tot(h) / 8 + tot(h) / 128 + kXqSlack (a queue holds every 8th
+// unit of every segment, so its share of a digit is tot(h) / 8 within a few
+// hundred items on any text whose digit-h items spread over the units).
+// Every queue keeps its own cursors, bases and segment chain: a unit waits
+// only for units of its own queue, and the runs that end next to one
+// another in a sub-region were written by the same XCD, whose L2 merges the
+// partial lines at their ends -- the write pattern that held the pass at
+// 0.46 of the HBM peak (microbench_seg.hip: one region 4.97 ms, per-XCD
+// regions 3.61 ms at 2^30 items, profiles/r05_b_microbench_seg.txt).  A
+// queue whose digit outgrows its sub-region sets words[9] (err2); the round
+// then runs the pass again without XQ.  k_bucket_starts_xq derives the
+// exact bucket starts and each bucket's chunk per region; the local sort
+// loads a one-bucket window from its 8 chunks.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kXqSlack = 2048;     // per (queue, digit) sub-region slack
+constexpr uint32_t kXqTicketStride = 32;   // one 128-byte line per queue ticket
+struct SegXq {
+    uint32_t* cur = nullptr;           // [kXq][kSegs][RADIX] claim cursors
+    uint64_t* sbase = nullptr;         // [kXq][kSegs][RADIX] published bases (bit 32: ready)
+    uint32_t* done = nullptr;          // [kXq][kSegs] claims per segment
+    uint32_t* tickets = nullptr;       // [kXq] at kXqTicketStride
+    const uint32_t* dh = nullptr;      // [RADIX + 1] digit sub-region starts inside a region (dh[RADIX]: its size)
+    uint32_t cap = 0;                  // output capacity (items)
+    uint32_t* err2 = nullptr;          // a sub-region overflowed
+};
+// words of the XQ workspace for a radix (cursors, bases, done, tickets)
+constexpr uint64_t xq_words(int radix) { return 3ull * kXq * kSegs * radix + kXq * kSegs + kXq * kXqTicketStride; }
+
+template <class Src, int RBITS, int ITEMS, int BLOCK = kSpBlock, bool XQ = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint64_t n, uint32_t shift,
                                                         const uint32_t* __restrict__ lo_base,
                                                         const uint32_t* __restrict__ digit_base,
@@ -923,7 +957,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                                                         uint32_t* __restrict__ err,
                                                         const uint32_t* __restrict__ seg_cnt = nullptr,
                                                         const uint32_t* __restrict__ dense_lo = nullptr,
-                                                        uint32_t stripes = 1) {
+                                                        uint32_t stripes = 1, SegXq xq = SegXq{}) {
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int WTILE = kWave * ITEMS;
@@ -942,9 +976,16 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     __shared__ uint32_t s_tile[2];
     __shared__ uint32_t s_last;
     __shared__ uint32_t s_claim[RADIX];
-    uint32_t* const cur = segw;
-    uint64_t* const sbase = reinterpret_cast<uint64_t*>(segw + (uint64_t)kSegs * RADIX);
-    uint32_t* const done = segw + 3ull * kSegs * RADIX;
+    // XQ: this workgroup's queue (= its XCD) and the queue's own cursors,
+    // bases, claim counts and ticket
+    const uint32_t xqq = XQ ? (blockIdx.x & (kXq - 1)) : 0u;
+    uint32_t* const cur = XQ ? xq.cur + (uint64_t)xqq * kSegs * RADIX : segw;
+    uint64_t* const sbase = XQ ? xq.sbase + (uint64_t)xqq * kSegs * RADIX
+                               : reinterpret_cast<uint64_t*>(segw + (uint64_t)kSegs * RADIX);
+    uint32_t* const done = XQ ? xq.done + xqq * kSegs : segw + 3ull * kSegs * RADIX;
+    if constexpr (XQ) ticket = xq.tickets + xqq * kXqTicketStride;
+    const uint64_t gcap = XQ ? (uint64_t)xq.cap : n;
+    const uint32_t xrs = XQ ? xq.dh[RADIX] : 0u;   // region size
     constexpr uint64_t kReady = 1ull << 32;
 
     const uint32_t wave = wave_id(), lane = lane_id();
@@ -988,8 +1029,13 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t units = s_ubase[nsub];
-    // units of segment l (all its sub-segments)
-    auto units_of = [&](uint32_t l) -> uint32_t { return s_ubase[(l + 1) * stripes] - s_ubase[l * stripes]; };
+    // XQ: units u < U of this queue (u mod 8 = xqq); a ticket t is unit 8 t + xqq
+    auto qcount = [&](uint32_t U) -> uint32_t { return XQ ? (U + (kXq - 1) - xqq) / kXq : U; };
+    auto unit_of = [&](uint32_t t) -> uint32_t { return XQ ? t * kXq + xqq : t; };
+    // units of segment l (all its sub-segments; XQ: of this queue)
+    auto units_of = [&](uint32_t l) -> uint32_t {
+        return qcount(s_ubase[(l + 1) * stripes]) - qcount(s_ubase[l * stripes]);
+    };
     // unit -> (segment, first position, size)
     auto locate = [&](uint32_t u, uint32_t& l, uint64_t& tb, uint32_t& valid) {
         uint32_t a = 0, b = nsub;   // last q with s_ubase[q] <= u (units of empty sub-segments are skipped)
@@ -1015,7 +1061,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             vv[j] = Src::kPk8 ? 0u : src.val(e);
         }
     };
-    uint32_t u = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint32_t u = unit_of((uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]));
     uint32_t l = 0, valid = 0;
     uint64_t tb = 0;
     if (u < units) {
@@ -1074,8 +1120,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         // published (with its ready bit) by segment l - 1's last claimer
         if (dg < (uint32_t)RADIX) {
             uint32_t bh;
-            if (dlo[l] == 0) {
-                bh = digit_base[dg];
+            if (XQ ? qcount(s_ubase[l * stripes]) == 0 : dlo[l] == 0) {
+                // the first segment of the (queue's) items: the digit's start
+                // (XQ: its sub-region in the queue's region)
+                bh = XQ ? xqq * xrs + xq.dh[dg] : digit_base[dg];
             } else {
                 uint64_t w;
                 uint32_t spins = 0;
@@ -1090,6 +1138,10 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
                 bh = (uint32_t)w;
             }
             s_gofs[dg] = bh + s_claim[dg];
+            if constexpr (XQ) {   // the run must end inside the digit's sub-region
+                if (tile_cnt && (uint64_t)bh + s_claim[dg] + tile_cnt > (uint64_t)xqq * xrs + xq.dh[dg + 1])
+                    atomicOr(xq.err2, 1u);
+            }
             s_claim[dg] = bh;
             if constexpr (!Src::kPk8) s_dmin[dg] = bucket_dmin(((dg << kLoBits) | l) + src.bofs, src.cmul, src.bsh);
         }
@@ -1110,7 +1162,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
         }
         // the next unit's loads (see k_split)
         __syncthreads();
-        const uint32_t un = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        const uint32_t un = unit_of((uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]));
         SEG_STAMP(3)
         uint32_t ln = l, validn = valid;
         uint64_t tbn = tb;
@@ -1139,7 +1191,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_seg(Src src, uint
             if (q < valid) {
                 const uint32_t dd = s_dig[q];
                 const uint64_t g = (uint64_t)s_gofs[dd] + (q - s_start[dd]);
-                if (g < n) out_w[g] = s_keys[q];
+                if (g < gcap) out_w[g] = s_keys[q];
             }
         }
         __syncthreads();
@@ -1188,6 +1240,70 @@ __global__ __launch_bounds__(kBlock) void k_bucket_starts(const uint32_t* __rest
         bstart[b] = lo_base[l] == 0 ? digit_base[h] : (uint32_t)sbase[(uint64_t)l * RADIX + h];
         bdmin[b] = bucket_dmin(b + bofs, cmul, bsh);
     }
+}
+
+// XQ digit sub-regions: dh[h] = sum of cap(h') for h' < h, dh[RADIX] = the
+// region size, from the digit totals tot (one workgroup of 1024 threads;
+// RADIX <= 1024).  exact_caps (tests): cap = tot / 8, no slack, so that a
+// queue overflows and the round takes the exact pass.
+__global__ __launch_bounds__(1024) void k_xq_dh(const uint32_t* __restrict__ tot, uint32_t radix, uint32_t exact_caps,
+                                                uint32_t* __restrict__ dh) {
+    __shared__ uint32_t s_tmp[1024 / kWave];
+    const uint32_t t = threadIdx.x;
+    uint32_t cap = 0;
+    if (t < radix) {
+        const uint32_t x = tot[t];
+        cap = exact_caps ? x / kXq : x / kXq + x / 128u + kXqSlack;
+    }
+    const uint32_t inc = wave_inclusive_sum(cap);
+    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+    if (t < radix) dh[t] = off + inc - cap;
+    if (t == radix - 1) dh[radix] = off + inc;
+}
+
+// XQ bucket tables: one workgroup per high digit h, one thread per segment
+// l (bucket b = h << kLoBits | l).  Queue q's count of bucket b is its final
+// cursor cur[q][l][h]; its chunk starts at q rs + dh[h] + the queue's counts
+// of (l' < l, h), and the bucket starts (exact, SA order) at digit_base[h] +
+// the counts of (l' < l, h) of all queues.  pc / pn: [kXq][nb] chunk starts
+// and counts; bstart[nb] = n.
+template <int RADIX>
+__global__ __launch_bounds__(kLoRadix) void k_bucket_starts_xq(const uint32_t* __restrict__ digit_base,
+                                                               const uint32_t* __restrict__ cur,
+                                                               const uint32_t* __restrict__ dh,
+                                                               uint64_t n, uint64_t cmul, uint32_t bsh,
+                                                               uint32_t* __restrict__ bstart,
+                                                               uint32_t* __restrict__ bdmin, uint32_t* __restrict__ pc,
+                                                               uint32_t* __restrict__ pn, uint32_t bofs) {
+    static_assert(kSegs == kLoRadix && kLoRadix % kWave == 0, "one thread per segment");
+    __shared__ uint32_t s_tmp[kLoRadix / kWave];
+    const uint32_t nb = (uint32_t)RADIX << kLoBits;
+    const uint32_t h = blockIdx.x, l = threadIdx.x;
+    const uint32_t b = (h << kLoBits) | l;
+    auto excl = [&](uint32_t x) {   // exclusive scan over the workgroup's segments
+        const uint32_t inc = wave_inclusive_sum(x);
+        __syncthreads();
+        if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+        __syncthreads();
+        uint32_t off = 0;
+        for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+        return off + inc - x;
+    };
+    const uint32_t rs = dh[RADIX];
+    uint32_t tot = 0;
+#pragma unroll 1
+    for (uint32_t q = 0; q < kXq; ++q) {
+        const uint32_t c = cur[((uint64_t)q * kSegs + l) * RADIX + h];
+        tot += c;
+        pn[(uint64_t)q * nb + b] = c;
+        pc[(uint64_t)q * nb + b] = q * rs + dh[h] + excl(c);
+    }
+    bstart[b] = digit_base[h] + excl(tot);
+    bdmin[b] = bucket_dmin(b + bofs, cmul, bsh);
+    if (b == 0) bstart[nb] = (uint32_t)n;
 }
 
 }  // namespace sa

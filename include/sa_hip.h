@@ -81,6 +81,10 @@ enum sa_kernel_kind {
 #define SA_DEBUG_NO_FAST32 0x10u        /* local sort: measured-span kernel, not the fixed-span 32-bit one */
 #define SA_DEBUG_NO_PIVOT 0x20u         /* later rounds: full sorts, never the three-way pivot split */
 #define SA_DEBUG_PERM_ALWAYS 0x40u      /* reference schedule: permutation re-rank at every n */
+#define SA_DEBUG_NO_XQ 0x80u            /* bucketed round 1: second pass into one region (one ticket), not per-XCD
+                                           queues and regions */
+#define SA_DEBUG_XQ_OVERFLOW 0x100u     /* per-XCD second pass with sub-regions of exactly 1/8 of each digit: a queue
+                                           overflows and the round re-runs with the one-region pass */
 
 typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
@@ -122,7 +126,8 @@ typedef struct {
                                             range builds: 3 records by one striped text scan, 4 a record
                                             stripe overflowed and the round ran again with the counting scan */
     int32_t round1_layout;               /* bucketed round 1: bit 0 compact key1 low (BucketSpec.cmp),
-                                            bit 1 packed 8-byte first-pass items (PK8) */
+                                            bit 1 packed 8-byte first-pass items (PK8), bit 2 the second
+                                            pass by per-XCD queues and regions (XQ) */
 } sa_stats;
 
 typedef struct sa_context sa_context;

@@ -690,7 +690,9 @@ def test_round1_layouts(gpu, oracle, golden, layout):
         k = golden["known"]["dna_64MiB"]
         t = oracle.gen_text(k["kind"], k["n"], seed=k["seed"])
         got, st = build_suffix_array(t, return_stats=True)
-        assert st["round1_layout"] == {"compact": True, "pk8": True}, st["round1_layout"]
+        # 2^26 suffixes: 16-bit buckets of ~1024 suffixes, below the fixed-span
+        # local sort's 4 window strides, so the second pass takes one region
+        assert st["round1_layout"] == {"compact": True, "pk8": True, "xq": False}, st["round1_layout"]
         assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
 
 
@@ -709,6 +711,50 @@ def test_compact_layout_text_tails(gpu, oracle, tail):
     smallest_run = tail.endswith(b"AA")   # "A" and "AA" pad alike
     assert st["round1_layout"]["compact"] == (not smallest_run), (tail, st["round1_layout"])
     assert (got == oracle.sa_c(t)).all()
+
+
+def test_round1_xq_second_pass(gpu):
+    """The second bucket pass by per-XCD queues and regions (sa_split.h
+    k_split_seg<.., XQ>, k_bucket_starts_xq; sa_bucket.h load_items_xq,
+    k_window_gather) against the one-region pass (debug no_xq), at 2^28 + 4097
+    suffixes (the smallest size whose buckets take the fixed-span local sort):
+    packed DNA items, a DNA text with "TT" made rare (uneven buckets: windows
+    of several buckets go through k_window_gather) and sub-regions without slack
+    (xq_overflow: a queue overflows, the round runs again with one region);
+    alnum and a widened span take one region at this size.  Same SA in every
+    case, O(n)-checked.  (1 GiB DNA, the bench, and the slow 2^30 - 1 known
+    answer run the XQ pass too.)"""
+    import torch
+    from hpc_suffix_array_amd import DeviceBuilder
+    n = (1 << 28) + 4097
+    b = DeviceBuilder(n)
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    got = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        for kind, alpha in (("dna", b"ACGT"), ("alnum", bytes(range(48, 58)) + bytes(range(65, 91)) + bytes(range(97, 123))),
+                            ("rare_tt", b"ACGT")):
+            b.generate_text(t, n, alpha, seed=7)
+            if kind == "rare_tt":   # "TT" made rare: buckets of TT-prefixes hold ~3 %, windows span several
+                g = torch.Generator(device="cuda").manual_seed(3)
+                tt = (t[1:] == ord("T")) & (t[:-1] == ord("T")) & (torch.rand(n - 1, device="cuda", generator=g) < 0.97)
+                repl = torch.tensor(list(b"ACG"), dtype=torch.uint8, device="cuda")[
+                    torch.randint(0, 3, (n - 1,), device="cuda", generator=g)]
+                t[1:] = torch.where(tt, repl, t[1:])
+                del tt, repl
+            t[-1] = max(alpha)   # no tail run of the smallest symbol (compact layout)
+            st0 = b.build(t, n, want, debug=("no_xq",))
+            assert not st0["round1_layout"]["xq"] and st0["round1"] == "bucketed", (kind, st0["round1_layout"])
+            assert b.check(t, n, want), kind
+            # (alnum at this size: buckets below 4 window strides, one region;
+            # span_extra 6: the span no longer fits the fixed-span words)
+            for dbg, extra, xq in (((), 0, kind != "alnum" or None), ((), 6, None), (("xq_overflow",), 0, False)):
+                st = b.build(t, n, got, debug=dbg, span_extra=extra)
+                print(kind, dbg, extra, st["round1_layout"], flush=True)
+                assert xq is None or st["round1_layout"]["xq"] == xq, (kind, dbg, extra, st["round1_layout"])
+                assert bool((got == want).all().item()), (kind, dbg, extra)
+    finally:
+        b.close()
 
 
 @pytest.mark.parametrize("extra", [0, 6])
