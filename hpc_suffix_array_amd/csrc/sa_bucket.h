@@ -1559,6 +1559,13 @@ __global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restr
             j = list[q];
             b0 = br.wb[j];
             one = fast && br.wb[j + 1] - b0 == 1u;
+            // XQ: a chunk under 64 items could put two boundaries in one row
+            // of 64 slots (k_window_rows): such windows take the wide kernel
+            if (one && hx)
+                for (uint32_t k = 0; k < kXq; ++k) {
+                    const uint32_t c = pn[(uint64_t)k * nb + b0];
+                    if (c && c < kWave) one = false;
+                }
         }
         const uint64_t m1 = __ballot(ok && one), m2 = __ballot(ok && !one);
         uint32_t base1 = 0, base2 = 0;
@@ -1677,19 +1684,24 @@ __device__ __forceinline__ void load_items(const uint64_t* __restrict__ w_in, ui
 // output.  Its header hx (16 words, k_window_split) holds, for chunk k,
 // d[k] = (chunk start) - P_k and P_1..P_7 (P_k: the window slots before
 // chunk k), so slot le reads w_in[d[k] + le] for the last k with P_k <= le.
-// Its row table (k_window_rows) holds one word per row r of 64 slots (wave
-// r / ITEMS, item r % ITEMS): d[k] of the row's chunk, or kXqCross when the
-// row crosses a chunk boundary (at most 7 of a window's rows; those lanes
-// search hx).  The local sort copies the next window's row table and header
-// into LDS while it sorts the current one, so the next window's loads (the
-// prefetch) cost an LDS read and an add per item, as contiguous items do.
-// (Reading the table from memory at the prefetch point put a round trip in
-// front of every load: local sort 3.5 -> 6.1 ms.)
+// Its row table (k_window_rows) holds three words per row r of 64 slots
+// (wave r / ITEMS, item r % ITEMS): d_a, d_b and split -- lanes below split
+// read at d_a + le, the others at d_b + le (split 64: the row lies in one
+// chunk; a window with a chunk under 64 items, whose rows could cross two
+// boundaries, is not a fast window: k_window_split lists it for
+// k_bucket_sort_wide).  Each wave loads its 18 rows' words into three VGPRs
+// (lane i: row i) when it takes the next window's ticket and reads them by
+// readlane at the prefetch point: a compare and a select per item on top of
+// the contiguous load.  Measured alternatives (1 GiB DNA local sort, 3.5 ms
+// over contiguous items): the table read at the prefetch point from memory
+// 6.1 ms (a round trip before every load), staged through LDS 3.9 ms (the
+// LDS store waited for the wave's previous stores), 18 scalar loads 4.2 ms
+// (SGPR spills), a per-lane search of the header in a call for rows that
+// cross a boundary 4.0 ms (the call waits for the loads in flight).
 struct XqWin {
     const uint32_t* __restrict__ hx = nullptr;     // [hdr index][16]
-    const uint32_t* __restrict__ rows = nullptr;   // [hdr index][rows per window]
+    const uint32_t* __restrict__ rows = nullptr;   // [hdr index][3][rows per window]
 };
-constexpr uint32_t kXqCross = 0xFFFFFFFFu;   // (an offset is C_k - P_k with C_k >= P_k, never ~0)
 
 // window slot le of chunk k: the last k with P_k <= le (P_0 = 0)
 __device__ __forceinline__ uint32_t xq_offset(const uint32_t* __restrict__ hx, uint32_t le) {
@@ -1699,35 +1711,38 @@ __device__ __forceinline__ uint32_t xq_offset(const uint32_t* __restrict__ hx, u
     return off;
 }
 
-// a row that crosses a chunk boundary (rare: at most 7 of a window's 144
-// rows), out of line so that its header reads do not stay live across the
-// inlined loads of the other rows
-__device__ __noinline__ uint64_t xq_cross_load(const uint64_t* __restrict__ w_in, const uint32_t* s_h, uint32_t lc) {
-    return w_in[(uint32_t)(xq_offset(s_h, lc) + lc)];
+// this wave's row words of a window: lane i < ITEMS holds word i of row
+// (wave ITEMS + i) of table t (0: d_a, 1: d_b, 2: split)
+template <int ITEMS, int ROWS>
+__device__ __forceinline__ void load_rows_xq(const uint32_t* __restrict__ rows, uint32_t (&rv)[3]) {
+    const uint32_t lane = lane_id();
+    const uint32_t w = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x / kWave));
+    const uint32_t r = w * ITEMS + (lane < (uint32_t)ITEMS ? lane : 0u);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) rv[t] = rows[t * ROWS + r];
 }
 
-// s_rw: this wave's ITEMS row words, s_h: the window's header (both LDS)
 template <int ITEMS>
-__device__ __forceinline__ void load_items_xq(const uint64_t* __restrict__ w_in, const uint32_t* s_rw,
-                                              const uint32_t* s_h, uint32_t m, uint64_t (&x)[ITEMS]) {
+__device__ __forceinline__ void load_items_xq(const uint64_t* __restrict__ w_in, const uint32_t (&rv)[3], uint32_t m,
+                                              uint64_t (&x)[ITEMS]) {
     const uint32_t l0 = slot0<ITEMS>();
+    const uint32_t lane = lane_id();
     const uint32_t last = m - 1;
 #pragma unroll
     for (int i = 0; i < ITEMS; ++i) {
         const uint32_t le = l0 + i * kWave;
         const uint32_t lc = le < m ? le : last;
-        // the row's offset is uniform: a scalar base and the lane's slot
-        const uint32_t off = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_rw[i]);
-        if (off == kXqCross)   // uniform: the row crosses a chunk boundary
-            x[i] = xq_cross_load(w_in, s_h, lc);
-        else
-            x[i] = (w_in + off)[lc];
+        const uint32_t da = (uint32_t)__builtin_amdgcn_readlane((int)rv[0], i);
+        const uint32_t db = (uint32_t)__builtin_amdgcn_readlane((int)rv[1], i);
+        const uint32_t sp = (uint32_t)__builtin_amdgcn_readlane((int)rv[2], i);
+        x[i] = w_in[(uint32_t)((lane < sp ? da : db) + lc)];
     }
 }
 
 // The row tables of the XQ one-bucket windows (k_window_split's headers
 // words[kHdrWord], hx), one wave per window: row r covers slots [64 r,
-// min(64 r + 63, m - 1)] (slots past m re-read item m - 1).
+// min(64 r + 63, m - 1)] (slots past m re-read item m - 1); at most one
+// chunk boundary lies inside a row (k_window_split).
 __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restrict__ words, const uint4* __restrict__ hdr,
                                                         const uint32_t* __restrict__ hx, uint32_t nrows,
                                                         uint32_t* __restrict__ rows) {
@@ -1735,19 +1750,21 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
     const uint32_t lane = lane_id();
     for (uint64_t q = (uint64_t)blockIdx.x * kWaves + wave_id(); q < nh; q += (uint64_t)gridDim.x * kWaves) {
         const uint32_t m = hdr[q].z;
-        const uint32_t* const h = hx + q * 16;
         uint32_t hv[16];
 #pragma unroll
-        for (int k = 0; k < 16; ++k) hv[k] = h[k];
+        for (int k = 0; k < 16; ++k) hv[k] = hx[q * 16 + k];
         for (uint32_t r = lane; r < nrows; r += kWave) {
             const uint32_t lo = std::min(r * kWave, m - 1), hi = std::min(r * kWave + (kWave - 1), m - 1);
-            uint32_t klo = 0, khi = 0;
+            uint32_t split = kWave;   // the first boundary inside (lo, hi]
 #pragma unroll
-            for (int k = 1; k < (int)kXq; ++k) {
-                klo += hv[kXq - 1 + k] <= lo ? 1u : 0u;
-                khi += hv[kXq - 1 + k] <= hi ? 1u : 0u;
+            for (int k = kXq - 1; k >= 1; --k) {
+                const uint32_t pk = hv[kXq - 1 + k];
+                if (pk > lo && pk <= hi) split = pk - r * kWave;
             }
-            rows[q * nrows + r] = klo == khi ? xq_offset(hv, lo) : kXqCross;
+            uint32_t* const e = rows + q * 3 * nrows + r;
+            e[0] = xq_offset(hv, lo);
+            e[nrows] = xq_offset(hv, hi);
+            e[2 * nrows] = split;
         }
     }
 }
@@ -1777,11 +1794,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     __shared__ unsigned long long s_tot[3];   // heads, U, U groups of the workgroup's windows (thread 0)
     constexpr int WPT = kSubBuckets / 2 / BLOCK;   // counter words per thread
     static_assert(WPT * 2 == 4 && WPT * 2 * BLOCK == kSubBuckets, "four sub-buckets per thread");
-    // XQ: row tables + headers of the current and the next window (load_items_xq)
-    constexpr int ROWS = WAVES * ITEMS;
-    constexpr int XRW = ROWS + 16;
-    static_assert(!XQ || XRW <= BLOCK, "one thread per row word");
-    __shared__ uint32_t s_xr[XQ ? 2 * XRW : 1];
+    constexpr int ROWS = WAVES * ITEMS;   // XQ: row words per window (load_items_xq)
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
@@ -1803,10 +1816,9 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     uint4 h = hdr[q];
     uint64_t w[ITEMS];
     if constexpr (XQ) {
-        if (dg < (uint32_t)XRW)
-            s_xr[dg] = dg < (uint32_t)ROWS ? xw.rows[(uint64_t)q * ROWS + dg] : xw.hx[(uint64_t)q * 16 + dg - ROWS];
-        __syncthreads();
-        load_items_xq<ITEMS>(keys_in, s_xr + wave * ITEMS, s_xr + ROWS, h.z, w);
+        uint32_t rv[3];
+        load_rows_xq<ITEMS, ROWS>(xw.rows + (uint64_t)q * 3 * ROWS, rv);
+        load_items_xq<ITEMS>(keys_in, rv, h.z, w);
     } else {
         load_items<ITEMS>(keys_in, h.y, h.z, w);
     }
@@ -1827,16 +1839,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         // the scatter (a conditional one kept them live through the sort)
         uint4 hn = make_uint4(0u, 0u, 1u, 0u);
         if (more) hn = hdr[qn];
-        // XQ: the next window's row table and header word of this thread
-        // (past the last window: the current one's), into LDS after the
-        // histogram, read at the prefetch point
-        uint32_t xr_next = 0;
-        if constexpr (XQ) {
-            const uint64_t qx = more ? qn : q;
-            if (dg < (uint32_t)XRW)
-                xr_next = dg < (uint32_t)ROWS ? xw.rows[qx * ROWS + dg] : xw.hx[qx * 16 + dg - ROWS];
-        }
-        const uint32_t* const s_xn = s_xr + (par ^ 1u) * XRW;
+        // XQ: the next window's row words of this wave (past the last
+        // window: the current one's), for the prefetch
+        uint32_t rwn[3] = {0u, 0u, 0u};
+        if constexpr (XQ) load_rows_xq<ITEMS, ROWS>(xw.rows + (uint64_t)(more ? qn : q) * 3 * ROWS, rwn);
         probe.mark(0);
         const uint32_t l0 = slot0<ITEMS>();
         // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
@@ -1855,9 +1861,6 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                     atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
                 }
             }
-        }
-        if constexpr (XQ) {
-            if (dg < (uint32_t)XRW) s_xr[(par ^ 1u) * XRW + dg] = xr_next;
         }
         __syncthreads();
         probe.mark(1);
@@ -1906,7 +1909,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // positions for it; storing the items here made this kernel spill)
             if (threadIdx.x == 0) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, s_xn + wave * ITEMS, s_xn + ROWS, hn.z, w);
+            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
             else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
         } else {
@@ -1932,7 +1935,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // scheduling barrier: hoisted above the scatter, they would hold
             // a second window of registers)
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, s_xn + wave * ITEMS, s_xn + ROWS, hn.z, w);
+            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
             else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
             probe.mark(3);
