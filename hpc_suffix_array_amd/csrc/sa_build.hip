@@ -130,6 +130,7 @@ struct sa_context {
     uint64_t segx_words = 0;
     uint32_t* os = nullptr;                     // onesweep ghist / digit bases / tickets
     uint32_t* lsd = nullptr;                    // k_lsd ghist [8][1024] | bases [8][1024] | tickets [8]
+    uint32_t* lsdx = nullptr;                   // XQ k_lsd: per-queue counts [passes][8][1024] | bases [8][1024] | tickets
     uint32_t* segw = nullptr;                   // second bucket pass: per-segment cursors / bases / flags
     uint64_t* states = nullptr;                 // onesweep tile states [tiles][256]
     uint32_t epoch = 0;                         // onesweep state tag of the last pass
@@ -590,30 +591,33 @@ static int blocks_per_cu(K kernel, int block) {
     return nb;
 }
 
-template <class Src, bool PACKED>
+// XQ (sa_lsd.h): per-XCD queues of tiles; base = qbase[8][1024], ticket =
+// the pass's 8 queue tickets, next_hist = the next pass's per-queue counts;
+// the grid is whole XCDs (every queue served)
+template <class Src, bool PACKED, bool XQ = false>
 static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits, const uint32_t* base,
                      uint32_t* ticket, uint64_t* ok, uint32_t* ov, hipStream_t s, uint32_t nshift, uint32_t nnbits,
-                     uint32_t* next_hist) {
+                     uint32_t* next_hist, QDiv qd = QDiv{}, uint32_t tpq = 0) {
     const uint32_t epoch = next_epoch(c, s);
     uint64_t tiles = 0;
     unsigned long long* prof = reinterpret_cast<unsigned long long*>(lsd_tickets(c) + kMaxPasses);
     if (SA_LSD_PROF) hipMemsetAsync(prof, 0, 5 * 8, s);
 #define SA_LSD_LAUNCH(RB)                                                                                   \
     do {                                                                                                    \
-        auto kern = k_lsd<Src, RB, PACKED>;                                                                 \
-        constexpr int B = lsd_block<PACKED, RB>();                                                          \
-        constexpr uint64_t T = (uint64_t)B * lsd_items<PACKED, RB>();                                       \
+        auto kern = k_lsd<Src, RB, PACKED, XQ>;                                                             \
+        constexpr int B = lsd_block<PACKED, RB, XQ>();                                                      \
+        constexpr uint64_t T = (uint64_t)B * lsd_items<PACKED, RB, XQ>();                                   \
         tiles = (n + T - 1) / T;                                                                            \
         static std::atomic<int> per_cu{0};                                                                  \
         if (!per_cu.load(std::memory_order_relaxed)) per_cu.store(blocks_per_cu(kern, B));                  \
         const uint64_t grid = (uint64_t)c->cus * (uint64_t)per_cu.load(std::memory_order_relaxed);          \
-        hipLaunchKernelGGL(kern, dim3((uint32_t)std::min<uint64_t>(tiles, grid)), dim3(B), 0, s,             \
+        hipLaunchKernelGGL(kern, dim3((uint32_t)(XQ ? grid : std::min<uint64_t>(tiles, grid))), dim3(B), 0, s, \
                            src, n, shift, nbits, base, c->states, ticket, epoch, ok, ov, c->words + 4, prof,   \
-                           nshift, nnbits, next_hist);                                                     \
+                           nshift, nnbits, next_hist, qd, tpq);                                            \
     } while (0)
     if (nbits <= 8) SA_LSD_LAUNCH(8);
     else if (nbits == 9) SA_LSD_LAUNCH(9);
-    else SA_LSD_LAUNCH(10);
+    else if constexpr (PACKED || !XQ) SA_LSD_LAUNCH(10);   // (unpacked XQ passes: <= 9 bits, lsd_sort)
 #undef SA_LSD_LAUNCH
     if (SA_LSD_PROF) {
         unsigned long long h[5];
@@ -642,6 +646,60 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
     // the first digit's totals here; every pass counts the next one's
     LsdPlan first_only = pl;
     first_only.P = 1;
+    // per-XCD queues of tiles (sa_lsd.h XQ): 8192-pair tiles, the queue span
+    // tpq tiles
+    const uint64_t xtiles = (n + kLsdXqTile - 1) / kLsdXqTile;
+    // (unpacked passes of 10 bits do not fit their LDS with the per-queue counters)
+    bool xq = SA_LSD_XQ && c->cus % 8 == 0 && xtiles >= 64 && !(c->dbg & SA_DEBUG_NO_XQ);
+    if (!PACKED)
+        for (uint32_t p = 0; p < pl.P; ++p) xq = xq && pl.bits[p] <= 9;
+    if (xq) {
+        const uint32_t tpq = (uint32_t)((xtiles + 7) / 8);
+        const uint64_t qspan = (uint64_t)tpq * kLsdXqTile;
+        QDiv qd;
+        qd.magic = (uint64_t)((((unsigned __int128)1 << 64) + qspan - 1) / qspan);
+        uint32_t* const qh = c->lsdx;                                    // [pass][8][1024]
+        uint32_t* const qb = qh + kMaxPasses * 8 * kLsdMaxRadix;         // [8][1024]
+        uint32_t* const qt = qb + 8 * kLsdMaxRadix;                      // [pass][8 x 32]
+        SA_HIP(hipMemsetAsync(c->lsdx, 0, kLsdXqWords * 4, s));
+        tm.begin(SA_K_HIST_FIRST);
+        hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + 8 * kBlock - 1) / (8 * kBlock),
+                                                                               (uint64_t)c->cus * 4)),
+                           dim3(kBlock), 0, s, first, n, first_only, qh, qd);
+        tm.end();
+        add_bytes(st, SA_K_HIST_FIRST, 8 * n);
+        const uint64_t pair = PACKED ? 8 : 12;
+        for (uint32_t p = 0; p < pl.P; ++p) {
+            tm.begin(SA_K_SCAN);
+            hipLaunchKernelGGL(k_lsd_qbase, dim3(1), dim3(1024), 0, s, (const uint32_t*)qh + p * 8 * kLsdMaxRadix,
+                               1u << pl.bits[p], qb);
+            tm.end();
+            const bool more = p + 1 < pl.P;
+            const uint32_t nsh = more ? pl.shift[p + 1] : 0u, nnb = more ? pl.bits[p + 1] : 1u;
+            uint32_t* nh = more ? qh + (p + 1) * 8 * kLsdMaxRadix : nullptr;
+            uint32_t* tk = qt + p * 8 * 32;
+            if (p == 0) {
+                tm.begin(SA_K_SCATTER_FIRST);
+                lsd_pass<Src0, PACKED, true>(c, first, n, pl.shift[0], pl.bits[0], qb, tk, kb[0], vb[0], s, nsh, nnb,
+                                             nh, qd, tpq);
+                tm.end();
+                add_bytes(st, SA_K_SCATTER_FIRST, (8 + pair) * n);
+            } else {
+                tm.begin(SA_K_SCATTER_KEYS);
+                if constexpr (PACKED)
+                    lsd_pass<SrcItems, true, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], qb, tk,
+                                                   kb[p & 1], nullptr, s, nsh, nnb, nh, qd, tpq);
+                else
+                    lsd_pass<SrcKeys, false, true>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p],
+                                                   pl.bits[p], qb, tk, kb[p & 1], vb[p & 1], s, nsh, nnb, nh, qd, tpq);
+                tm.end();
+                add_bytes(st, SA_K_SCATTER_KEYS, 2 * pair * n);
+            }
+        }
+        SA_HIP(hipGetLastError());
+        *sorted = kb[(pl.P - 1) & 1];
+        return SA_OK;
+    }
     tm.begin(SA_K_HIST_FIRST);
     hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + 8 * kBlock - 1) / (8 * kBlock),
                                                                            (uint64_t)c->cus * 4)),
@@ -1553,6 +1611,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         hipMalloc(&c->code, 256 * 2) != hipSuccess ||
         hipMalloc(&c->os, (2 * kMaxPasses * kRadix + kMaxPasses) * 4) != hipSuccess ||
         hipMalloc(&c->lsd, (2 * kMaxPasses * kLsdMaxRadix + kMaxPasses) * 4 + 64) != hipSuccess ||
+        hipMalloc(&c->lsdx, kLsdXqWords * 4) != hipSuccess ||
         hipMalloc(&c->segw, (kBstartOff + 2 * kBstartWords) * 4) != hipSuccess ||
         hipHostMalloc(&c->host_words, 16384, hipHostMallocDefault) != hipSuccess) {
         (void)hipGetLastError();
@@ -1587,6 +1646,7 @@ void sa_context_destroy(sa_context* c) {
     hipFree(c->code);
     hipFree(c->os);
     hipFree(c->lsd);
+    hipFree(c->lsdx);
     hipFree(c->segw);
     hipFree(c->segx);
     hipFree(c->hist);

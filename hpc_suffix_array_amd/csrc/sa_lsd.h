@@ -48,11 +48,38 @@ namespace sa {
 #ifndef SA_LSD_UP_ITEMS
 #define SA_LSD_UP_ITEMS 8
 #endif
-template <bool PACKED, int RBITS>
-constexpr int lsd_block() { return RBITS > 9 ? 1024 : PACKED ? SA_LSD_PK_BLOCK : SA_LSD_UP_BLOCK; }
-template <bool PACKED, int RBITS>
-constexpr int lsd_items() { return RBITS > 9 ? 8 : PACKED ? SA_LSD_PK_ITEMS : SA_LSD_UP_ITEMS; }
+// XQ passes (below): 1024 x 8 for every digit width (their per-queue
+// next-pass counters take 32 KiB of LDS)
+template <bool PACKED, int RBITS, bool XQ = false>
+constexpr int lsd_block() { return XQ || RBITS > 9 ? 1024 : PACKED ? SA_LSD_PK_BLOCK : SA_LSD_UP_BLOCK; }
+template <bool PACKED, int RBITS, bool XQ = false>
+constexpr int lsd_items() { return XQ || RBITS > 9 ? 8 : PACKED ? SA_LSD_PK_ITEMS : SA_LSD_UP_ITEMS; }
 constexpr int kLsdMaxRadix = 1024;
+constexpr int kLsdXqTile = 1024 * 8;
+// per-queue counts of every pass, the bases of one, the tickets of every pass
+constexpr int kLsdXqWords = kMaxPasses * 8 * kLsdMaxRadix + 8 * kLsdMaxRadix + kMaxPasses * 8 * 32;
+#ifndef SA_LSD_XQ
+#define SA_LSD_XQ 1
+#endif
+
+// ---------------------------------------------------------------------------
+// XQ passes (round 5; the second bucket pass's per-XCD queues, sa_split.h
+// SegXq, made stable): queue q = workgroup mod 8 (= its XCD) takes the tiles
+// of the q-th eighth of the input, [q tpq, (q + 1) tpq), from its own ticket,
+// and its items of digit d go to [base(d) + sum_{q' < q} count(q', d), ...):
+// the output stays in (digit, tile) order -- stable, as the LSD sort needs --
+// while each (queue, digit) run is written by one XCD, whose L2 merges the
+// partial lines at the run ends.  The decoupled look-back runs over the
+// queue's own tiles.  count(q, d) of a pass is counted by the pass before it
+// (the item's queue in the next pass is its output position over the queue
+// span) or, for the first pass of a round, by k_lsd_hist.
+// ---------------------------------------------------------------------------
+// floor(g / qspan) as the high half of g * ceil(2^64 / qspan): exact for g <
+// 2^33 and qspan < 2^31 (the error g / 2^64 stays below 1 / qspan)
+struct QDiv {
+    uint64_t magic = 0;   // 0: one queue
+    __device__ __forceinline__ uint32_t q(uint64_t g) const { return magic ? (uint32_t)__umul64hi(g, magic) : 0u; }
+};
 
 // the passes of one sort: digit p is bits [shift[p], shift[p] + bits[p])
 struct LsdPlan {
@@ -102,11 +129,15 @@ struct SrcItems {
 // (the multiset of keys is the same in every pass); one atomic per run of
 // equal digits across neighbouring lanes (hist_add_runs: a degenerate
 // text's equal keys would otherwise put 64 lanes on one bin).
+// qd.magic != 0 (XQ, plan.P = 1): the first digit counted per queue of the
+// input position, ghist[q][d].
 template <class Src>
 __global__ __launch_bounds__(kBlock) void k_lsd_hist(Src src, uint64_t n, LsdPlan plan,
-                                                     uint32_t* __restrict__ ghist) {
+                                                     uint32_t* __restrict__ ghist, QDiv qd = QDiv{}) {
+    static_assert(kMaxPasses >= 8, "the per-queue counts use the per-pass rows");
     __shared__ uint32_t s_h[kMaxPasses * kLsdMaxRadix];
-    for (uint32_t i = threadIdx.x; i < plan.P * kLsdMaxRadix; i += kBlock) s_h[i] = 0;
+    const uint32_t rows = qd.magic ? 8u : plan.P;
+    for (uint32_t i = threadIdx.x; i < rows * kLsdMaxRadix; i += kBlock) s_h[i] = 0;
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
@@ -125,19 +156,48 @@ __global__ __launch_bounds__(kBlock) void k_lsd_hist(Src src, uint64_t n, LsdPla
             const uint64_t e = b + (uint64_t)j * kBlock + threadIdx.x;
             if (e >= n) break;   // the active lanes stay a prefix of the wave
             const uint32_t nact = (uint32_t)__popcll(__ballot(1));
+            const uint32_t qrow = qd.q(e);   // XQ: the input position's queue
             for (uint32_t p = 0; p < plan.P; ++p) {
                 const uint32_t d = (uint32_t)(k[j] >> plan.shift[p]) & ((1u << plan.bits[p]) - 1u);
-                const uint32_t dl = __shfl_up(d, 1, 64);
-                const bool head = lane == 0 || dl != d;
+                const uint32_t slot = (qd.magic ? qrow : p) * kLsdMaxRadix + d;
+                const uint32_t dl = __shfl_up(slot, 1, 64);
+                const bool head = lane == 0 || dl != slot;
                 const uint64_t hm = __ballot(head) & above;
                 const uint32_t next = hm ? (uint32_t)__ffsll((long long)hm) - 1u : nact;
-                if (head) atomicAdd(&s_h[p * kLsdMaxRadix + d], next - lane);
+                if (head) atomicAdd(&s_h[slot], next - lane);
             }
         }
     }
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < plan.P * kLsdMaxRadix; i += kBlock)
+    for (uint32_t i = threadIdx.x; i < rows * kLsdMaxRadix; i += kBlock)
         if (s_h[i]) atomicAdd(&ghist[i], s_h[i]);
+}
+
+// XQ bases of one pass from its per-queue counts qh[q][d] (one 1024-thread
+// workgroup): qbase[q][d] = (digits below d, all queues) + (digit d in queues
+// below q)
+__global__ __launch_bounds__(1024) void k_lsd_qbase(const uint32_t* __restrict__ qh, uint32_t bins,
+                                                    uint32_t* __restrict__ qbase) {
+    __shared__ uint32_t s_tmp[16];
+    const uint32_t i = threadIdx.x;
+    uint32_t c[8], tot = 0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+        c[q] = i < bins ? qh[q * kLsdMaxRadix + i] : 0u;
+        tot += c[q];
+    }
+    const uint32_t inc = wave_inclusive_sum(tot);
+    if (lane_id() == kWave - 1) s_tmp[wave_id()] = inc;
+    __syncthreads();
+    uint32_t off = 0;
+    for (uint32_t w = 0; w < wave_id(); ++w) off += s_tmp[w];
+    uint32_t b = off + inc - tot;
+    if (i < bins)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            qbase[q * kLsdMaxRadix + i] = b;
+            b += c[q];
+        }
 }
 
 // base[p][d] = exclusive scan of ghist[p][..] (one 1024-thread workgroup per pass)
@@ -156,16 +216,20 @@ __global__ __launch_bounds__(1024) void k_lsd_base(const uint32_t* __restrict__ 
 }
 
 // One stable pass over digit (key >> shift) & (2^nbits - 1), nbits <= RBITS.
-template <class Src, int RBITS, bool PACKED>
-__global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
+// XQ: digit_base is qbase[8][kLsdMaxRadix], ticket the 8 queue tickets (at
+// a stride of 32 words), next_hist the next pass's [8][kLsdMaxRadix] counts;
+// qd divides an output position by the queue span (tpq tiles).
+template <class Src, int RBITS, bool PACKED, bool XQ = false>
+__global__ __launch_bounds__((lsd_block<PACKED, RBITS, XQ>()), 4) void k_lsd(Src src, uint64_t n, uint32_t shift, uint32_t nbits,
                                                    const uint32_t* __restrict__ digit_base,
                                                    uint64_t* __restrict__ states, uint32_t* __restrict__ ticket,
                                                    uint32_t epoch, uint64_t* __restrict__ out_keys,
                                                    uint32_t* __restrict__ out_vals, uint32_t* __restrict__ err,
                                                    unsigned long long* __restrict__ prof, uint32_t nshift,
-                                                   uint32_t nnbits, uint32_t* __restrict__ next_hist) {
-    constexpr int BLOCK = lsd_block<PACKED, RBITS>();
-    constexpr int ITEMS = lsd_items<PACKED, RBITS>();
+                                                   uint32_t nnbits, uint32_t* __restrict__ next_hist,
+                                                   QDiv qd = QDiv{}, uint32_t tpq = 0) {
+    constexpr int BLOCK = lsd_block<PACKED, RBITS, XQ>();
+    constexpr int ITEMS = lsd_items<PACKED, RBITS, XQ>();
     constexpr int WAVES = BLOCK / kWave;
     constexpr int RADIX = 1 << RBITS;
     constexpr int RWAVES = RADIX / kWave;
@@ -180,20 +244,30 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
     __shared__ uint32_t s_gofs[RADIX];
     __shared__ uint32_t s_tmp[RWAVES];
     __shared__ uint32_t s_tile[2];
-    __shared__ uint32_t s_nh[kLsdMaxRadix];     // the next pass's digit totals of this workgroup's tiles
+    // the next pass's digit totals of this workgroup's tiles (XQ: per queue)
+    constexpr int NH = XQ ? 8 * kLsdMaxRadix : kLsdMaxRadix;
+    __shared__ uint32_t s_nh[NH];
 
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint32_t dg = threadIdx.x;
     const uint32_t mask = (1u << nbits) - 1u;
     const uint32_t nmask = (1u << nnbits) - 1u;
-    for (int i = dg; i < kLsdMaxRadix; i += BLOCK) s_nh[i] = 0;
-    const uint64_t tiles = (n + TILE - 1) / TILE;
+    for (int i = dg; i < NH; i += BLOCK) s_nh[i] = 0;
+    const uint64_t tiles_all = (n + TILE - 1) / TILE;
+    // XQ: this workgroup's queue and its tiles [t0, t1) (tile ids are global)
+    const uint32_t xq = XQ ? (blockIdx.x & 7u) : 0u;
+    const uint64_t t0 = XQ ? std::min<uint64_t>((uint64_t)xq * tpq, tiles_all) : 0ull;
+    const uint64_t tiles = XQ ? std::min<uint64_t>(t0 + tpq, tiles_all) : tiles_all;   // the end of the tiles taken
+    if constexpr (XQ) {
+        ticket += xq * 32;
+        digit_base += xq * kLsdMaxRadix;
+    }
     const uint64_t tag = (uint64_t)(epoch & kEpochMask) << 48;
     uint32_t* const wc32 = reinterpret_cast<uint32_t*>(&s_wcnt[0][0]);
     if (dg == 0) s_tile[0] = atomicAdd(ticket, 1u);
     for (int i = dg; i < WAVES * RADIX / 2; i += BLOCK) wc32[i] = 0;
     __syncthreads();
-    uint64_t t = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
+    uint64_t t = t0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[0]);
     uint64_t k[ITEMS];
     uint32_t v[ITEMS];
     // clamped loads (pairs past the end are never ranked)
@@ -241,7 +315,7 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t le = wave * WTILE + j * kWave + lane;
             const bool ok = le < valid;
-            if (next_hist && ok) atomicAdd(&s_nh[(uint32_t)(k[j] >> nshift) & nmask], 1u);
+            if (!XQ && next_hist && ok) atomicAdd(&s_nh[(uint32_t)(k[j] >> nshift) & nmask], 1u);
             const uint32_t d = ok ? (uint32_t)(k[j] >> shift) & mask : (uint32_t)RADIX;
             uint64_t peers = __ballot(ok);
             for (uint32_t b = 0; b < nbits; ++b) {
@@ -264,7 +338,7 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
                 s_wcnt[w][dg] = (uint16_t)tile_cnt;
                 tile_cnt += x;
             }
-            st_store(&states[t * RADIX + dg], (t == 0 ? kStPrefix : kStAgg) | tag | tile_cnt);
+            st_store(&states[t * RADIX + dg], (t == t0 ? kStPrefix : kStAgg) | tag | tile_cnt);
         }
         {
             const uint32_t x = (dg < (uint32_t)RADIX) ? tile_cnt : 0u;
@@ -278,7 +352,9 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
         }
         stamp(1);
         if (dg < (uint32_t)RADIX) {
-            const uint64_t excl = tile_lookback<RADIX, false, SA_LSD_LOOK>(states, t, dg, tile_cnt, tag, err);
+            // (XQ: over the queue's own tiles, t0 first)
+            const uint64_t excl =
+                tile_lookback<RADIX, false, SA_LSD_LOOK>(states + t0 * RADIX, t - t0, dg, tile_cnt, tag, err);
             s_gofs[dg] = digit_base[dg] + (uint32_t)excl;
         }
         // the next tile's ticket only now (see k_split), its loads in flight
@@ -286,7 +362,7 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
         if (dg == 0) s_tile[par ^ 1u] = atomicAdd(ticket, 1u);
         __syncthreads();
         stamp(2);
-        const uint64_t tn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
+        const uint64_t tn = t0 + (uint32_t)__builtin_amdgcn_readfirstlane((int)s_tile[par ^ 1u]);
         uint64_t kn[ITEMS];
         uint32_t vn[ITEMS];
         load(tn < tiles ? tn : tiles - 1, kn, vn);
@@ -312,6 +388,8 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
                 if (g < n) {
                     out_keys[g] = key;
                     if constexpr (!PACKED) out_vals[g] = s_vals[q];
+                    // XQ: the next pass's digit in the queue of this output position
+                    if (XQ && next_hist) atomicAdd(&s_nh[qd.q(g) * kLsdMaxRadix + ((uint32_t)(key >> nshift) & nmask)], 1u);
                 }
             }
         }
@@ -330,8 +408,13 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS>()), 4) void k_lsd(Src src
             for (int q = 0; q < 5; ++q) atomicAdd(prof + q, (unsigned long long)tacc[q]);
     if (next_hist) {
         __syncthreads();
-        for (uint32_t i = dg; i <= nmask; i += BLOCK)
-            if (s_nh[i]) atomicAdd(&next_hist[i], s_nh[i]);
+        if constexpr (XQ) {
+            for (uint32_t i = dg; i < (uint32_t)NH; i += BLOCK)
+                if ((i & (kLsdMaxRadix - 1)) <= nmask && s_nh[i]) atomicAdd(&next_hist[i], s_nh[i]);
+        } else {
+            for (uint32_t i = dg; i <= nmask; i += BLOCK)
+                if (s_nh[i]) atomicAdd(&next_hist[i], s_nh[i]);
+        }
     }
 }
 

@@ -379,12 +379,12 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // m >> bb undercounted them by G, and ranges took k_bucket_sort_wide)
     const bool fast32 = bits1 > (uint32_t)kSubBits && bits1 - kSubBits <= kLowMax &&
                         m / (uint64_t)(bhi - blo) >= 4ull * kWinStride && !(c->dbg & SA_DEBUG_NO_FAST32);
-    // the second pass by per-XCD queues and regions (sa_split.h SegXq): one
-    // GPU's padded round (n >= 2^26: the regions' slack is in keys_u), the
+    // the second pass by per-XCD queues and regions (sa_split.h SegXq): the
     // fixed-span local sort (which loads a one-bucket window's 8 chunks), a
-    // grid of whole XCDs
-    const bool xq = SA_SEG_XQ && allow_xq && padded && fast32 && c->cus % (int)kXq == 0 &&
-                    !(c->dbg & SA_DEBUG_NO_XQ) && c->kucap >= n + n / 16 + 8ull * 1024 * kXqSlack;
+    // grid of whole XCDs, the regions' slack in keys_u (ensure_u_capacity:
+    // 2^26 entries and up; one GPU or a rank's range)
+    const bool xq = SA_SEG_XQ && allow_xq && fast32 && c->cus % (int)kXq == 0 && !(c->dbg & SA_DEBUG_NO_XQ) &&
+                    c->kucap >= m + m / 16 + 8ull * 1024 * kXqSlack;
     if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0);
     // XQ workspace: queue cursors / bases / claim counts / tickets, the digit
     // sub-region starts, the per-region chunk starts and counts per bucket

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 30)
     ap.add_argument("--kind", default="dna")
     ap.add_argument("--reps", type=int, default=6)
+    ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("variants", nargs="+")
     a = ap.parse_args()
     import torch
@@ -32,12 +33,12 @@ def main():
     sa = torch.empty(a.n, dtype=torch.int32, device="cuda")
     res = {v: [] for v in a.variants}
     for v in a.variants:   # warm-up
-        b.build(t, a.n, sa, profile=True, debug=() if v == "default" else tuple(v.split("+")))
+        b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=() if v == "default" else tuple(v.split("+")))
     for _ in range(a.reps):
         for v in a.variants:
             dbg = () if v == "default" else tuple(v.split("+"))
             torch.cuda.synchronize()
-            st = b.build(t, a.n, sa, profile=True, debug=dbg)
+            st = b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=dbg)
             torch.cuda.synchronize()
             res[v].append(st)
     ok = {v: b.check(t, a.n, sa) for v in a.variants[-1:]}
@@ -45,8 +46,9 @@ def main():
         kinds = [k for k, x in sts[0]["kernels"].items() if x["launches"]]
         med = {k: statistics.median(s["kernels"][k]["ms"] for s in sts) for k in kinds}
         tot = statistics.median(s["total_ms"] for s in sts)
+        rounds = [round(statistics.median(s["round_ms"][j] for s in sts), 3) for j in range(sts[-1]["rounds"])]
         print(f"{v:14s} total {tot:7.3f} " + " ".join(f"{k} {x:.3f}" for k, x in med.items())
-              + f" layout {sts[-1].get('round1_layout')}", flush=True)
+              + f" rounds {rounds} layout {sts[-1].get('round1_layout')}", flush=True)
     print("checked", ok)
     b.close()
 

@@ -89,6 +89,21 @@ def test_reference_rerank_permutation(gpu, oracle, kind):
     assert (got == np.arange(70_000, -1, -1, dtype=np.uint32)).all()
 
 
+@pytest.mark.parametrize("debug", [(), ("no_xq",)])
+def test_reference_lsd_queues(gpu, oracle, debug):
+    """The reference schedule's LSD passes with per-XCD queues of tiles
+    (sa_lsd.h XQ: stable in (digit, tile) order, per-queue look-backs and
+    next-pass counts; packed and unpacked 12-byte passes) and without
+    (debug no_xq): SA, round count and every D_j equal the oracle's."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21), ("alnum", 1_500_007), ("binary", 600_001)):
+        t = oracle.gen_text(kind, n, seed=n + 11)
+        got, st = build_suffix_array(t, return_stats=True, schedule="reference", debug=debug)
+        ref, rounds, _, dj = oracle.sa_c(t, stats=True)
+        assert (got == ref).all(), (kind, n, debug)
+        assert st["rounds"] == rounds and st["distinct"] == dj, (kind, n, debug)
+
+
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("radix", ["onesweep", "reduce_scan"])
 def test_radix_algorithms(gpu, oracle, schedule, radix):
@@ -423,7 +438,8 @@ def _multi_rank_worker(rank, world, port, q, large=False):
             dist.all_reduce(tot)
             say("checked large", ok.tolist(), tot.tolist())
             if rank == 0:
-                res["dna_large"] = (bool(ok[0] == 1 and int(tot[0]) == n), d.stats["path"], len(d.stats["unsorted"]))
+                res["dna_large"] = (bool(ok[0] == 1 and int(tot[0]) == n), d.stats["path"], len(d.stats["unsorted"]),
+                                    ops.round1_stats.to_dict()["round1_layout"])
                 q.put(res)
             return
         for name, kind, n, seed in (("dna", "dna", 3_000_017, 8), ("byte256", "byte256", 2_000_003, 2),
@@ -486,6 +502,8 @@ def test_distributed_hip_multi_rank_large(gpu):
     span 32-bit kernel (k_bucket_sort), checked against the single-GPU build."""
     res = _multi_rank(4, large=True)
     assert res["dna_large"][0] and res["dna_large"][1] == "range", res
+    # ~100 M suffixes per range: the second pass by per-XCD queues (sa_split.h SegXq)
+    assert res["dna_large"][3]["xq"], res
 
 
 def _multi_rank(world, large=False):
