@@ -506,10 +506,11 @@ static PermPlan plan_perm(uint64_t n) {
 // buffers (the sorted keys are read by the first step and then free)
 // first-level tiles of the permutation and their head offsets (k_tile_heads)
 constexpr uint64_t kPermTile = (uint64_t)kPermBlock * kPermItems;
+static_assert((kPermTile & (kPermTile - 1)) == 0, "power-of-two first-level tiles");
 static uint32_t* perm_tile_off(sa_context* c) { return c->hist + ((uint64_t)kRadix * kMaxChunks) / 2; }
 
 static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa, const Chunking& ch,
-                          hipStream_t s, Timer& tm, sa_stats* st, uint32_t kshift = 0) {
+                          hipStream_t s, Timer& tm, sa_stats* st, uint32_t kshift = 0, NextHist nh = NextHist{}) {
     const uint64_t n = ch.n;
     const PermPlan p = plan_perm(n);
     const uint64_t half = (uint64_t)kRadix * kMaxChunks / 2;   // cursors below, tile offsets above
@@ -531,12 +532,21 @@ static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa,
                            (const uint64_t*)sorted, d_sa, n, toff, p.s1, 0u, cur1, other);
     const uint64_t* placed = other;
     if (p.s1 > p.s2) {
-        hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3(p.nb1 * p.tpb), dim3(kPermBlock), 0, s,
+        hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3((p.nb1 + 7) / 8 * 8 * p.tpb), dim3(kPermBlock), 0, s,
                            (const uint64_t*)other, n, p.s1, p.s2, p.tpb, cur2, sorted);
         placed = sorted;
     }
-    hipLaunchKernelGGL((k_perm_place<kPermBlock>), dim3((uint32_t)((n + (1ull << kPermSub) - 1) >> kPermSub)),
-                       dim3(kPermBlock), 0, s, placed, n, c->rank, c->words + kPermErrWord);
+    if (nh.out) {   // the next round's first-digit counts too (persistent: one count flush per workgroup)
+        SA_HIP(hipMemsetAsync(nh.out, 0, 8 * kLsdMaxRadix * 4, s));
+        const uint64_t nsub = (n + (1ull << kPermSub) - 1) >> kPermSub;
+        const uint64_t g = std::min<uint64_t>(nsub, 2ull * (uint64_t)c->cus);   // two workgroups per CU
+        const uint32_t spb = (uint32_t)((nsub + g - 1) / g);
+        hipLaunchKernelGGL((k_perm_place<kPermBlock, true>), dim3((uint32_t)((nsub + spb - 1) / spb)),
+                           dim3(kPermBlock), 0, s, placed, n, c->rank, c->words + kPermErrWord, nh, spb);
+    } else {
+        hipLaunchKernelGGL((k_perm_place<kPermBlock>), dim3((uint32_t)((n + (1ull << kPermSub) - 1) >> kPermSub)),
+                           dim3(kPermBlock), 0, s, placed, n, c->rank, c->words + kPermErrWord);
+    }
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_RERANK, (p.s1 > p.s2 ? 48ull : 32ull) * n - (kshift ? 4ull * n : 0ull));
@@ -631,12 +641,32 @@ static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, 
     }
 }
 
+// per-XCD queues of 8192-pair tiles (sa_lsd.h XQ): whether a sort takes
+// them (unpacked passes of 10 bits do not fit their LDS with the per-queue
+// counters) and the queue span
+static bool lsd_xq_ok(const sa_context* c, uint64_t n, const LsdPlan& pl, bool packed) {
+    const uint64_t xtiles = (n + kLsdXqTile - 1) / kLsdXqTile;
+    bool xq = SA_LSD_XQ && c->cus % 8 == 0 && xtiles >= 64 && !(c->dbg & SA_DEBUG_NO_XQ);
+    if (!packed)
+        for (uint32_t p = 0; p < pl.P; ++p) xq = xq && pl.bits[p] <= 9;
+    return xq;
+}
+static void lsd_xq_span(uint64_t n, uint32_t* tpq, uint64_t* qspan, QDiv* qd) {
+    const uint64_t xtiles = (n + kLsdXqTile - 1) / kLsdXqTile;
+    *tpq = (uint32_t)((xtiles + 7) / 8);
+    *qspan = (uint64_t)*tpq * kLsdXqTile;
+    qd->magic = (uint64_t)((((unsigned __int128)1 << 64) + *qspan - 1) / *qspan);
+}
+
 // Stable LSD sort of n pairs by the plan's digits, pass 0 reading `first`.
 // PACKED: one item buffer ping-pong; else keys + values, the last pass
 // writing its values into vals_final.  *sorted = the sorted key / item buffer.
+// hist_ready (XQ): the first pass's per-queue counts are already in
+// lsdx[0] (the previous round's k_perm_place counted them).
 template <bool PACKED, class Src0>
 static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan& pl, uint32_t* vals_final,
-                    uint32_t* vals_other, hipStream_t s, Timer& tm, sa_stats* st, uint64_t** sorted) {
+                    uint32_t* vals_other, hipStream_t s, Timer& tm, sa_stats* st, uint64_t** sorted,
+                    bool hist_ready = false) {
     if (pl.P < 1 || pl.P > kMaxPasses) return set_err(SA_E_INTERNAL, "%u radix passes", pl.P);
     uint64_t* kb[2] = {c->keys[0], c->keys[1]};
     uint32_t* vb[2];
@@ -646,28 +676,26 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
     // the first digit's totals here; every pass counts the next one's
     LsdPlan first_only = pl;
     first_only.P = 1;
-    // per-XCD queues of tiles (sa_lsd.h XQ): 8192-pair tiles, the queue span
-    // tpq tiles
-    const uint64_t xtiles = (n + kLsdXqTile - 1) / kLsdXqTile;
-    // (unpacked passes of 10 bits do not fit their LDS with the per-queue counters)
-    bool xq = SA_LSD_XQ && c->cus % 8 == 0 && xtiles >= 64 && !(c->dbg & SA_DEBUG_NO_XQ);
-    if (!PACKED)
-        for (uint32_t p = 0; p < pl.P; ++p) xq = xq && pl.bits[p] <= 9;
-    if (xq) {
-        const uint32_t tpq = (uint32_t)((xtiles + 7) / 8);
-        const uint64_t qspan = (uint64_t)tpq * kLsdXqTile;
+    // per-XCD queues of tiles (sa_lsd.h XQ)
+    if (lsd_xq_ok(c, n, pl, PACKED)) {
+        uint32_t tpq;
+        uint64_t qspan;
         QDiv qd;
-        qd.magic = (uint64_t)((((unsigned __int128)1 << 64) + qspan - 1) / qspan);
+        lsd_xq_span(n, &tpq, &qspan, &qd);
         uint32_t* const qh = c->lsdx;                                    // [pass][8][1024]
         uint32_t* const qb = qh + kMaxPasses * 8 * kLsdMaxRadix;         // [8][1024]
         uint32_t* const qt = qb + 8 * kLsdMaxRadix;                      // [pass][8 x 32]
-        SA_HIP(hipMemsetAsync(c->lsdx, 0, kLsdXqWords * 4, s));
-        tm.begin(SA_K_HIST_FIRST);
-        hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + 8 * kBlock - 1) / (8 * kBlock),
-                                                                               (uint64_t)c->cus * 4)),
-                           dim3(kBlock), 0, s, first, n, first_only, qh, qd);
-        tm.end();
-        add_bytes(st, SA_K_HIST_FIRST, 8 * n);
+        if (hist_ready) {   // pass 0's counts came with the previous round's re-rank
+            SA_HIP(hipMemsetAsync(c->lsdx + 8 * kLsdMaxRadix, 0, (kLsdXqWords - 8 * kLsdMaxRadix) * 4, s));
+        } else {
+            SA_HIP(hipMemsetAsync(c->lsdx, 0, kLsdXqWords * 4, s));
+            tm.begin(SA_K_HIST_FIRST);
+            hipLaunchKernelGGL(k_lsd_hist<Src0>, dim3((uint32_t)std::min<uint64_t>((n + 8 * kBlock - 1) / (8 * kBlock),
+                                                                                   (uint64_t)c->cus * 4)),
+                               dim3(kBlock), 0, s, first, n, first_only, qh, qd);
+            tm.end();
+            add_bytes(st, SA_K_HIST_FIRST, 8 * n);
+        }
         const uint64_t pair = PACKED ? 8 : 12;
         for (uint32_t p = 0; p < pl.P; ++p) {
             tm.begin(SA_K_SCAN);
@@ -778,6 +806,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint64_t perm_min = perm_min_n(c);
     const uint32_t ib = std::max<uint32_t>(1, bit_width(n - 1));   // index bits of a packed item
     bool used_perm = false;
+    bool hist_ready = false;   // this round's first-digit counts came with the previous re-rank
     for (uint64_t h = 1;; h *= 2) {
         SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t w = bit_width(D);          // ranks are 0..D
@@ -792,8 +821,8 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             const LsdPlan pl = lsd_plan(2 * w, packed ? ib : 0, lsd_max_bits(c));
             P = pl.P;
             rc = packed ? lsd_sort<true>(c, SrcRankPk{c->rank, n, h, w, ib}, n, pl, d_sa, c->vals_alt, s, tm, st,
-                                         &sorted)
-                        : lsd_sort<false>(c, src, n, pl, d_sa, c->vals_alt, s, tm, st, &sorted);
+                                         &sorted, hist_ready)
+                        : lsd_sort<false>(c, src, n, pl, d_sa, c->vals_alt, s, tm, st, &sorted, hist_ready);
         } else {
             rc = radix_sort(c, src, 4 * n, ch, 2 * w, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &sorted,
                             &P);
@@ -835,10 +864,28 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             SA_HIP(hipGetLastError());
             add_bytes(st, SA_K_RERANK, 12 * n);
         }
+        hist_ready = false;
         if (!done) {
             if (use_perm) {
                 used_perm = true;
-                rc = rerank_permute(c, sorted, d_sa, ch, s, tm, st, packed ? ib : 0u);
+                // the next round's first digit lies in rank[i + 2h] alone (its
+                // width <= w'): the re-rank counts it per queue of that round's
+                // LSD passes while it writes rank[] (no histogram read then)
+                NextHist nh;
+                if (c->radix == 0) {
+                    const uint32_t w2 = bit_width(Dn);
+                    const bool packed2 = 2 * w2 + ib <= 64;
+                    const LsdPlan pl2 = lsd_plan(2 * w2, packed2 ? ib : 0, lsd_max_bits(c));
+                    if (pl2.bits[0] <= w2 && lsd_xq_ok(c, n, pl2, packed2)) {
+                        uint32_t tpq;
+                        lsd_xq_span(n, &tpq, &nh.qspan, &nh.qd);
+                        nh.out = c->lsdx;
+                        nh.mask = (1u << pl2.bits[0]) - 1u;
+                        nh.h = 2 * h;
+                        hist_ready = true;
+                    }
+                }
+                rc = rerank_permute(c, sorted, d_sa, ch, s, tm, st, packed ? ib : 0u, nh);
                 if (rc) return rc;
             } else {
                 tm.begin(SA_K_RERANK);

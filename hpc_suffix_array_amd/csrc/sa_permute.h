@@ -23,6 +23,7 @@
 // or in runs of ~32 pairs) instead of 12 read + one random 4-byte write.
 #pragma once
 #include "sa_kernels.h"
+#include "sa_lsd.h"
 
 namespace sa {
 
@@ -107,6 +108,11 @@ __global__ __launch_bounds__(BLOCK) void k_tile_heads(const uint64_t* __restrict
 // from a counting pass measured slower: 223.5 vs 216 ms for the 1 GiB DNA
 // reference schedule, the counts' scattered writes and scan cost more).
 // PACKED: keys are (key << kshift | idx) items (sa_lsd.h k_lsd), idx unused.
+// (Per-XCD sub-ranges of the bins -- tile t claiming from cursor (t mod 8,
+// bin) inside its queue's share of the bin, the shares counted by the
+// round's last LSD pass -- saved ~0.5 ms of the three levels' 44 ms per
+// 1 GiB build and cost the LSD passes ~7 ms of LDS atomics: removed,
+// profiles/r05_k_ab_refsched_perm_xq.txt.)
 template <int BLOCK, int ITEMS, bool PACKED>
 __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ idx, uint64_t n,
@@ -186,7 +192,12 @@ __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict_
     }
 }
 
-// Level 2: tile t of bin b = workgroup b * tpb + t.
+// Level 2: tile t of bin b.  Workgroup w runs on XCD w mod 8 (round robin),
+// so bin b's tiles go to the workgroups w = 8 (t + tpb (b / 8)) + b mod 8:
+// every tile of a bin on one XCD, whose L2 then merges the partial lines
+// where consecutive tiles' runs of a sub-bin meet (~8 pairs per sub-bin and
+// tile) -- one bin per XCD at a time instead of each bin's tiles dealt over
+// all eight.  grid = 8 ceil(nb1 / 8) tpb.
 template <int BLOCK, int ITEMS>
 __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
                                                        uint32_t s2, uint32_t tpb, uint32_t* __restrict__ cur,
@@ -200,7 +211,8 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
     __shared__ uint32_t s_gofs[NB];
     __shared__ uint32_t s_tmp[NB / kWave];
     const uint32_t tid = threadIdx.x;
-    const uint32_t b = blockIdx.x / tpb, t = blockIdx.x % tpb;
+    const uint32_t r = blockIdx.x / 8u;
+    const uint32_t b = (r / tpb) * 8u + (blockIdx.x & 7u), t = r % tpb;
     const uint32_t nsub = 1u << (s1 - s2);
     const uint64_t bin0 = (uint64_t)b << s1;
     const uint64_t bin1 = (bin0 + (1ull << s1)) < n ? bin0 + (1ull << s1) : n;
@@ -246,49 +258,105 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
     }
 }
 
-// Level 3: one workgroup per 2^kPermSub sub-bin; a pair whose idx lies
+// The next reference round's first-digit counts, taken while the ranks are
+// written (the LSD sort's histogram kernel then skips its 8-byte-per-suffix
+// read): its key of position i is (rank[i] << w | rank[i + h]) with the
+// first digit in the low `bits` bits of rank[i + h] (bits <= w), so rank[j]
+// counts for i = j - h, in that position's queue of the next round's LSD
+// passes (sa_lsd.h XQ: out[q][digit]); positions i >= n - h (rank[i + h] =
+// 0: digit 0) are added by workgroup 0.
+struct NextHist {
+    uint32_t* out = nullptr;   // [8][kLsdMaxRadix]; nullptr: none
+    uint32_t mask = 0;
+    uint64_t h = 0;
+    QDiv qd;
+    uint64_t qspan = 0;        // positions per queue (qd divides by it)
+};
+
+// Level 3: sub-bins of 2^kPermSub ranks, one at a time; a pair whose idx lies
 // outside the sub-bin (a broken partition) raises err bit 1 and is dropped.
 // Dense ranks are >= 1, so the sub-bin's LDS copy starts at 0 and a slot
 // still 0 at the write (a missing or duplicated idx) raises err bit 2.
-template <int BLOCK>
+// HIST: the NextHist counts; each workgroup takes a contiguous run of
+// sub-bins (spb of them), whose positions lie in at most two queues of the
+// next round, counted in LDS (2 x 1024 words: two workgroups per CU still)
+// and added to the global counts once.
+template <int BLOCK, bool HIST = false>
 __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict__ in, uint64_t n,
-                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ err) {
+                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ err,
+                                                       NextHist nh = NextHist{}, uint32_t spb = 1) {
     constexpr uint32_t S = 1u << kPermSub;
     __shared__ uint32_t s_r[S];
-    const uint64_t base = (uint64_t)blockIdx.x << kPermSub;
-    const uint32_t valid = (uint32_t)((n - base) < (uint64_t)S ? (n - base) : (uint64_t)S);
-    bool bad = false;
-    for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) s_r[q] = 0u;
-    __syncthreads();
-    for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) {
-        const uint64_t p = in[base + q];
-        const uint32_t x = (uint32_t)(p >> 32);
-        if ((x >> kPermSub) != blockIdx.x || (x & (S - 1u)) >= valid) {
-            bad = true;
-            continue;
-        }
-        s_r[x & (S - 1u)] = (uint32_t)p;
+    __shared__ uint32_t s_h[HIST ? 2 * kLsdMaxRadix : 1];
+    const uint32_t nsub = (uint32_t)((n + S - 1) >> kPermSub);
+    const uint32_t sb0 = HIST ? blockIdx.x * spb : blockIdx.x;
+    const uint32_t sb1 = HIST ? std::min(nsub, sb0 + spb) : std::min(nsub, sb0 + 1);
+    // the queue of this workgroup's first counted position
+    const uint64_t j0 = std::max<uint64_t>((uint64_t)sb0 << kPermSub, nh.h);
+    const uint32_t q0 = HIST ? nh.qd.q(j0 - nh.h) : 0u;
+    if constexpr (HIST) {
+        for (uint32_t i = threadIdx.x; i < 2 * kLsdMaxRadix; i += BLOCK) s_h[i] = 0u;
     }
-    if (bad) atomicOr(err, 2u);
-    __syncthreads();
-    bool hole = false;
-    for (uint32_t q = threadIdx.x * 4; q < valid; q += BLOCK * 4) {
-        if (q + 4 <= valid) {
-            uint4 v;
-            v.x = s_r[q];
-            v.y = s_r[q + 1];
-            v.z = s_r[q + 2];
-            v.w = s_r[q + 3];
-            hole |= (v.x == 0u) | (v.y == 0u) | (v.z == 0u) | (v.w == 0u);
-            *reinterpret_cast<uint4*>(rank + base + q) = v;
-        } else {
-            for (uint32_t i = q; i < valid; ++i) {
-                hole |= s_r[i] == 0u;
-                rank[base + i] = s_r[i];
+    auto count = [&](uint64_t j, uint32_t r) {
+        if (HIST && j >= nh.h) {
+            const uint32_t dq = nh.qd.q(j - nh.h) - q0;   // 0 or 1
+            const uint32_t d = r & nh.mask;
+            if (dq < 2u) atomicAdd(&s_h[dq * kLsdMaxRadix + d], 1u);
+            else atomicAdd(&nh.out[(q0 + dq) * kLsdMaxRadix + d], 1u);   // (not reached: spb sub-bins < a queue)
+        }
+    };
+    bool bad = false, hole = false;
+    for (uint32_t sb = sb0; sb < sb1; ++sb) {
+        const uint64_t base = (uint64_t)sb << kPermSub;
+        const uint32_t valid = (uint32_t)((n - base) < (uint64_t)S ? (n - base) : (uint64_t)S);
+        __syncthreads();   // s_r of the previous sub-bin read out
+        for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) s_r[q] = 0u;
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < valid; q += BLOCK) {
+            const uint64_t p = in[base + q];
+            const uint32_t x = (uint32_t)(p >> 32);
+            if ((x >> kPermSub) != sb || (x & (S - 1u)) >= valid) {
+                bad = true;
+                continue;
+            }
+            s_r[x & (S - 1u)] = (uint32_t)p;
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x * 4; q < valid; q += BLOCK * 4) {
+            if (q + 4 <= valid) {
+                uint4 v;
+                v.x = s_r[q];
+                v.y = s_r[q + 1];
+                v.z = s_r[q + 2];
+                v.w = s_r[q + 3];
+                hole |= (v.x == 0u) | (v.y == 0u) | (v.z == 0u) | (v.w == 0u);
+                *reinterpret_cast<uint4*>(rank + base + q) = v;
+                count(base + q, v.x);
+                count(base + q + 1, v.y);
+                count(base + q + 2, v.z);
+                count(base + q + 3, v.w);
+            } else {
+                for (uint32_t i = q; i < valid; ++i) {
+                    hole |= s_r[i] == 0u;
+                    rank[base + i] = s_r[i];
+                    count(base + i, s_r[i]);
+                }
             }
         }
     }
+    if (bad) atomicOr(err, 2u);
     if (hole) atomicOr(err, 4u);
+    if constexpr (HIST) {
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < 2 * kLsdMaxRadix; i += BLOCK)
+            if (s_h[i] && q0 + i / kLsdMaxRadix < 8u) atomicAdd(&nh.out[q0 * kLsdMaxRadix + i], s_h[i]);
+        if (blockIdx.x == 0 && threadIdx.x < 8) {   // positions [n - h, n) of queue t: digit 0
+            const uint64_t lo = nh.h < n ? n - nh.h : 0;
+            const uint64_t a = std::max<uint64_t>(lo, threadIdx.x * nh.qspan);
+            const uint64_t b = std::min<uint64_t>(n, (threadIdx.x + 1) * nh.qspan);
+            if (b > a) atomicAdd(&nh.out[threadIdx.x * kLsdMaxRadix], (uint32_t)(b - a));
+        }
+    }
 }
 
 }  // namespace sa
