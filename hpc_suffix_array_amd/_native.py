@@ -48,7 +48,8 @@ class SAError(RuntimeError):
 # sa_opts.debug flags (include/sa_hip.h SA_DEBUG_*): alternative paths the
 # tests force; every combination gives the same suffix array
 DEBUG_FLAGS = {"no_cmp": 0x1, "no_pk8": 0x2, "no_pad": 0x4, "pad_overflow": 0x8, "no_fast32": 0x10,
-               "no_pivot": 0x20, "perm_always": 0x40, "no_xq": 0x80, "xq_overflow": 0x100}
+               "no_pivot": 0x20, "perm_always": 0x40, "no_xq": 0x80, "xq_overflow": 0x100,
+               "no_tied": 0x200}
 
 
 def debug_bits(names) -> int:
@@ -108,7 +109,7 @@ class SaStats(ctypes.Structure):
             "init_chars": self.init_chars,
             "sigma": self.sigma,
             "sparse_ranks": bool(self.sparse_ranks),
-            "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed"}.get(self.round1, "lsd"),
+            "round1": {ROUND1_LSD: "lsd", ROUND1_BUCKETED: "bucketed", 3: "pivot"}.get(self.round1, "lsd"),
             "largest_window": self.largest_window,
             "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow", 3: "striped-records",
                                 4: "striped-records-overflow"}.get(self.round1_segments, "exact"),

@@ -972,10 +972,12 @@ template <class Pos>
 static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, const Chunking& ch, Pos pos,
                     bool sparse_ok, bool* sparse_out,
                     uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
-                    uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0, RankMap rm = RankMap{}) {
+                    uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0, RankMap rm = RankMap{},
+                    uint64_t set_off = 0, uint32_t g_off = 0) {
     // rank_arr / rank_off / rm: the range-partitioned build's compact rank map
     // and its SA offset (sa_dist.h); the context's rank array, 0 and the
-    // identity map on one GPU
+    // identity map on one GPU.  set_off / g_off: the next unsorted set's
+    // first slot and group id (the tied-block round's rest, sa_pivot.h)
     if (!rank_arr) rank_arr = c->rank;
     uint32_t* c_h = c->counts;
     uint32_t* c_u = c->counts + kMaxChunks;
@@ -1005,7 +1007,8 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     tm.begin(SA_K_SEG_WRITE);
     hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
                        (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, rank_arr, sa,
-                       c->u_pos[uo], c->u_idx[uo], c->u_g[uo], member, sparse ? 0 : 1, (uint32_t)rank_off, rm);
+                       c->u_pos[uo] + set_off, c->u_idx[uo] + set_off, c->u_g[uo] + set_off, member, sparse ? 0 : 1,
+                       (uint32_t)rank_off, rm, g_off);
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);
@@ -1021,14 +1024,27 @@ static bool pivot_ok(const sa_context* c, uint64_t m, uint64_t G, uint32_t wr, b
     return !(c->dbg & SA_DEBUG_NO_PIVOT) && c->radix == 0 && !sparse && m >= (1u << 16) && G >= 1 && G <= m / 4 && bit_width(2 * G + 1) + wr <= 64;
 }
 
+// tied-block rounds (sa_pivot.h) scan the groups in one workgroup
+constexpr uint64_t kPivotTiedMaxG = 1u << 18;
+
 static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, uint64_t G, uint64_t h, uint32_t wr,
-                       uint64_t* ukb0, uint64_t* ukb1, uint64_t* kbA, const Chunking& cu, hipStream_t s, Timer& tm,
-                       sa_stats* st, uint64_t** sorted, uint32_t* P) {
+                       uint64_t* ukb0, uint64_t* ukb1, uint64_t* kbA, const Chunking& cu, uint32_t* d_sa,
+                       hipStream_t s, Timer& tm, sa_stats* st, uint64_t** sorted, uint32_t* P, bool* segs_done,
+                       uint64_t* Du, uint64_t* m2, uint64_t* G2) {
     *sorted = nullptr;
-    uint32_t* const gs = c->u_pos[uo];   // G + 1 group starts (the next set is written by segments())
-    uint32_t* const pr = gs + G + 1;     // G pivot ranks (2 G + 1 <= m / 2 + 1 words of the buffer)
-    uint32_t* const gP = c->vals_alt;    // 3 (G + 1): members of each class before each group
-    uint32_t* const cc = c->hist;        // 3 x chunks class counts, scanned in place
+    *segs_done = false;
+    // tied-block round: its scratch is ukb0 (free: the tied members skip the
+    // sorted output) -- gs, pr, toff, tid, then the rest's values (3 x
+    // m' <= 3 m / 2 words)
+    const uint64_t scap = 2 * align_up(c->cap, 64);
+    const uint64_t sbase = align_up(4 * G + 3, 64);
+    const uint64_t ra_max = align_up(m / 2, 64);
+    const bool tied = !(c->dbg & SA_DEBUG_NO_TIED) && G <= kPivotTiedMaxG && sbase + 3 * ra_max <= scap;
+    uint32_t* const scr = reinterpret_cast<uint32_t*>(ukb0);
+    uint32_t* const gs = tied ? scr : c->u_pos[uo];   // G + 1 group starts
+    uint32_t* const pr = gs + G + 1;                  // G pivot ranks
+    uint32_t* const gP = c->vals_alt;                 // 3 (G + 1): members of each class before each group
+    uint32_t* const cc = c->hist;                     // 3 x chunks class counts, scanned in place
     const uint32_t Gu = (uint32_t)G;
     tm.begin(SA_K_SORT_U);
     hipLaunchKernelGGL(k_pivot_keys, dim3((uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192)), dim3(kBlock),
@@ -1036,7 +1052,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
                        n, h, wr, Gu, ukb1, gs, pr);
     hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
                        (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
-                       (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr);
+                       (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
     hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
     tm.end();
     SA_HIP(hipGetLastError());
@@ -1047,41 +1063,166 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     if (t0 + t1 + t2 != m) return set_err(SA_E_INTERNAL, "pivot classes %llu + %llu + %llu != %llu",
                                           (unsigned long long)t0, (unsigned long long)t1, (unsigned long long)t2,
                                           (unsigned long long)m);
-    SA_TRACE("  round h=%llu: pivot split, tied %llu of %llu", (unsigned long long)h, (unsigned long long)t1,
-             (unsigned long long)m);
+    SA_TRACE("  round h=%llu: pivot split, tied %llu of %llu%s", (unsigned long long)h, (unsigned long long)t1,
+             (unsigned long long)m, tied ? " (tied blocks to the next set)" : "");
     if (t1 * 2 < m) return SA_OK;   // mostly distinct keys: the full sort is cheaper
     tm.begin(SA_K_SORT_U);
     hipLaunchKernelGGL(k_pivot_gp, dim3((uint32_t)std::min<uint64_t>((G + kBlock) / kBlock, 8192)), dim3(kBlock), 0, s,
                        (const uint32_t*)gs, Gu, (const uint32_t*)cc, cu, (const uint32_t*)c->totals, gP);
-    hipLaunchKernelGGL(k_pivot_pass<2>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
-                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
-                       (const uint32_t*)pr, Gu, wr, cc, gP, ukb0, c->vals_u, kbA, c->u_idx[uo]);
+    const uint64_t mr = t0 + t2;
+    const uint64_t ra = align_up(mr, 64);
+    uint32_t* const ridx = tied ? scr + sbase : c->u_idx[uo];
+    uint64_t T = 0, Gt = 0, Dt = 0;
+    if (tied) {
+        uint32_t* const toff = scr + 2 * G + 1;
+        uint32_t* const tid = toff + G + 1;
+        hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, Gu, toff, tid,
+                           c->totals + 4);
+        const TiedOut to{c->u_pos[ui], toff, tid, c->rank, d_sa, c->u_pos[uo], c->u_idx[uo], c->u_g[uo]};
+        hipLaunchKernelGGL(k_pivot_pass<3>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
+                           (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                           (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, kbA, ridx, to);
+    } else {
+        hipLaunchKernelGGL(k_pivot_pass<2>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
+                           (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                           (const uint32_t*)pr, Gu, wr, cc, gP, ukb0, c->vals_u, kbA, ridx, TiedOut{});
+    }
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_SORT_U, 36 * m);
-    const uint64_t mr = t0 + t2;
+    add_bytes(st, SA_K_SORT_U, tied ? 16 * m + 16 * t1 + 12 * mr : 36 * m);
+    if (tied) {
+        SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
+        SA_HIP(hipStreamSynchronize(s));
+        T = c->host_words[20];
+        Gt = c->host_words[21];
+        Dt = c->host_words[22];
+        if (T > t1 || Gt > G || Dt > G)
+            return set_err(SA_E_INTERNAL, "tied blocks %llu / %llu / %llu out of range", (unsigned long long)T,
+                           (unsigned long long)Gt, (unsigned long long)Dt);
+    }
     uint32_t Pr = 0;
+    uint64_t Dr = 0, mrr = 0, Gr = 0;
     if (mr > 0) {
         // the rest sorted by (2 g + [> pivot], rank): values in u_idx / u_g
-        // of the next set (free until segments()), keys through kbA and ukb1
+        // of the next set (free until segments()) or the tied round's
+        // scratch, keys through kbA and ukb1
         const uint32_t bits = bit_width(2 * G - 1) + wr;
         const uint32_t Pn = (bits + 7) / 8;
-        uint32_t* vfinal = (Pn & 1u) ? c->u_g[uo] : c->u_idx[uo];
-        uint32_t* vother = (Pn & 1u) ? c->u_idx[uo] : c->u_g[uo];
+        uint32_t* const va = tied ? ridx + ra : c->u_g[uo];
+        uint32_t* const vb = tied ? ridx + 2 * ra : c->u_idx[uo];
+        uint32_t* vfinal = (Pn & 1u) ? va : vb;
+        uint32_t* vother = (Pn & 1u) ? vb : va;
         uint64_t* rs = nullptr;
-        int rc = radix_sort(c, SrcKeys{kbA, c->u_idx[uo]}, 12 * mr, plan_chunks(mr), bits, vfinal, vother, ukb1, kbA, s,
-                            tm, st, &rs, &Pr, false, true);
+        int rc = radix_sort(c, SrcKeys{kbA, ridx}, 12 * mr, plan_chunks(mr), bits, vfinal, vother, ukb1, kbA, s, tm,
+                            st, &rs, &Pr, false, true);
         if (rc) return rc;
         tm.begin(SA_K_SORT_U);
-        hipLaunchKernelGGL(k_pivot_place, dim3((uint32_t)std::min<uint64_t>((mr + kBlock - 1) / kBlock, 8192)),
-                           dim3(kBlock), 0, s, (const uint64_t*)rs, (const uint32_t*)vfinal, mr, (const uint32_t*)gs,
-                           (const uint32_t*)gP, Gu, wr, ukb0, c->vals_u, m);
+        const dim3 pg((uint32_t)std::min<uint64_t>((mr + kBlock - 1) / kBlock, 8192));
+        if (tied)
+            hipLaunchKernelGGL(k_pivot_place<true>, pg, dim3(kBlock), 0, s, (const uint64_t*)rs,
+                               (const uint32_t*)vfinal, mr, (const uint32_t*)gs, (const uint32_t*)gP, Gu, wr, nullptr,
+                               nullptr, m, (const uint32_t*)c->u_pos[ui], c->vals_u);
+        else
+            hipLaunchKernelGGL(k_pivot_place<false>, pg, dim3(kBlock), 0, s, (const uint64_t*)rs,
+                               (const uint32_t*)vfinal, mr, (const uint32_t*)gs, (const uint32_t*)gP, Gu, wr, ukb0,
+                               c->vals_u, m, nullptr, nullptr);
         tm.end();
         SA_HIP(hipGetLastError());
-        add_bytes(st, SA_K_SORT_U, 24 * mr);
+        add_bytes(st, SA_K_SORT_U, tied ? 20 * mr : 24 * mr);
+        if (tied) {
+            // the rest's segments, appended to the next set after the tied blocks
+            rc = segments(c, rs, vfinal, plan_chunks(mr), PosArray{c->vals_u}, false, nullptr, d_sa, uo, s, tm, st,
+                          &Dr, &mrr, &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt);
+            if (rc) return rc;
+        }
+    }
+    *P = 1 + Pr;
+    if (tied) {
+        *segs_done = true;
+        *Du = Dr + Dt;
+        *m2 = mrr + T;
+        *G2 = Gr + Gt;
     }
     *sorted = ukb0;
-    *P = 1 + Pr;
+    return SA_OK;
+}
+
+// Round 1 by the pivot split (sa_pivot.h, R1): when the LSD round 1 would
+// run and at least half of all suffixes share the key of suffix 0 (a text of
+// one repeated symbol, configs[4]: all but the last K), those form one tied
+// block -- ranks and the next unsorted set written directly -- and only the
+// rest is radix sorted (then segments() over it, SA positions around the
+// block's gap).  *done = false (nothing written but the class counts) when
+// fewer share it: the caller runs the LSD sort.
+static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_sa, hipStream_t s, Timer& tm,
+                        sa_stats* st, bool* done, uint64_t* D, uint64_t* m, uint64_t* G, uint32_t* P) {
+    *done = false;
+    const Chunking ch = plan_chunks(n);
+    const uint64_t* keys = c->keys[1];
+    uint32_t* const gs = c->u_pos[1];   // {0, n}: one group
+    uint32_t* const toff = gs + 2;
+    uint32_t* const tid = gs + 4;
+    uint32_t* const gP = c->vals_alt;   // 3 x 2
+    uint32_t* const cc = c->hist;       // 3 x chunks class counts
+    c->host_words[24] = 0;
+    c->host_words[25] = (uint32_t)n;
+    SA_HIP(hipMemcpyAsync(gs, c->host_words + 24, 8, hipMemcpyHostToDevice, s));
+    tm.begin(SA_K_SORT_U);
+    hipLaunchKernelGGL((k_pivot_pass<0, true>), dim3(ch.chunks), dim3(kBlock), 0, s, keys, nullptr, nullptr, ch,
+                       (const uint32_t*)gs, nullptr, 1u, 0u, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
+    hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, ch.chunks, c->totals);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_SORT_U, 8 * n);
+    SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
+    if (t0 + t1 + t2 != n) return set_err(SA_E_INTERNAL, "round-1 pivot classes %llu + %llu + %llu != %llu",
+                                          (unsigned long long)t0, (unsigned long long)t1, (unsigned long long)t2,
+                                          (unsigned long long)n);
+    SA_TRACE("  round 1: pivot split, tied %llu of %llu", (unsigned long long)t1, (unsigned long long)n);
+    if (t1 * 2 < n) return SA_OK;
+    const uint64_t mr = t0 + t2;
+    // the rest: keys -> keys[0], values ping-pong in u_idx[1] / u_g[1] (the
+    // next set goes to u_*[0]), key buffers keys_u / keys[0]
+    uint64_t* const rk = c->keys[0];
+    uint32_t* const ridx = c->u_idx[1];
+    tm.begin(SA_K_SORT_U);
+    hipLaunchKernelGGL(k_pivot_gp, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gs, 1u, (const uint32_t*)cc, ch,
+                       (const uint32_t*)c->totals, gP);
+    hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, 1u, toff, tid,
+                       c->totals + 4);
+    const TiedOut to{nullptr, toff, tid, c->rank, d_sa, c->u_pos[0], c->u_idx[0], c->u_g[0]};
+    hipLaunchKernelGGL((k_pivot_pass<3, true>), dim3(ch.chunks), dim3(kBlock), 0, s, keys, nullptr, nullptr, ch,
+                       (const uint32_t*)gs, nullptr, 1u, 0u, cc, gP, nullptr, nullptr, rk, ridx, to);
+    tm.end();
+    SA_HIP(hipGetLastError());
+    add_bytes(st, SA_K_SORT_U, 8 * n + 16 * t1 + 12 * mr);
+    SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    const uint64_t T = c->host_words[20], Gt = c->host_words[21], Dt = c->host_words[22];
+    if (T > t1 || Gt > 1 || Dt > 1)
+        return set_err(SA_E_INTERNAL, "round-1 tied block %llu / %llu / %llu out of range", (unsigned long long)T,
+                       (unsigned long long)Gt, (unsigned long long)Dt);
+    uint32_t Pr = 0;
+    uint64_t Dr = 0, mrr = 0, Gr = 0;
+    if (mr > 0) {
+        const uint32_t Pn = (bits1 + 7) / 8;
+        uint32_t* const vfinal = (Pn & 1u) ? c->u_g[1] : ridx;
+        uint32_t* const vother = (Pn & 1u) ? ridx : c->u_g[1];
+        uint64_t* rs = nullptr;
+        int rc = radix_sort(c, SrcKeys{rk, ridx}, 12 * mr, plan_chunks(mr), bits1, vfinal, vother, c->keys_u, rk, s,
+                            tm, st, &rs, &Pr);
+        if (rc) return rc;
+        rc = segments(c, rs, vfinal, plan_chunks(mr), PosGap{t0, t1}, false, nullptr, d_sa, 0, s, tm, st, &Dr, &mrr,
+                      &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt);
+        if (rc) return rc;
+    }
+    *done = true;
+    *D = Dr + Dt;
+    *m = mrr + T;
+    *G = Gr + Gt;
+    *P = 2 + Pr;
     return SA_OK;
 }
 
@@ -1131,6 +1272,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     if (bucketed && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
         bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, false);
     bool fused = false;
+    bool r1_pivot = false;   // round 1 by the pivot split (pivot_round1)
+    uint64_t D = 0, m = 0, G = 0;
     uint64_t seg1[3] = {0, 0, 0};
     if (bucketed) {
         bool done = false;
@@ -1158,20 +1301,26 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         tm.end();
         SA_HIP(hipGetLastError());
         add_bytes(st, SA_K_PACK, 9 * n);
-        SrcKeysIota src{c->keys[1]};
-        rc = radix_sort(c, src, 8 * n, ch, bits1, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &keys1, &P,
-                        true);
-        if (rc) return rc;
+        if (c->radix == 0 && !(c->dbg & SA_DEBUG_NO_PIVOT) && n >= (1u << 16)) {
+            rc = pivot_round1(c, n, bits1, d_sa, s, tm, st, &r1_pivot, &D, &m, &G, &P);
+            if (rc) return rc;
+        }
+        if (!r1_pivot) {
+            SrcKeysIota src{c->keys[1]};
+            rc = radix_sort(c, src, 8 * n, ch, bits1, d_sa, c->vals_alt, c->keys[0], c->keys[1], s, tm, st, &keys1,
+                            &P, true);
+            if (rc) return rc;
+        }
     }
     if (st) {
         st->init_chars = (int32_t)K;
         st->sigma = (int32_t)sigma;
-        st->round1 = bucketed ? SA_ROUND1_BUCKETED : SA_ROUND1_LSD;
+        st->round1 = bucketed ? SA_ROUND1_BUCKETED : r1_pivot ? SA_ROUND1_PIVOT : SA_ROUND1_LSD;
     }
-    uint64_t D, m, G;
     int uo = 0;
     bool sparse = false;
-    if (bucketed && fused) {   // segments came with the local sort (sparse ranks)
+    if (r1_pivot) {   // pivot_round1 ran the segments (dense ranks)
+    } else if (bucketed && fused) {   // segments came with the local sort (sparse ranks)
         D = seg1[0];
         m = seg1[1];
         G = seg1[2];
@@ -1205,6 +1354,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         const int ui = uo;
         uo ^= 1;
         uint64_t* sorted = nullptr;
+        bool segs_done = false;   // a tied-block pivot round ran its own segments
+        uint64_t Du = 0, m2 = 0, G2 = 0;
         if (c->radix == 0 && G > 0 && m <= kUsAvg * G) {
             // small groups on average: sort each group in registers, unless
             // one of them is larger than kUsLimit (then the radix sort below)
@@ -1247,7 +1398,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         }
         if (!sorted && pivot_ok(c, m, G, wr, sparse)) {
             uint64_t* kbA = ukb0 == c->keys[0] ? c->keys[1] : c->keys[0];   // the round-1 keys: dead with dense ranks
-            rc = pivot_round(c, ui, uo, n, m, G, h, wr, ukb0, ukb1, kbA, cu, s, tm, st, &sorted, &P);
+            rc = pivot_round(c, ui, uo, n, m, G, h, wr, ukb0, ukb1, kbA, cu, d_sa, s, tm, st, &sorted, &P,
+                             &segs_done, &Du, &m2, &G2);
             if (rc) return rc;
         }
         if (sorted) {
@@ -1281,10 +1433,11 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
                             false, true);
         }
         if (rc) return rc;
-        uint64_t Du, m2, G2;
-        rc = segments(c, sorted, c->vals_u, cu, PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm, st, &Du,
-                      &m2, &G2);
-        if (rc) return rc;
+        if (!segs_done) {
+            rc = segments(c, sorted, c->vals_u, cu, PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm, st, &Du,
+                          &m2, &G2);
+            if (rc) return rc;
+        }
         SA_HIP(hipEventRecord(ev.e[1], s));
         SA_HIP(hipEventSynchronize(ev.e[1]));
         tm.flush();

@@ -947,6 +947,12 @@ struct PosArray {
     const uint32_t* __restrict__ p;
     __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return p[s]; }
 };
+// the pivot round 1's sorted rest (sa_pivot.h): t0 keys below the pivot at
+// 0..t0-1, then a gap of t1 tied suffixes, then the keys above it
+struct PosGap {
+    uint64_t t0, t1;
+    __device__ __forceinline__ uint32_t operator()(uint64_t s) const { return (uint32_t)(s < t0 ? s : s + t1); }
+};
 
 // Keys of one wave's 16 rows of 64 (s = w0 + 64 j + lane), all loads issued
 // before any is used; lane 0 / 63 also fetch the key before / after its row.
@@ -1142,7 +1148,8 @@ struct RankMap {
 //   rank[idx]   = pos(head of s's group) + 1  (at rm.slot(idx))
 //   sa[pos(s)]  = idx                               (when sa != nullptr)
 //   unsorted members are compacted, in order, to (u_pos, u_idx, u_g) with
-//   u_g the dense id of their group among unsorted groups.
+//   u_g the dense id of their group among unsorted groups (+ g_off: the
+//   tied-block round puts its tied groups first, sa_pivot.h).
 template <class Pos>
 __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ idx, Chunking ch, Pos pos,
@@ -1152,7 +1159,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                                                       uint32_t* __restrict__ rank, uint32_t* __restrict__ sa,
                                                       uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
                                                       uint32_t* __restrict__ u_g, uint32_t* __restrict__ member,
-                                                      int dense_rank, uint32_t rank_off, RankMap rm = RankMap{}) {
+                                                      int dense_rank, uint32_t rank_off, RankMap rm = RankMap{},
+                                                      uint32_t g_off = 0) {
     __shared__ uint64_t s_m[kWaves][kItems][3];
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
@@ -1239,7 +1247,7 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                     const uint32_t q = off_u + (uint32_t)__popcll(mu & lt);
                     u_pos[q] = p;
                     u_idx[q] = x;
-                    u_g[q] = off_uh + (uint32_t)__popcll(muh & le) - 1u;
+                    u_g[q] = g_off + off_uh + (uint32_t)__popcll(muh & le) - 1u;
                 }
             }
             off_u += __popcll(mu);

@@ -31,6 +31,16 @@
 //   k_pivot_gp      gP[c][g] = P_c(gs_g) (members of class c before g)
 //   k_pivot_pass<2> tied members to their final slots, the rest compacted
 //   k_pivot_place   the sorted rest to their final slots
+// Tied-block round (pivot_round's default when G is small): the tied block of
+// group g is already one group of the next round, so nothing of it needs the
+// segment scan -- k_pivot_pass<3> writes each tied member's rank (its block's
+// first SA position + 1, as k_seg_write would), the SA entry of a one-member
+// block, and the next unsorted set's entries (u_pos, u_idx, u_g) of blocks of
+// two or more at the front of that set (block ids 0..Gt-1 in group order,
+// offsets from k_pivot_tied_scan); only the sorted rest goes through
+// segments(), appended after them with group ids from Gt.  Per tied member
+// 36 bytes (keys, u_g, u_idx read; rank and three set words written) instead
+// of the 84 of pass<2> + k_seg_count + k_seg_write.
 #pragma once
 #include "sa_kernels.h"
 
@@ -55,13 +65,29 @@ __global__ __launch_bounds__(kBlock) void k_pivot_keys(const uint32_t* __restric
     }
 }
 
+// where k_pivot_pass<3> puts the tied members (see the header)
+struct TiedOut {
+    const uint32_t* __restrict__ pos_in = nullptr;   // the round's u_pos: SA position per U slot
+    const uint32_t* __restrict__ toff = nullptr;     // per group: next-set offset of its tied block
+    const uint32_t* __restrict__ tid = nullptr;      // per group: the tied block's next-set group id
+    uint32_t* __restrict__ rank = nullptr;
+    uint32_t* __restrict__ sa = nullptr;
+    uint32_t* __restrict__ u_pos = nullptr;
+    uint32_t* __restrict__ u_idx = nullptr;
+    uint32_t* __restrict__ u_g = nullptr;
+};
+
 // MODE 0: cc[c * chunks + chunk] = members of class c in the chunk, and for
 //         every group starting in the chunk gP[c * (G + 1) + g] = members of
 //         class c before gs_g inside the chunk (k_pivot_gp adds the chunk's
 //         scanned offset).
 // MODE 2: tied members -> okeys / oidx at their final slots; the rest ->
 //         rkeys / ridx at (members of classes 0 and 2 before them).
-template <int MODE>
+// MODE 3: the rest as MODE 2; tied members -> rank / sa / next set (TiedOut).
+// R1: round 1 (build_packed's pivot round 1): every suffix in one group, index
+//     e itself, keys the packed K-symbol keys, pivot keys[0]; the rest keeps
+//     its plain key (one group: key order already puts < p before > p).
+template <int MODE, bool R1 = false>
 __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ u_idx,
                                                        const uint32_t* __restrict__ u_g, Chunking ch,
@@ -69,16 +95,18 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                                                        uint32_t G, uint32_t wr,
                                                        uint32_t* __restrict__ cc, uint32_t* __restrict__ gP,
                                                        uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
-                                                       uint64_t* __restrict__ rkeys, uint32_t* __restrict__ ridx) {
+                                                       uint64_t* __restrict__ rkeys, uint32_t* __restrict__ ridx,
+                                                       TiedOut to = TiedOut{}) {
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint64_t lt = lanemask_lt();
     uint32_t run[3] = {0, 0, 0};
-    if (MODE == 2)
+    if (MODE != 0)
         for (int k = 0; k < 3; ++k) run[k] = cc[(uint64_t)k * ch.chunks + c];
     const uint64_t gstride = (uint64_t)G + 1;
+    const uint64_t p1 = R1 ? keys[0] : 0ull;
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
         uint64_t key[kItems];
@@ -87,14 +115,14 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
         for (int j = 0; j < kItems; ++j) {
             const uint64_t e = w0 + (uint64_t)j * kWave + lane;
             key[j] = e < e1 ? keys[e] : 0ull;
-            g[j] = e < e1 ? u_g[e] : 0u;
+            g[j] = (e < e1 && !R1) ? u_g[e] : 0u;
         }
         uint32_t cls[kItems];
         uint32_t wc[3] = {0, 0, 0};
 #pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t e = w0 + (uint64_t)j * kWave + lane;
-            const uint64_t p = e < e1 ? (((uint64_t)g[j] << wr) | pr[g[j]]) : 0ull;
+            const uint64_t p = R1 ? p1 : e < e1 ? (((uint64_t)g[j] << wr) | pr[g[j]]) : 0ull;
             cls[j] = e < e1 ? (key[j] < p ? 0u : key[j] == p ? 1u : 2u) : 3u;
 #pragma unroll
             for (int k = 0; k < 3; ++k) wc[k] += (uint32_t)__popcll(__ballot(cls[j] == (uint32_t)k));
@@ -125,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                     const uint32_t P1 = off[1] + (uint32_t)__popcll(bm[1] & lt);
                     const uint32_t P2 = off[2] + (uint32_t)__popcll(bm[2] & lt);
                     const uint32_t gg = g[j];
-                    const uint32_t s0 = gs[gg];
+                    const uint32_t s0 = R1 ? 0u : gs[gg];
                     if (MODE == 0) {
                         if (s0 == (uint32_t)e) {   // in-chunk counts before the group start
                             gP[gg] = P0;
@@ -133,16 +161,32 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                             gP[2 * gstride + gg] = P2;
                         }
                     } else {
-                        const uint32_t x = u_idx[e];
-                        if (cls[j] == 1u) {
+                        const uint32_t x = R1 ? (uint32_t)e : u_idx[e];
+                        if (MODE == 3 && cls[j] == 1u) {
+                            const uint32_t cnt0 = gP[gg + 1] - gP[gg];
+                            const uint32_t b1 = gP[gstride + gg];
+                            const uint32_t cnt1 = gP[gstride + gg + 1] - b1;
+                            const uint32_t t = P1 - b1;
+                            const uint32_t bp = (R1 ? 0u : to.pos_in[s0]) + cnt0;   // the block's first SA position
+                            to.rank[x] = bp + 1u;
+                            if (cnt1 == 1u) {
+                                to.sa[bp] = x;
+                            } else {
+                                const uint32_t q = to.toff[gg] + t;
+                                to.u_pos[q] = bp + t;
+                                to.u_idx[q] = x;
+                                to.u_g[q] = to.tid[gg];
+                            }
+                        } else if (cls[j] == 1u) {
                             const uint32_t cnt0 = gP[gg + 1] - gP[gg];
                             const uint64_t ne = (uint64_t)s0 + cnt0 + (P1 - gP[gstride + gg]);
                             okeys[ne] = key[j];
                             oidx[ne] = x;
                         } else {
                             const uint64_t ri = (uint64_t)P0 + P2;
-                            rkeys[ri] = ((uint64_t)(2u * gg + (cls[j] == 2u ? 1u : 0u)) << wr) |
-                                        (key[j] & ((1ull << wr) - 1ull));
+                            rkeys[ri] = R1 ? key[j]
+                                           : ((uint64_t)(2u * gg + (cls[j] == 2u ? 1u : 0u)) << wr) |
+                                                 (key[j] & ((1ull << wr) - 1ull));
                             ridx[ri] = x;
                         }
                     }
@@ -175,14 +219,65 @@ __global__ __launch_bounds__(kBlock) void k_pivot_gp(const uint32_t* __restrict_
     }
 }
 
+// toff[g] / tid[g] (k_pivot_pass<3>): exclusive scans over the groups of the
+// tied block sizes of two or more and of the number of such blocks;
+// totals[0..2] = (members of such blocks, such blocks, nonempty blocks).  One
+// workgroup (pivot_round takes this path for G <= kPivotTiedMaxG only).
+__global__ __launch_bounds__(kBlock) void k_pivot_tied_scan(const uint32_t* __restrict__ gP, uint32_t G,
+                                                            uint32_t* __restrict__ toff, uint32_t* __restrict__ tid,
+                                                            uint32_t* __restrict__ totals) {
+    __shared__ uint32_t s_tmp[kWaves];
+    const uint32_t* const g1 = gP + (uint64_t)G + 1;   // class-1 members before each group
+    uint32_t ct = 0, cb = 0, cd = 0;
+    for (uint32_t base = 0; base < G; base += kBlock * 4) {
+        uint32_t vt[4], vb[4], st = 0, sb = 0, sd = 0;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = base + threadIdx.x * 4 + j;
+            const uint32_t cnt = i < G ? g1[i + 1] - g1[i] : 0u;
+            vt[j] = cnt >= 2u ? cnt : 0u;
+            vb[j] = cnt >= 2u ? 1u : 0u;
+            st += vt[j];
+            sb += vb[j];
+            sd += cnt ? 1u : 0u;
+        }
+        uint32_t tt, tb, td;
+        uint32_t ot = block_exclusive_sum(st, s_tmp, &tt) + ct;
+        uint32_t ob = block_exclusive_sum(sb, s_tmp, &tb) + cb;
+        (void)block_exclusive_sum(sd, s_tmp, &td);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t i = base + threadIdx.x * 4 + j;
+            if (i < G) {
+                toff[i] = ot;
+                tid[i] = ob;
+            }
+            ot += vt[j];
+            ob += vb[j];
+        }
+        ct += tt;
+        cb += tb;
+        cd += td;
+    }
+    if (threadIdx.x == 0) {
+        totals[0] = ct;
+        totals[1] = cb;
+        totals[2] = cd;
+    }
+}
+
 // the sorted rest (keys (2 g + [> p]) << wr | rank) to the final slots of
-// their group: class 0 first, class 2 after the tied block
+// their group: class 0 first, class 2 after the tied block.  POS: only each
+// member's SA position, rpos[j] = pos_in[slot] (the tied-block round keeps
+// the rest in sorted order and runs segments() over it).
+template <bool POS>
 __global__ __launch_bounds__(kBlock) void k_pivot_place(const uint64_t* __restrict__ rkeys,
                                                         const uint32_t* __restrict__ ridx, uint64_t mr,
                                                         const uint32_t* __restrict__ gs,
                                                         const uint32_t* __restrict__ gP, uint32_t G, uint32_t wr,
                                                         uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
-                                                        uint64_t m) {
+                                                        uint64_t m, const uint32_t* __restrict__ pos_in = nullptr,
+                                                        uint32_t* __restrict__ rpos = nullptr) {
     const uint64_t gstride = (uint64_t)G + 1;
     for (uint64_t j = (uint64_t)blockIdx.x * kBlock + threadIdx.x; j < mr; j += (uint64_t)gridDim.x * kBlock) {
         const uint64_t k = rkeys[j];
@@ -193,8 +288,12 @@ __global__ __launch_bounds__(kBlock) void k_pivot_place(const uint64_t* __restri
         const uint32_t cnt1 = gP[gstride + g + 1] - gP[gstride + g];
         const uint64_t ne = (sub & 1u) ? (uint64_t)gs[g] + cnt1 + (j - R) : (uint64_t)gs[g] + (j - R);
         if (ne < m) {
-            okeys[ne] = ((uint64_t)g << wr) | (k & ((1ull << wr) - 1ull));
-            oidx[ne] = ridx[j];
+            if (POS) {
+                rpos[j] = pos_in[ne];
+            } else {
+                okeys[ne] = ((uint64_t)g << wr) | (k & ((1ull << wr) - 1ull));
+                oidx[ne] = ridx[j];
+            }
         }
     }
 }

@@ -59,6 +59,9 @@ enum sa_kernel_kind {
 #define SA_ROUND1_LSD 1       /* LSD radix sort of the packed K-symbol key */
 #define SA_ROUND1_BUCKETED 2  /* two bucket passes + per-window LDS sort (falls
                                  back to LSD when a window exceeds the LDS tile) */
+#define SA_ROUND1_PIVOT 3     /* sa_stats.round1 only: the LSD round's keys split
+                                 around the key of suffix 0, half or more of the
+                                 suffixes tied to it (sa_pivot.h) */
 
 /* doubling schedules */
 #define SA_SCHEDULE_PACKED 0     /* default: first round sorts a packed K-symbol
@@ -85,6 +88,8 @@ enum sa_kernel_kind {
                                            queues and regions */
 #define SA_DEBUG_XQ_OVERFLOW 0x100u     /* per-XCD second pass with sub-regions of exactly 1/8 of each digit: a queue
                                            overflows and the round re-runs with the one-region pass */
+#define SA_DEBUG_NO_TIED 0x200u         /* pivot rounds: tied blocks through the sorted output and segments(), not
+                                           written straight to the next unsorted set (sa_pivot.h) */
 
 typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
@@ -115,7 +120,7 @@ typedef struct {
     int32_t init_chars;                  /* K of the packed schedule */
     int32_t sigma;                       /* distinct symbols in the text */
     int32_t sparse_ranks;                /* 1: round-1 ranks kept for unsorted suffixes only */
-    int32_t round1;                      /* SA_ROUND1_LSD or SA_ROUND1_BUCKETED: first round taken */
+    int32_t round1;                      /* SA_ROUND1_LSD, _BUCKETED or _PIVOT: first round taken */
     int32_t largest_window;              /* bucketed round 1: largest window (suffixes) */
     uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
     double kern_ms[SA_K_COUNT];          /* profile only */

@@ -29,7 +29,10 @@ def main():
     from hpc_suffix_array_amd import DeviceBuilder
     b = DeviceBuilder(a.n)
     t = torch.empty(a.n, dtype=torch.uint8, device="cuda")
-    b.generate_text(t, a.n, ALPHABETS[a.kind], seed=1)
+    if a.kind == "degenerate":
+        t.fill_(ord("a"))
+    else:
+        b.generate_text(t, a.n, ALPHABETS[a.kind], seed=1)
     sa = torch.empty(a.n, dtype=torch.int32, device="cuda")
     res = {v: [] for v in a.variants}
     for v in a.variants:   # warm-up

@@ -156,23 +156,27 @@ def test_config2_64mib_dna_known_answer(gpu, oracle, golden, schedule):
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("n", [2, 17, 4096, 65537, 1 << 20, (1 << 22) + 3])
 def test_degenerate(gpu, n, schedule):
-    """configs[4] shape: one repeated symbol, log2 n rounds, analytic SA."""
+    """configs[4] shape: one repeated symbol, log2 n rounds, analytic SA
+    (packed: the tied-block pivot rounds, and the split ones for comparison)."""
     from hpc_suffix_array_amd import build_suffix_array
-    got, st = build_suffix_array(np.full(n, ord("a"), np.uint8), return_stats=True, schedule=schedule)
-    assert (got == np.arange(n - 1, -1, -1, dtype=np.uint32)).all()
-    assert st["distinct"][-1] == n
+    for dbg in ((), ("no_tied",)) if schedule == "packed" else ((),):
+        got, st = build_suffix_array(np.full(n, ord("a"), np.uint8), return_stats=True, schedule=schedule, debug=dbg)
+        assert (got == np.arange(n - 1, -1, -1, dtype=np.uint32)).all(), dbg
+        assert st["distinct"][-1] == n
 
 
-@pytest.mark.parametrize("pivot", [True, False])
-def test_pivot_split_rounds(gpu, oracle, pivot):
+@pytest.mark.parametrize("mode", ["tied", "split", "no_pivot"])
+def test_pivot_split_rounds(gpu, oracle, mode):
     """Unsorted-set rounds with large groups by the three-way pivot split
     (sa_pivot.h): periodic texts with sparse noise (a dominant key per group,
     plus members below and above the pivot), runs of one symbol inside random
     text, and a short first key on random DNA (many distinct keys per group:
-    the split gives up and the full sort runs); debug "no_pivot"
-    (SA_DEBUG_NO_PIVOT) forces the full LSD sort for comparison."""
+    the split gives up and the full sort runs).  "tied" (default): tied blocks
+    straight to the next unsorted set; "split": debug "no_tied"
+    (SA_DEBUG_NO_TIED), tied blocks through the sorted output and segments();
+    "no_pivot" (SA_DEBUG_NO_PIVOT): the full LSD sort."""
     from hpc_suffix_array_amd import build_suffix_array
-    dbg = () if pivot else ("no_pivot",)
+    dbg = {"tied": (), "split": ("no_tied",), "no_pivot": ("no_pivot",)}[mode]
     rng = np.random.default_rng(7)
     cases = []
     for period, noise, n in ((b"ab", 0.002, 400_003), (b"abc", 0.01, 300_001), (b"aab", 0.0005, 1 << 20)):
@@ -183,13 +187,18 @@ def test_pivot_split_rounds(gpu, oracle, pivot):
     t = oracle.gen_text("dna", 500_000, seed=3)
     t[100_000:260_000] = ord("G")
     cases.append(t)
+    # runs of one symbol with random lengths: many groups per round, tied
+    # blocks of one member (sorted at once) and of many
+    lens = rng.integers(1, 600, 3000)
+    t = np.repeat(rng.integers(ord("a"), ord("d"), len(lens), dtype=np.uint8), lens)
+    cases.append(t)
     for t in cases:
         got = build_suffix_array(t, debug=dbg)
-        assert (got == oracle.sa_c(t)).all(), (len(t), pivot)
+        assert (got == oracle.sa_c(t)).all(), (len(t), mode)
     for n in (70_001, 1_000_000):
         t = oracle.gen_text("dna", n, seed=n)
         got = build_suffix_array(t, init_chars=2, debug=dbg)
-        assert (got == oracle.sa_c(t)).all(), (n, pivot)
+        assert (got == oracle.sa_c(t)).all(), (n, mode)
 
 
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
@@ -611,10 +620,35 @@ def test_bucketed_round1_fallback(gpu, oracle):
               np.tile(np.frombuffer(b"abaababa", np.uint8), n // 8),
               np.concatenate([oracle.gen_text("dna", n // 2, seed=3), np.full(n // 2, ord("C"), np.uint8)])):
         got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
-        assert st["round1"] == "lsd"
+        # one symbol: all but the last K suffixes share suffix 0's key -> the
+        # LSD round's pivot split (pivot_round1)
+        assert st["round1"] == ("pivot" if len(np.unique(t)) == 1 else "lsd"), st["round1"]
         if len(np.unique(t)) > 1:   # one symbol: no bucketing at all (sigma < 2)
             assert st["largest_window"] > 18432, st["largest_window"]
         assert (got == oracle.sa_c(t)).all()
+
+
+def test_pivot_round1(gpu, oracle):
+    """The LSD round 1 split around suffix 0's key (pivot_round1, sa_pivot.h
+    R1) when half or more of the suffixes share it: a long run of one symbol
+    before random text, one symbol with sparse noise (the rest above the
+    pivot, the text's last suffixes below it), ragged sizes; a text whose
+    suffix 0 key is rare keeps the LSD sort.  Same SA as the oracle and as the full LSD sort (debug no_pivot)."""
+    from hpc_suffix_array_amd import build_suffix_array
+    rng = np.random.default_rng(5)
+    cases = [(np.concatenate([np.full(700_001, ord("a"), np.uint8), oracle.gen_text("dna", 300_000, seed=1)]),
+              "pivot"),
+             (np.where(rng.random(600_000) < 0.001, ord("b"), ord("a")).astype(np.uint8), "pivot"),
+             (np.concatenate([np.full(65_600, ord("z"), np.uint8), rng.integers(97, 100, 999, dtype=np.uint8)]),
+              "pivot"),
+             (np.concatenate([oracle.gen_text("dna", 300_000, seed=2), np.full(700_000, ord("a"), np.uint8)]),
+              "lsd")]
+    for t, want in cases:
+        got, st = build_suffix_array(t, return_stats=True, round1="lsd")
+        assert st["round1"] == want, (len(t), st["round1"])
+        assert (got == oracle.sa_c(t)).all(), len(t)
+        ref = build_suffix_array(t, round1="lsd", debug=("no_pivot",))
+        assert (got == ref).all()
 
 
 def test_bucketed_round1_known_answers(gpu, oracle, golden):
