@@ -1047,7 +1047,9 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     uint32_t* const cc = c->hist;                     // 3 x chunks class counts, scanned in place
     const uint32_t Gu = (uint32_t)G;
     tm.begin(SA_K_SORT_U);
-    hipLaunchKernelGGL(k_pivot_keys, dim3((uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192)), dim3(kBlock),
+    hipLaunchKernelGGL(k_pivot_keys,
+                       dim3((uint32_t)std::min<uint64_t>((m + kBlock * kPkItems - 1) / (kBlock * kPkItems), 8192)),
+                       dim3(kBlock),
                        0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m, (const uint32_t*)c->rank,
                        n, h, wr, Gu, ukb1, gs, pr);
     hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,

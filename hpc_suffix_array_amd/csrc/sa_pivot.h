@@ -39,29 +39,52 @@
 // two or more at the front of that set (block ids 0..Gt-1 in group order,
 // offsets from k_pivot_tied_scan); only the sorted rest goes through
 // segments(), appended after them with group ids from Gt.  Per tied member
-// 36 bytes (keys, u_g, u_idx read; rank and three set words written) instead
-// of the 84 of pass<2> + k_seg_count + k_seg_write.
+// 28 bytes (key and u_idx read; rank and three set words written) instead
+// of the 80 of pass<2> + k_seg_count + k_seg_write.  (The passes take a
+// member's group from its key, g = key >> wr, not from u_g.)
 #pragma once
+#include <type_traits>
+
 #include "sa_kernels.h"
 
 namespace sa {
 
-// keys of a pivot round (dense ranks only) and the group starts
+// keys of a pivot round (dense ranks only) and the group starts; kPkItems
+// members per thread, all loads of a batch issued before the rank gathers
+// that depend on them
+constexpr int kPkItems = 4;
 __global__ __launch_bounds__(kBlock) void k_pivot_keys(const uint32_t* __restrict__ u_idx,
                                                        const uint32_t* __restrict__ u_g, uint64_t m,
                                                        const uint32_t* __restrict__ rank, uint64_t n, uint64_t h,
                                                        uint32_t wr, uint32_t G, uint64_t* __restrict__ keys,
                                                        uint32_t* __restrict__ gs, uint32_t* __restrict__ pr) {
-    for (uint64_t e = (uint64_t)blockIdx.x * kBlock + threadIdx.x; e < m; e += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t x = u_idx[e];
-        const uint32_t g = u_g[e];
-        const uint32_t r1 = x + h < n ? rank[x + h] : 0u;
-        keys[e] = ((uint64_t)g << wr) | r1;
-        if (e == 0 || u_g[e - 1] != g) {
-            gs[g] = (uint32_t)e;
-            pr[g] = r1;
+    const uint64_t step = (uint64_t)gridDim.x * kBlock * kPkItems;
+    for (uint64_t base = (uint64_t)blockIdx.x * kBlock * kPkItems; base < m; base += step) {
+        uint32_t x[kPkItems], g[kPkItems], gp[kPkItems], r1[kPkItems];
+#pragma unroll
+        for (int i = 0; i < kPkItems; ++i) {
+            const uint64_t e = base + (uint64_t)i * kBlock + threadIdx.x;
+            x[i] = e < m ? u_idx[e] : 0u;
+            g[i] = e < m ? u_g[e] : 0u;
+            gp[i] = (e < m && e > 0) ? u_g[e - 1] : ~0u;
         }
-        if (e == m - 1) gs[G] = (uint32_t)m;
+#pragma unroll
+        for (int i = 0; i < kPkItems; ++i) {
+            const uint64_t e = base + (uint64_t)i * kBlock + threadIdx.x;
+            r1[i] = (e < m && x[i] + h < n) ? rank[x[i] + h] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < kPkItems; ++i) {
+            const uint64_t e = base + (uint64_t)i * kBlock + threadIdx.x;
+            if (e < m) {
+                keys[e] = ((uint64_t)g[i] << wr) | r1[i];
+                if (gp[i] != g[i]) {   // e == 0 or a group start
+                    gs[g[i]] = (uint32_t)e;
+                    pr[g[i]] = r1[i];
+                }
+                if (e == m - 1) gs[G] = (uint32_t)m;
+            }
+        }
     }
 }
 
@@ -107,26 +130,69 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
         for (int k = 0; k < 3; ++k) run[k] = cc[(uint64_t)k * ch.chunks + c];
     const uint64_t gstride = (uint64_t)G + 1;
     const uint64_t p1 = R1 ? keys[0] : 0ull;
+    // the per-group words of the lane's current group, reloaded only when its
+    // group changes (U is in group order: a lane's groups only increase).  A
+    // wave whose 1024 members lie in one group (first == last) loads them once,
+    // outside the row loops, so its rows hold no load that a store must wait
+    // for; other waves refresh them per member.
+    uint32_t cg = ~0u, c_pr = 0, c_s0 = 0, c_cnt0 = 0, c_b1 = 0, c_cnt1 = 0, c_bp = 0, c_toff = 0, c_tid = 0;
+    auto group = [&](uint32_t gg) {
+        if (gg == cg) return;
+        cg = gg;
+        c_pr = R1 ? 0u : pr[gg];
+        c_s0 = R1 ? 0u : gs[gg];
+        if (MODE != 0) {
+            c_cnt0 = gP[gg + 1] - gP[gg];
+            c_b1 = gP[gstride + gg];
+            c_cnt1 = gP[gstride + gg + 1] - c_b1;
+        }
+        if (MODE == 3) {
+            c_bp = (R1 ? 0u : to.pos_in[c_s0]) + c_cnt0;   // the tied block's first SA position
+            c_toff = to.toff[gg];
+            c_tid = to.tid[gg];
+        }
+    };
+    if (R1) group(0u);
     for (uint64_t tb = e0; tb < e1; tb += kTile) {
         const uint64_t w0 = tb + (uint64_t)wave * kWaveTile;
         uint64_t key[kItems];
-        uint32_t g[kItems];
+        uint32_t g[kItems], xs[kItems];
+        // every row's key and index loaded before any store (vmcnt counts
+        // loads and stores in order: a load issued between stores would make
+        // its row wait for them)
 #pragma unroll
         for (int j = 0; j < kItems; ++j) {
             const uint64_t e = w0 + (uint64_t)j * kWave + lane;
             key[j] = e < e1 ? keys[e] : 0ull;
-            g[j] = (e < e1 && !R1) ? u_g[e] : 0u;
+            xs[j] = (MODE != 0 && !R1 && e < e1) ? u_idx[e] : (uint32_t)e;
+            g[j] = (e < e1 && !R1) ? (uint32_t)(key[j] >> wr) : 0u;   // key = g << wr | rank
+        }
+        bool uni = true;
+        if (!R1) {
+            const uint32_t g0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)g[0]);
+            uint64_t diff = 0;
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) diff |= __ballot(w0 + (uint64_t)j * kWave + lane < e1 && g[j] != g0);
+            uni = diff == 0;
+            if (uni) group(g0);
         }
         uint32_t cls[kItems];
         uint32_t wc[3] = {0, 0, 0};
+        auto classify = [&](auto uni_tag) {
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) {
-            const uint64_t e = w0 + (uint64_t)j * kWave + lane;
-            const uint64_t p = R1 ? p1 : e < e1 ? (((uint64_t)g[j] << wr) | pr[g[j]]) : 0ull;
-            cls[j] = e < e1 ? (key[j] < p ? 0u : key[j] == p ? 1u : 2u) : 3u;
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                if (!decltype(uni_tag)::value && e < e1) group(g[j]);
+                const uint64_t p = R1 ? p1 : e < e1 ? (((uint64_t)g[j] << wr) | c_pr) : 0ull;
+                cls[j] = e < e1 ? (key[j] < p ? 0u : key[j] == p ? 1u : 2u) : 3u;
 #pragma unroll
-            for (int k = 0; k < 3; ++k) wc[k] += (uint32_t)__popcll(__ballot(cls[j] == (uint32_t)k));
-        }
+                for (int k = 0; k < 3; ++k) wc[k] += (uint32_t)__popcll(__ballot(cls[j] == (uint32_t)k));
+            }
+        };
+        if (uni)
+            classify(std::true_type{});
+        else
+            classify(std::false_type{});
         if (lane == 0)
             for (int k = 0; k < 3; ++k) s_w[k][wave] = wc[k];
         __syncthreads();
@@ -140,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                 tot[k] += v;
             }
         }
-        {
+        auto scatter = [&](auto uni_tag) {
 #pragma unroll
             for (int j = 0; j < kItems; ++j) {
                 const uint64_t e = w0 + (uint64_t)j * kWave + lane;
@@ -153,33 +219,28 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                     const uint32_t P1 = off[1] + (uint32_t)__popcll(bm[1] & lt);
                     const uint32_t P2 = off[2] + (uint32_t)__popcll(bm[2] & lt);
                     const uint32_t gg = g[j];
-                    const uint32_t s0 = R1 ? 0u : gs[gg];
+                    if (!decltype(uni_tag)::value) group(gg);
                     if (MODE == 0) {
-                        if (s0 == (uint32_t)e) {   // in-chunk counts before the group start
+                        if (c_s0 == (uint32_t)e) {   // in-chunk counts before the group start
                             gP[gg] = P0;
                             gP[gstride + gg] = P1;
                             gP[2 * gstride + gg] = P2;
                         }
                     } else {
-                        const uint32_t x = R1 ? (uint32_t)e : u_idx[e];
+                        const uint32_t x = xs[j];
                         if (MODE == 3 && cls[j] == 1u) {
-                            const uint32_t cnt0 = gP[gg + 1] - gP[gg];
-                            const uint32_t b1 = gP[gstride + gg];
-                            const uint32_t cnt1 = gP[gstride + gg + 1] - b1;
-                            const uint32_t t = P1 - b1;
-                            const uint32_t bp = (R1 ? 0u : to.pos_in[s0]) + cnt0;   // the block's first SA position
-                            to.rank[x] = bp + 1u;
-                            if (cnt1 == 1u) {
-                                to.sa[bp] = x;
+                            const uint32_t t = P1 - c_b1;
+                            to.rank[x] = c_bp + 1u;
+                            if (c_cnt1 == 1u) {
+                                to.sa[c_bp] = x;
                             } else {
-                                const uint32_t q = to.toff[gg] + t;
-                                to.u_pos[q] = bp + t;
+                                const uint32_t q = c_toff + t;
+                                to.u_pos[q] = c_bp + t;
                                 to.u_idx[q] = x;
-                                to.u_g[q] = to.tid[gg];
+                                to.u_g[q] = c_tid;
                             }
                         } else if (cls[j] == 1u) {
-                            const uint32_t cnt0 = gP[gg + 1] - gP[gg];
-                            const uint64_t ne = (uint64_t)s0 + cnt0 + (P1 - gP[gstride + gg]);
+                            const uint64_t ne = (uint64_t)c_s0 + c_cnt0 + (P1 - c_b1);
                             okeys[ne] = key[j];
                             oidx[ne] = x;
                         } else {
@@ -194,7 +255,11 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
 #pragma unroll
                 for (int k = 0; k < 3; ++k) off[k] += (uint32_t)__popcll(bm[k]);
             }
-        }
+        };
+        if (uni)
+            scatter(std::true_type{});
+        else
+            scatter(std::false_type{});
         for (int k = 0; k < 3; ++k) run[k] += tot[k];
         __syncthreads();
     }
