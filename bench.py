@@ -67,6 +67,9 @@ KERNEL_NAMES = {
     "pack": "k_bucket_hist (first-pass digit totals) | k_pack_text (LSD first round keys)",
     "seg_count": "k_seg_count", "seg_write": "k_seg_write | k_wscan_* + k_u_gather",
     "sort_u": "unsorted-set sorts (k_materialize + k_onesweep<SrcKeys>)",
+    "pivot_keys": "k_pivot_keys (pivot round keys g << wr | rank[i + h], group starts)",
+    "pivot_count": "k_pivot_pass<0> + k_scan_rows (pivot round class counts)",
+    "pivot_write": "k_pivot_pass<3> (pivot round: tied blocks to the next unsorted set, the rest compacted)",
 }
 
 

@@ -20,7 +20,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 SA_MAX_ROUNDS = 64
 KERNEL_KINDS = ["init", "hist_first", "hist_keys", "scan", "scatter_first", "scatter_keys",
                 "heads", "heads_scan", "rerank", "seg_count", "seg_scan", "seg_write", "alphabet", "pack",
-                "sort_u", "windows", "local_sort"]
+                "sort_u", "windows", "local_sort", "pivot_keys", "pivot_count", "pivot_write"]
 SCHEDULE_PACKED = 0
 SCHEDULE_REFERENCE = 1
 ROUND1_AUTO = 0

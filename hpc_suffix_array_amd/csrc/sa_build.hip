@@ -1046,19 +1046,22 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     uint32_t* const gP = c->vals_alt;                 // 3 (G + 1): members of each class before each group
     uint32_t* const cc = c->hist;                     // 3 x chunks class counts, scanned in place
     const uint32_t Gu = (uint32_t)G;
-    tm.begin(SA_K_SORT_U);
+    tm.begin(SA_K_PIVOT_KEYS);
     hipLaunchKernelGGL(k_pivot_keys,
                        dim3((uint32_t)std::min<uint64_t>((m + kBlock * kPkItems - 1) / (kBlock * kPkItems), 8192)),
                        dim3(kBlock),
                        0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m, (const uint32_t*)c->rank,
                        n, h, wr, Gu, ukb1, gs, pr);
+    tm.end();
+    add_bytes(st, SA_K_PIVOT_KEYS, 20 * m);
+    tm.begin(SA_K_PIVOT_COUNT);
     hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
                        (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
                        (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
     hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_SORT_U, 28 * m);
+    add_bytes(st, SA_K_PIVOT_COUNT, 8 * m);
     SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
@@ -1068,7 +1071,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     SA_TRACE("  round h=%llu: pivot split, tied %llu of %llu%s", (unsigned long long)h, (unsigned long long)t1,
              (unsigned long long)m, tied ? " (tied blocks to the next set)" : "");
     if (t1 * 2 < m) return SA_OK;   // mostly distinct keys: the full sort is cheaper
-    tm.begin(SA_K_SORT_U);
+    tm.begin(SA_K_PIVOT_WRITE);
     hipLaunchKernelGGL(k_pivot_gp, dim3((uint32_t)std::min<uint64_t>((G + kBlock) / kBlock, 8192)), dim3(kBlock), 0, s,
                        (const uint32_t*)gs, Gu, (const uint32_t*)cc, cu, (const uint32_t*)c->totals, gP);
     const uint64_t mr = t0 + t2;
@@ -1091,7 +1094,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     }
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_SORT_U, tied ? 16 * m + 16 * t1 + 12 * mr : 36 * m);
+    add_bytes(st, SA_K_PIVOT_WRITE, tied ? 12 * m + 16 * t1 + 12 * mr : 12 * m + 12 * m);
     if (tied) {
         SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
         SA_HIP(hipStreamSynchronize(s));
@@ -1169,13 +1172,13 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     c->host_words[24] = 0;
     c->host_words[25] = (uint32_t)n;
     SA_HIP(hipMemcpyAsync(gs, c->host_words + 24, 8, hipMemcpyHostToDevice, s));
-    tm.begin(SA_K_SORT_U);
+    tm.begin(SA_K_PIVOT_COUNT);
     hipLaunchKernelGGL((k_pivot_pass<0, true>), dim3(ch.chunks), dim3(kBlock), 0, s, keys, nullptr, nullptr, ch,
                        (const uint32_t*)gs, nullptr, 1u, 0u, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
     hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, ch.chunks, c->totals);
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_SORT_U, 8 * n);
+    add_bytes(st, SA_K_PIVOT_COUNT, 8 * n);
     SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
@@ -1189,7 +1192,7 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     // next set goes to u_*[0]), key buffers keys_u / keys[0]
     uint64_t* const rk = c->keys[0];
     uint32_t* const ridx = c->u_idx[1];
-    tm.begin(SA_K_SORT_U);
+    tm.begin(SA_K_PIVOT_WRITE);
     hipLaunchKernelGGL(k_pivot_gp, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gs, 1u, (const uint32_t*)cc, ch,
                        (const uint32_t*)c->totals, gP);
     hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, 1u, toff, tid,
@@ -1199,7 +1202,7 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
                        (const uint32_t*)gs, nullptr, 1u, 0u, cc, gP, nullptr, nullptr, rk, ridx, to);
     tm.end();
     SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_SORT_U, 8 * n + 16 * t1 + 12 * mr);
+    add_bytes(st, SA_K_PIVOT_WRITE, 8 * n + 16 * t1 + 12 * mr);
     SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     const uint64_t T = c->host_words[20], Gt = c->host_words[21], Dt = c->host_words[22];

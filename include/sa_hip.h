@@ -51,7 +51,10 @@ enum sa_kernel_kind {
     SA_K_SORT_U = 14,        /* every pass of an unsorted-set (later round) sort */
     SA_K_WINDOWS = 15,       /* bucketed round 1: window starts over the bucket-sorted keys */
     SA_K_LOCAL_SORT = 16,    /* bucketed round 1: per-window LDS sort */
-    SA_K_COUNT = 17
+    SA_K_PIVOT_KEYS = 17,    /* pivot round: keys (g, rank[i + h]) and group starts */
+    SA_K_PIVOT_COUNT = 18,   /* pivot round: class counts (< = > pivot) per chunk, scanned */
+    SA_K_PIVOT_WRITE = 19,   /* pivot round: tied blocks out, the rest compacted */
+    SA_K_COUNT = 20
 };
 
 /* first round of the packed schedule */

@@ -62,7 +62,7 @@ def test_stats_struct_matches_header(sa_lib):
     L.sa_struct_size.restype = ctypes.c_uint64
     assert ctypes.sizeof(sa_lib.SaStats) == L.sa_struct_size(0)
     assert ctypes.sizeof(sa_lib.SaOpts) == L.sa_struct_size(1)
-    assert len(sa_lib.KERNEL_KINDS) == sa_lib.SA_K_COUNT == 17
+    assert len(sa_lib.KERNEL_KINDS) == sa_lib.SA_K_COUNT == 20
 
 
 def test_create_has_strncpy_semantics(sa_lib):
