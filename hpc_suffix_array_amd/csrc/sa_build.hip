@@ -767,6 +767,10 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
     return SA_OK;
 }
 
+// round 1's first-digit counts taken by the init kernel (A/B switch)
+#ifndef SA_INIT_HIST
+#define SA_INIT_HIST 1
+#endif
 static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                            sa_stats* st, Timer& tm) {
     Events ev;
@@ -791,22 +795,39 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
+    uint64_t D = sigma;   // ranks 1..sigma (manber_myers.c:94 sizes its bins for 256)
+    const uint64_t perm_min = perm_min_n(c);
+    const uint32_t ib = std::max<uint32_t>(1, bit_width(n - 1));   // index bits of a packed item
+    bool used_perm = false;
+    bool hist_ready = false;   // this round's first-digit counts came with the previous re-rank (or the init)
     tm.begin(SA_K_INIT);
     {
-        const uint64_t grid = std::min<uint64_t>((n + kBlock * 4 - 1) / (kBlock * 4), 4096);
-        hipLaunchKernelGGL(k_init_rank_dense, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n,
-                           (const uint16_t*)c->code, c->rank);
+        // round 1's first-digit counts per XCD queue with the ranks (k_init_rank_hist)
+        const uint32_t w1 = bit_width(D);
+        const bool packed1 = c->radix == 0 && 2 * w1 + ib <= 64;
+        const LsdPlan pl1 = lsd_plan(2 * w1, packed1 ? ib : 0, lsd_max_bits(c));
+        if (SA_INIT_HIST && c->radix == 0 && lsd_xq_ok(c, n, pl1, packed1)) {
+            uint32_t tpq;
+            uint64_t qspan;
+            QDiv qd;
+            lsd_xq_span(n, &tpq, &qspan, &qd);
+            SA_HIP(hipMemsetAsync(c->lsdx, 0, 8 * kLsdMaxRadix * 4, s));
+            const uint64_t grid = std::min<uint64_t>((n + kBlock * 16 - 1) / (kBlock * 16), 4ull * (uint64_t)c->cus);
+            hipLaunchKernelGGL(k_init_rank_hist, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, c->rank, w1, pl1.shift[0] - (packed1 ? ib : 0u),
+                               (1u << pl1.bits[0]) - 1u, qd, c->lsdx);
+            hist_ready = true;
+        } else {
+            const uint64_t grid = std::min<uint64_t>((n + kBlock * 4 - 1) / (kBlock * 4), 4096);
+            hipLaunchKernelGGL(k_init_rank_dense, dim3((uint32_t)grid), dim3(kBlock), 0, s, d_text, n,
+                               (const uint16_t*)c->code, c->rank);
+        }
     }
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_INIT, 5 * n);
     if (st) st->sigma = (int32_t)sigma;
 
-    uint64_t D = sigma;   // ranks 1..sigma (manber_myers.c:94 sizes its bins for 256)
-    const uint64_t perm_min = perm_min_n(c);
-    const uint32_t ib = std::max<uint32_t>(1, bit_width(n - 1));   // index bits of a packed item
-    bool used_perm = false;
-    bool hist_ready = false;   // this round's first-digit counts came with the previous re-rank
     for (uint64_t h = 1;; h *= 2) {
         SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t w = bit_width(D);          // ranks are 0..D

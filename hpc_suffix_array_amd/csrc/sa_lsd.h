@@ -28,6 +28,9 @@ namespace sa {
 #ifndef SA_LSD_LOOK
 #define SA_LSD_LOOK 4   // predecessor states read per look-back step (8: 1.02x, 16: 1.3x the pass time)
 #endif
+#ifndef SA_HIST_PREFETCH
+#define SA_HIST_PREFETCH 1   // k_lsd_hist issues the next step's loads before counting this one's
+#endif
 #ifndef SA_LSD_PROF
 #define SA_LSD_PROF 0       // per-phase clock64 spans of k_lsd printed per pass (diagnostic builds)
 #endif
@@ -141,15 +144,27 @@ __global__ __launch_bounds__(kBlock) void k_lsd_hist(Src src, uint64_t n, LsdPla
     __syncthreads();
     const uint32_t lane = lane_id();
     const uint64_t above = lane == 63 ? 0ull : (~0ull << (lane + 1));
-    // 8 keys per lane per step, all loads issued before the counting
+    // 8 keys per lane per step, all loads issued before the counting, and
+    // the next step's issued before this one's are counted
     constexpr int U = 8;
     const uint64_t step = (uint64_t)gridDim.x * kBlock * U;
-    for (uint64_t b = (uint64_t)blockIdx.x * kBlock * U; b < n; b += step) {
-        uint64_t k[U];
+    uint64_t kn[U];
+    auto load = [&](uint64_t b2, uint64_t (&kk)[U]) {
 #pragma unroll
         for (int j = 0; j < U; ++j) {
-            const uint64_t e = b + (uint64_t)j * kBlock + threadIdx.x;
-            k[j] = src.key(e < n ? e : n - 1);
+            const uint64_t e = b2 + (uint64_t)j * kBlock + threadIdx.x;
+            kk[j] = src.key(e < n ? e : n - 1);
+        }
+    };
+    if (SA_HIST_PREFETCH && (uint64_t)blockIdx.x * kBlock * U < n) load((uint64_t)blockIdx.x * kBlock * U, kn);
+    for (uint64_t b = (uint64_t)blockIdx.x * kBlock * U; b < n; b += step) {
+        uint64_t k[U];
+        if constexpr (SA_HIST_PREFETCH) {
+#pragma unroll
+            for (int j = 0; j < U; ++j) k[j] = kn[j];
+            load(b + step < n ? b + step : b, kn);
+        } else {
+            load(b, k);
         }
 #pragma unroll
         for (int j = 0; j < U; ++j) {
@@ -416,6 +431,56 @@ __global__ __launch_bounds__((lsd_block<PACKED, RBITS, XQ>()), 4) void k_lsd(Src
                 if (s_nh[i]) atomicAdd(&next_hist[i], s_nh[i]);
         }
     }
+}
+
+// The reference schedule's first ranks (as k_init_rank_dense: rank[i] =
+// dense code of text[i], manber_myers.c:88-92) with round 1's first-digit
+// counts per XCD queue of its LSD passes: item i's key is rank[i] << w |
+// rank[i + 1] (0 past the end, SrcRankPk), its digit (key >> dshift) & dmask,
+// its queue qd.q(i) -- so round 1 reads no histogram pass (k_lsd_hist over
+// n rank pairs).  A workgroup's 1024 positions per step lie in one queue but
+// for the step that crosses a queue border; counts flushed per workgroup.
+__global__ __launch_bounds__(kBlock) void k_init_rank_hist(const uint8_t* __restrict__ text, uint64_t n,
+                                                           const uint16_t* __restrict__ code,
+                                                           uint32_t* __restrict__ rank, uint32_t w, uint32_t dshift,
+                                                           uint32_t dmask, QDiv qd, uint32_t* __restrict__ qh) {
+    constexpr int RUN = 16;   // positions per thread and step: one 16-byte text load
+    __shared__ uint16_t s_code[256];
+    __shared__ uint32_t s_h[8 * kLsdMaxRadix];
+    s_code[threadIdx.x] = code[threadIdx.x];
+    for (uint32_t i = threadIdx.x; i < 8 * kLsdMaxRadix; i += kBlock) s_h[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock * RUN;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * RUN; i < n; i += stride) {
+        uint32_t r[RUN + 1];
+        if (i + RUN + 1 <= n && (((uintptr_t)(text + i)) & 15) == 0) {
+            const uint4 v = *reinterpret_cast<const uint4*>(text + i);
+            const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+                for (int y = 0; y < 4; ++y) r[4 * q + y] = s_code[(wv[q] >> (8 * y)) & 0xFFu];
+            r[RUN] = s_code[text[i + RUN]];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                *reinterpret_cast<uint4*>(rank + i + 4 * q) = make_uint4(r[4 * q], r[4 * q + 1], r[4 * q + 2], r[4 * q + 3]);
+        } else {
+#pragma unroll
+            for (int j = 0; j <= RUN; ++j) r[j] = i + j < n ? (uint32_t)s_code[text[i + j]] : 0u;
+            for (uint64_t j = i; j < n && j < i + RUN; ++j) rank[j] = r[j - i];
+        }
+        // one queue for the thread's 16 positions unless they cross a border
+        const uint32_t q0 = qd.q(i), q1 = qd.q(i + RUN - 1);
+#pragma unroll
+        for (int j = 0; j < RUN; ++j)
+            if (i + j < n) {
+                const uint32_t q = q0 == q1 ? q0 : qd.q(i + j);
+                atomicAdd(&s_h[q * kLsdMaxRadix + ((((r[j] << w) | r[j + 1]) >> dshift) & dmask)], 1u);
+            }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < 8 * kLsdMaxRadix; i += kBlock)
+        if (s_h[i]) atomicAdd(&qh[i], s_h[i]);
 }
 
 // SA from the sorted items of a PACKED final round
