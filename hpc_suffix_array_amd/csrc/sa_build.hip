@@ -88,6 +88,7 @@ static_assert(kMaxChunks >= 1 && kMaxChunks <= (1u << 20), "chunk scratch sized 
 // sparse round-1 ranks when at most n / kSparseDiv suffixes stay unsorted
 constexpr uint64_t kSparseDiv = 8;
 constexpr int kEvPool = 256;
+constexpr int kRoundEv = SA_MAX_ROUNDS + 1;   // round boundary events (Timer::round_mark)
 
 static uint64_t align_up(uint64_t x, uint64_t a) { return (x + a - 1) / a * a; }
 
@@ -145,7 +146,7 @@ struct sa_context {
     uint16_t* code = nullptr;      // 256 byte -> dense code 1..sigma
     uint32_t* host_words = nullptr;  // pinned (4096 words): 64 words, 256 counts, 128 words of codes at 320, the text tail (64 B) at 2048,
                                      // per-rank counts of the range-partitioned build at 1024
-    hipEvent_t ev[sa::kEvPool];
+    hipEvent_t ev[sa::kEvPool + sa::kRoundEv];   // Timer pairs, then the round boundaries
     int ev_ready = 0;
     sa::DistState* dist = nullptr;   // range-partitioned build state (sa_dist.h)
     // sa_opts debug / tune fields of the current build (sa_build_device's
@@ -288,6 +289,24 @@ struct Timer {
         if (!on) return;
         hipEventRecord(c->ev[2 * used + 1], s);
         ++used;
+    }
+    // round boundaries: one event before the first round and one after each,
+    // read when the build has finished (round_times), so no round waits for
+    // the GPU to drain before the next one is launched
+    int nr = 0;
+    void round_mark() {
+        if (nr < kRoundEv) hipEventRecord(c->ev[kEvPool + nr], s);
+        ++nr;
+    }
+    void round_times() {
+        const int last = std::min(nr, kRoundEv) - 1;
+        if (!st || last < 1) return;
+        hipEventSynchronize(c->ev[kEvPool + last]);
+        for (int r = 0; r < last && r < st->rounds; ++r) {
+            float ms = 0.f;
+            hipEventElapsedTime(&ms, c->ev[kEvPool + r], c->ev[kEvPool + r + 1]);
+            st->round_ms[r] = ms;
+        }
     }
     void flush() {
         if (!on || used == 0) return;
@@ -773,9 +792,7 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
 #endif
 static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                            sa_stats* st, Timer& tm) {
-    Events ev;
-    int rc = ev.make();
-    if (rc) return rc;
+    int rc = SA_OK;
     const Chunking ch = plan_chunks(n);
     // first ranks: dense codes 1..sigma of the bytes present (the order of
     // manber_myers.c:90's text[i] + 1, so D_j and the round count are the
@@ -828,8 +845,8 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     add_bytes(st, SA_K_INIT, 5 * n);
     if (st) st->sigma = (int32_t)sigma;
 
+    tm.round_mark();
     for (uint64_t h = 1;; h *= 2) {
-        SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t w = bit_width(D);          // ranks are 0..D
         // (key << ib | index) items while they fit 64 bits (onesweep only)
         const bool packed = c->radix == 0 && 2 * w + ib <= 64;
@@ -917,10 +934,8 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                 add_bytes(st, SA_K_RERANK, 16 * n);
             }
         }
-        SA_HIP(hipEventRecord(ev.e[1], s));
-        SA_HIP(hipEventSynchronize(ev.e[1]));
-        tm.flush();
-        record_round(st, elapsed(ev.e[0], ev.e[1]), Dn, P, n, 2 * h);
+        tm.round_mark();
+        record_round(st, 0.f, Dn, P, n, 2 * h);   // (its time: Timer::round_times)
         if (Dn > n || Dn == 0)
             return set_err(SA_E_INTERNAL, "distinct count %llu out of range", (unsigned long long)Dn);
         if (done) break;
@@ -1254,12 +1269,10 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
 
 static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32_t* d_sa, hipStream_t s,
                         const sa_opts* opts, sa_stats* st, Timer& tm) {
-    Events ev;
-    int rc = ev.make();
-    if (rc) return rc;
+    int rc = SA_OK;
     rc = ensure_u_capacity(c, n);
     if (rc) return rc;
-    SA_HIP(hipEventRecord(ev.e[0], s));
+    tm.round_mark();
     // alphabet -> dense codes (host reads the 256-bit presence mask)
     uint32_t* h_alpha = c->host_words + 64;
     uint16_t* h_code = reinterpret_cast<uint16_t*>(c->host_words + 320);
@@ -1361,10 +1374,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K,
                         bucketed ? 1u : 0u, bp.bs, bucketed ? c->segw + kBstartOff : nullptr, d_sa, ksh1};
     if (st) st->sparse_ranks = sparse ? 1 : 0;
-    SA_HIP(hipEventRecord(ev.e[1], s));
-    SA_HIP(hipEventSynchronize(ev.e[1]));
-    tm.flush();
-    record_round(st, elapsed(ev.e[0], ev.e[1]), D, P, n, K);
+    tm.round_mark();
+    record_round(st, 0.f, D, P, n, K);
     SA_TRACE("  round 1: D=%llu unsorted=%llu groups=%llu", (unsigned long long)D, (unsigned long long)m,
              (unsigned long long)G);
 
@@ -1372,7 +1383,6 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const uint32_t wr = bit_width(n);   // rank values 0..n
     for (uint64_t h = K; m > 0; h *= 2) {
         if (h >= 2 * n) return set_err(SA_E_INTERNAL, "doubling did not converge (h=%llu)", (unsigned long long)h);
-        SA_HIP(hipEventRecord(ev.e[0], s));
         const uint32_t wg = G > 1 ? bit_width(G - 1) : 0;
         const uint32_t bits = wg + wr;
         if (bits > 64) return set_err(SA_E_INTERNAL, "key of %u bits", bits);
@@ -1464,11 +1474,9 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
                           &m2, &G2);
             if (rc) return rc;
         }
-        SA_HIP(hipEventRecord(ev.e[1], s));
-        SA_HIP(hipEventSynchronize(ev.e[1]));
-        tm.flush();
+        tm.round_mark();
         D = (n - m) + Du;
-        record_round(st, elapsed(ev.e[0], ev.e[1]), D, P, m, 2 * h);
+        record_round(st, 0.f, D, P, m, 2 * h);
         SA_TRACE("  round h=%llu: sorted %llu, D=%llu unsorted=%llu groups=%llu", (unsigned long long)h,
                  (unsigned long long)m, (unsigned long long)D, (unsigned long long)m2, (unsigned long long)G2);
         m = m2;
@@ -1517,6 +1525,7 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     SA_HIP(hipEventRecord(ev.e[1], s));
     SA_HIP(hipEventSynchronize(ev.e[1]));
     tm.flush();
+    tm.round_times();
     if (st) st->total_ms = elapsed(ev.e[0], ev.e[1]);
     return SA_OK;
 }
@@ -1844,7 +1853,7 @@ int sa_context_create(int device, uint64_t max_n, sa_context** out) {
         sa_context_destroy(c);
         return set_err(SA_E_NOMEM, "context allocation failed");
     }
-    for (int i = 0; i < kEvPool; ++i) {
+    for (int i = 0; i < kEvPool + kRoundEv; ++i) {
         if (hipEventCreate(&c->ev[i]) != hipSuccess) {
             sa_context_destroy(c);
             return set_err(SA_E_HIP, "hipEventCreate failed");

@@ -688,33 +688,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     add_bytes(st, SA_K_LOCAL_SORT, 12 * m + (m >> kKeySample) * 8);
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
-    if (c->host_words[6]) {
-        SA_TRACE("  bucketed round 1: local sort flags %u, full sort instead", c->host_words[6]);
-        return SA_OK;
-    }
-    seg[0] = c->host_words[0];
-    seg[1] = c->host_words[1];
-    seg[2] = c->host_words[2];
-    add_bytes(st, SA_K_LOCAL_SORT, seg[1] * 28);   // unsorted set: rank, member bit, 3 tmp words
-    if (!br_.always_u && seg[1] > n / kSparseDiv) {
-        // dense ranks follow (segments() over every key1): the same sort
-        // again, writing every key1 and nothing of the unsorted set
-        SegOut full{};
-        full.ksh = 0;
-        SA_HIP(hipMemsetAsync(c->words + 10, 0, 4, s));   // the skewed-window list is rebuilt
-        tm.begin(SA_K_LOCAL_SORT);
-        local_sort(full);
-        tm.end();
-        add_bytes(st, SA_K_LOCAL_SORT, 20 * m);
-        SA_HIP(hipGetLastError());
-    } else {
-        *ksh = kKeySample;
-    }
-    if (br_.always_u || seg[1] <= n / kSparseDiv) {
-        // the unsorted set, in SA order
-        tm.begin(SA_K_SEG_WRITE);
+    // the unsorted set, in SA order, compacted before the counts are read
+    // back (its launches overlap that round trip; a round that turns out
+    // dense, or falls back, ignores it: segments() writes the set again)
+    tm.begin(SA_K_SEG_WRITE);
+    {
         const uint32_t wb = (uint32_t)((nw + 1 + kWsBlock - 1) / kWsBlock);
         uint32_t* part = c->hist;   // 2 words per block (<= 2 * 256 * kMaxChunks)
         hipLaunchKernelGGL(k_wscan_reduce, dim3(wb), dim3(kBlock), 0, s, (const uint32_t*)cnt_u, (const uint32_t*)cnt_g,
@@ -738,9 +716,33 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         hipLaunchKernelGGL(k_u_gather, dim3(g), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)c->words,
                            (const uint32_t*)ws, (const uint32_t*)cnt_u, (const uint32_t*)cnt_g, so, c->u_pos[0],
                            c->u_idx[0], c->u_g[0], rm);
+    }
+    tm.end();
+    SA_HIP(hipGetLastError());
+    SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipStreamSynchronize(s));
+    if (c->host_words[6]) {
+        SA_TRACE("  bucketed round 1: local sort flags %u, full sort instead", c->host_words[6]);
+        return SA_OK;
+    }
+    seg[0] = c->host_words[0];
+    seg[1] = c->host_words[1];
+    seg[2] = c->host_words[2];
+    add_bytes(st, SA_K_LOCAL_SORT, seg[1] * 28);   // unsorted set: rank, member bit, 3 tmp words
+    add_bytes(st, SA_K_SEG_WRITE, 8 * (2 * nw + 2) + seg[1] * 24);
+    if (!br_.always_u && seg[1] > n / kSparseDiv) {
+        // dense ranks follow (segments() over every key1): the same sort
+        // again, writing every key1 and nothing of the unsorted set
+        SegOut full{};
+        full.ksh = 0;
+        SA_HIP(hipMemsetAsync(c->words + 10, 0, 4, s));   // the skewed-window list is rebuilt
+        tm.begin(SA_K_LOCAL_SORT);
+        local_sort(full);
         tm.end();
-        add_bytes(st, SA_K_SEG_WRITE, 8 * (2 * nw + 2) + seg[1] * 24);
+        add_bytes(st, SA_K_LOCAL_SORT, 20 * m);
         SA_HIP(hipGetLastError());
+    } else {
+        *ksh = kKeySample;
         *fused = true;
     }
     SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u cmp=%u pk8=%d windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R,
