@@ -439,13 +439,15 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         const bool pow2 = (bp.bs.sigma & (bp.bs.sigma - 1)) == 0;
         // (the DNA kernel keys each position from a 32-symbol window)
         const bool dna = SA_DNA_SWAR && c->dna && bp.bs.s + bp.bs.R + kItemsA - 1 <= 32 && 2 * bp.bs.s <= 32;
+        // (sigma = 256: each position's key from the 8-byte window at it)
+        const bool ident = SA_TEXT_IDENT && bp.bs.sigma == 256 && bp.bs.s + bp.bs.R <= 8 && bp.bs.s <= 4;
         auto text_grid = [&](int block) {
             const uint64_t tile = (uint64_t)block * kItemsA;
             return (uint32_t)std::max<uint64_t>(
                 1, std::min<uint64_t>((n + tile - 1) / tile, (uint64_t)c->cus * (kSpBlock / block)));
         };
-#define SA_TEXT_PASS(P, PK, BLK, DNA)                                                                         \
-    hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK, DNA>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n, \
+#define SA_TEXT_PASS(P, PK, BLK, DNA, ID)                                                                     \
+    hipLaunchKernelGGL((k_split_text<kItemsA, BLK, P, PK, DNA, ID>), dim3(text_grid(BLK)), dim3(BLK), 0, s, d_text, n, \
                        (const uint16_t*)c->code, bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)),           \
                        os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, m, blo, bhi,                          \
                        padded ? (const uint32_t*)pstart + 1 : nullptr, padded ? c->words + 11 : nullptr, hb, bp.ib, \
@@ -466,13 +468,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u,
                                    striped ? (const uint32_t*)rcur : nullptr, rcap);
         } else if (pk8 && dna) {
-            SA_TEXT_PASS(true, true, kTextBlock, true);
+            SA_TEXT_PASS(true, true, kTextBlock, true, false);
+        } else if (pk8 && ident) {
+            SA_TEXT_PASS(true, true, kTextBlock, false, true);
         } else if (pk8) {
-            SA_TEXT_PASS(true, true, kTextBlock, false);
+            SA_TEXT_PASS(true, true, kTextBlock, false, false);
+        } else if (pow2 && ident) {
+            SA_TEXT_PASS(true, false, kTextBlock, false, true);
         } else if (pow2) {
-            SA_TEXT_PASS(true, false, kTextBlock, false);
+            SA_TEXT_PASS(true, false, kTextBlock, false, false);
         } else {
-            SA_TEXT_PASS(false, false, kSpBlock, false);
+            SA_TEXT_PASS(false, false, kSpBlock, false, false);
         }
 #undef SA_TEXT_PASS
     }

@@ -358,10 +358,17 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // without per-item tests (its LDS atomics unpredicated): 3.54 -> 3.27-3.37
 // ms at 1 GiB DNA; the staging and write loops alone made no difference
 // (profiles/r04_n_ab_full_tiles.txt)
+#ifndef SA_TEXT_IDENT
+#define SA_TEXT_IDENT 1   // sigma = 256: keys from byte windows (k_split_text<.., IDENT>)
+#endif
 #ifndef SA_TEXT_FULL
 #define SA_TEXT_FULL 1
 #endif
-template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false, bool DNA = false>
+// IDENT (sigma = 256, every byte present, K <= 8): the dense digit is the
+// byte itself -- staged without the byte map, and each position's D and
+// remainder are bit fields of the big-endian 8-byte window at it (two
+// alignbyte + bswap of the lane's staged words) instead of a roll by bytes
+template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false, bool DNA = false, bool IDENT = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -485,6 +492,8 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 if (whole) {
                     if constexpr (DNA)
                         o = ((raw[i] >> 1) ^ (raw[i] >> 2)) & 0x03030303u;
+                    else if constexpr (IDENT)
+                        o = raw[i];
                     else
                         o = (uint32_t)s_map[raw[i] & 0xFFu] | ((uint32_t)s_map[(raw[i] >> 8) & 0xFFu] << 8) |
                             ((uint32_t)s_map[(raw[i] >> 16) & 0xFFu] << 16) | ((uint32_t)s_map[raw[i] >> 24] << 24);
@@ -524,7 +533,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             // interior low = r mulR + addR (BucketSpec: compact or not)
             const uint64_t mulR = b.cmp ? 2u : b.R + 1u, addR = b.cmp ? 1u : b.s + b.R;
             uint64_t win = 0;   // DNA: symbols l0 .. l0 + 31, the first on top
-            if constexpr (DNA) {
+            uint32_t wid[IDENT ? ITEMS / 4 + 2 : 1];   // IDENT: the lane's staged words from l0
+            if constexpr (IDENT) {
+#pragma unroll
+                for (int q = 0; q < ITEMS / 4 + 2; ++q) wid[q] = s_dcw[l0 / 4 + q];
+            } else if constexpr (DNA) {
                 const uint32_t bo = l0 / 4, sh = bo & 3u;   // l0 % 4 == 0: one packed byte per 4 symbols
                 const uint32_t w0 = s_pkw[bo >> 2], w1 = s_pkw[(bo >> 2) + 1], w2 = s_pkw[(bo >> 2) + 2];
                 win = ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(w1, w0, sh)) << 32) |
@@ -541,7 +554,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             // the digits leaving D (l0 ..), moving from the remainder into D
             // (l0 + s ..) and entering the remainder (l0 + K ..)
             uint32_t xo[ITEMS / 4], xm[ITEMS / 4], xn[ITEMS / 4];
-            if constexpr (!DNA) {
+            if constexpr (!DNA && !IDENT) {
                 lds_bytes<ITEMS>(s_dcw, l0, xo);
                 lds_bytes<ITEMS>(s_dcw, l0 + b.s, xm);
                 lds_bytes<ITEMS>(s_dcw, l0 + K, xn);
@@ -557,6 +570,12 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                     const uint64_t x = win << (2 * j);
                     D = (uint32_t)(x >> dsh);
                     r = (x >> rsh) & rmask;
+                } else if constexpr (IDENT) {
+                    const uint64_t x =
+                        ((uint64_t)__builtin_bswap32(__builtin_amdgcn_alignbyte(wid[j / 4 + 1], wid[j / 4], j % 4)) << 32) |
+                        __builtin_bswap32(__builtin_amdgcn_alignbyte(wid[j / 4 + 2], wid[j / 4 + 1], j % 4));
+                    D = (uint32_t)(x >> (64u - 8u * b.s));
+                    r = (x >> (64u - 8u * K)) & rmask;
                 } else if (j > 0) {
                     const uint32_t xi = byte_at<ITEMS>(xm, j - 1);
                     if constexpr (POW2) {
