@@ -794,7 +794,24 @@ __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__
     uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) * 16;
     uint4 v = make_uint4(0u, 0u, 0u, 0u);
     if (i < n && whole(i)) v = *reinterpret_cast<const uint4*>(text + i);
+    // a wave whose lanes together have seen all 256 byte values stops
+    // reading (presence cannot grow further): checked after steps 1, 2, 4,
+    // 8, ... so a text with fewer values (DNA) pays a few checks per wave;
+    // byte256 text reads ~1 KiB per wave instead of its whole share
+    uint32_t step = 0;
     for (; i < n; i += stride) {
+        if (step && (step & (step - 1)) == 0) {   // uniform
+            uint32_t all = ~0u;
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                uint32_t x = m[q];
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o, kWave);
+                all &= x;
+            }
+            if (all == ~0u) break;
+        }
+        ++step;
         const uint64_t in = i + stride;
         uint4 vn = make_uint4(0u, 0u, 0u, 0u);
         if (in < n && whole(in)) vn = *reinterpret_cast<const uint4*>(text + in);
@@ -809,12 +826,24 @@ __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__
         }
         v = vn;
     }
+    // one global atomic per word and workgroup, and none for bits already
+    // set there (8 same-address atomics per wave serialised in the L2: 0.4 ms
+    // of byte256's alphabet pass once its waves stopped early)
+    __shared__ uint32_t s_or[8];
+    if (threadIdx.x < 8) s_or[threadIdx.x] = 0;
+    __syncthreads();
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
         uint32_t x = m[i];
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) x |= __shfl_xor(x, o, kWave);
-        if (lane_id() == 0 && x) atomicOr(&present[i], x);
+        if (lane_id() == 0 && x) atomicOr(&s_or[i], x);
+    }
+    __syncthreads();
+    if (threadIdx.x < 8) {
+        const uint32_t x = s_or[threadIdx.x];
+        if (x & ~__hip_atomic_load(&present[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+            atomicOr(&present[threadIdx.x], x);
     }
 }
 
