@@ -104,6 +104,32 @@ def test_reference_lsd_queues(gpu, oracle, debug):
         assert st["rounds"] == rounds and st["distinct"] == dj, (kind, n, debug)
 
 
+def test_alphabet_late_values(gpu, oracle):
+    """The alphabet pass stops a wave once its lanes have seen all 256 byte
+    values (k_alphabet): texts where some values appear only near the end,
+    or only once, still report every value present -- sigma and the SA
+    agree with the oracle; byte256 text takes the 8-byte window first pass."""
+    from hpc_suffix_array_amd import build_suffix_array
+    rng = np.random.default_rng(13)
+    n = 3_000_017
+    # all 256 values early (waves stop), and a text missing 0x7F but at its end
+    t = rng.integers(0, 256, n, dtype=np.uint8)
+    t[t == 0x7F] = 0x80
+    t[-1] = 0x7F
+    cases = [t]
+    # every value once, each in a different part of a mostly-'a' text
+    u = np.full(n, ord("a"), np.uint8)
+    u[rng.choice(n, 256, replace=False)] = np.arange(256, dtype=np.uint8)
+    cases.append(u)
+    # random bytes without one value at all (255 present)
+    v = rng.integers(0, 255, n, dtype=np.uint8)
+    cases.append(v)
+    for x, sigma in zip(cases, (256, 256, 255)):
+        got, st = build_suffix_array(x, return_stats=True)
+        assert st["sigma"] == sigma, (st["sigma"], sigma)
+        assert (got == oracle.sa_c(x)).all()
+
+
 @pytest.mark.parametrize("schedule", ["packed", "reference"])
 @pytest.mark.parametrize("radix", ["onesweep", "reduce_scan"])
 def test_radix_algorithms(gpu, oracle, schedule, radix):
