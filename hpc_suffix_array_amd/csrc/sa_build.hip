@@ -125,6 +125,8 @@ struct sa_context {
     uint32_t* u_pos[2] = {nullptr, nullptr};    // compacted unsorted set, ping-pong
     uint32_t* u_idx[2] = {nullptr, nullptr};
     uint32_t* u_g[2] = {nullptr, nullptr};
+    uint32_t* u_gs[2] = {nullptr, nullptr};     // each set's group starts (pivot rounds; allocated at the first)
+    uint64_t gscap = 0;
     uint64_t* keys_u = nullptr;                 // third key buffer (unsorted-set rounds)
     uint64_t kucap = 0;                         // keys_u capacity (items): ucap + the XQ regions' slack
     uint32_t* segx = nullptr;                   // second bucket pass, per-XCD queues (sa_split.h SegXq) + tables
@@ -208,8 +210,10 @@ static void free_u_buffers(sa_context* c) {
         hipFree(c->u_pos[i]);
         hipFree(c->u_idx[i]);
         hipFree(c->u_g[i]);
-        c->u_pos[i] = c->u_idx[i] = c->u_g[i] = nullptr;
+        hipFree(c->u_gs[i]);
+        c->u_pos[i] = c->u_idx[i] = c->u_g[i] = c->u_gs[i] = nullptr;
     }
+    c->gscap = 0;
     c->ucap = 0;
     c->kucap = 0;
 }
@@ -270,6 +274,33 @@ static int ensure_u_capacity(sa_context* c, uint64_t n) {
     SA_TRACE("unsorted-set buffers: vals_u %p keys_u %p", (void*)c->vals_u, (void*)c->keys_u);
     return SA_OK;
 }
+
+// each unsorted set's group starts (pivot rounds, sa_pivot.h MODE 1): G <=
+// m / 2 <= n / 2 words per set, allocated when a build first takes a pivot
+// round (range builds never do)
+static int ensure_gs(sa_context* c, uint64_t n) {
+    if (n <= c->gscap && c->u_gs[0]) return SA_OK;
+    for (int i = 0; i < 2; ++i) {
+        hipFree(c->u_gs[i]);
+        c->u_gs[i] = nullptr;
+    }
+    c->gscap = 0;
+    const uint64_t w = n / 2 + 64;
+    for (int i = 0; i < 2; ++i)
+        if (hipMalloc(&c->u_gs[i], w * 4) != hipSuccess) {
+            (void)hipGetLastError();
+            for (int k = 0; k < 2; ++k) {
+                hipFree(c->u_gs[k]);
+                c->u_gs[k] = nullptr;
+            }
+            return set_err(SA_E_NOMEM, "group-start buffers (%llu words)", (unsigned long long)w);
+        }
+    c->gscap = n;
+    return SA_OK;
+}
+
+// set i's group-start buffer when it holds an n-suffix build's groups
+static uint32_t* gs_buf(const sa_context* c, uint64_t n, int i) { return n <= c->gscap ? c->u_gs[i] : nullptr; }
 
 // Per-launch HIP-event timing, enabled by sa_opts.profile.
 struct Timer {
@@ -1009,7 +1040,7 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
                     bool sparse_ok, bool* sparse_out,
                     uint32_t* sa, int uo, hipStream_t s, Timer& tm, sa_stats* st, uint64_t* D, uint64_t* m,
                     uint64_t* G, uint32_t* rank_arr = nullptr, uint64_t rank_off = 0, RankMap rm = RankMap{},
-                    uint64_t set_off = 0, uint32_t g_off = 0) {
+                    uint64_t set_off = 0, uint32_t g_off = 0, uint32_t* gsn = nullptr) {
     // rank_arr / rank_off / rm: the range-partitioned build's compact rank map
     // and its SA offset (sa_dist.h); the context's rank array, 0 and the
     // identity map on one GPU.  set_off / g_off: the next unsorted set's
@@ -1044,7 +1075,7 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     hipLaunchKernelGGL(k_seg_write<Pos>, dim3(ch.chunks), dim3(kBlock), 0, s, keys, idx, ch, pos,
                        (const uint32_t*)c_u, (const uint32_t*)c_uh, (const uint32_t*)c_l, rank_arr, sa,
                        c->u_pos[uo] + set_off, c->u_idx[uo] + set_off, c->u_g[uo] + set_off, member, sparse ? 0 : 1,
-                       (uint32_t)rank_off, rm, g_off);
+                       (uint32_t)rank_off, rm, g_off, gsn ? gsn + g_off : nullptr, (uint32_t)set_off);
     tm.end();
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_SEG_COUNT, 8 * ch.n);
@@ -1060,15 +1091,23 @@ static bool pivot_ok(const sa_context* c, uint64_t m, uint64_t G, uint32_t wr, b
     return !(c->dbg & SA_DEBUG_NO_PIVOT) && c->radix == 0 && !sparse && m >= (1u << 16) && G >= 1 && G <= m / 4 && bit_width(2 * G + 1) + wr <= 64;
 }
 
+// keys + class counts of a pivot round in one pass when the set came with its
+// group starts (sa_pivot.h MODE 1; A/B switch)
+#ifndef SA_PIVOT_MERGED
+#define SA_PIVOT_MERGED 1
+#endif
 // tied-block rounds (sa_pivot.h) scan the groups in one workgroup
 constexpr uint64_t kPivotTiedMaxG = 1u << 18;
 
 static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, uint64_t G, uint64_t h, uint32_t wr,
                        uint64_t* ukb0, uint64_t* ukb1, uint64_t* kbA, const Chunking& cu, uint32_t* d_sa,
                        hipStream_t s, Timer& tm, sa_stats* st, uint64_t** sorted, uint32_t* P, bool* segs_done,
-                       uint64_t* Du, uint64_t* m2, uint64_t* G2) {
+                       uint64_t* Du, uint64_t* m2, uint64_t* G2, bool have_gs, bool* gs_written) {
+    // have_gs: the set's group starts are in u_gs[ui] (written with it by the
+    // previous round); *gs_written: this round wrote the next set's to u_gs[uo]
     *sorted = nullptr;
     *segs_done = false;
+    *gs_written = false;
     // tied-block round: its scratch is ukb0 (free: the tied members skip the
     // sorted output) -- gs, pr, toff, tid, then the rest's values (3 x
     // m' <= 3 m / 2 words)
@@ -1077,27 +1116,46 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     const uint64_t ra_max = align_up(m / 2, 64);
     const bool tied = !(c->dbg & SA_DEBUG_NO_TIED) && G <= kPivotTiedMaxG && sbase + 3 * ra_max <= scap;
     uint32_t* const scr = reinterpret_cast<uint32_t*>(ukb0);
-    uint32_t* const gs = tied ? scr : c->u_pos[uo];   // G + 1 group starts
-    uint32_t* const pr = gs + G + 1;                  // G pivot ranks
+    const bool merged = SA_PIVOT_MERGED && tied && have_gs;
+    uint32_t* const gs = merged ? c->u_gs[ui] : tied ? scr : c->u_pos[uo];   // G (+ 1) group starts
+    uint32_t* const pr = (tied ? scr : gs) + G + 1;                          // G pivot ranks
     uint32_t* const gP = c->vals_alt;                 // 3 (G + 1): members of each class before each group
     uint32_t* const cc = c->hist;                     // 3 x chunks class counts, scanned in place
     const uint32_t Gu = (uint32_t)G;
-    tm.begin(SA_K_PIVOT_KEYS);
-    hipLaunchKernelGGL(k_pivot_keys,
-                       dim3((uint32_t)std::min<uint64_t>((m + kBlock * kPkItems - 1) / (kBlock * kPkItems), 8192)),
-                       dim3(kBlock),
-                       0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m, (const uint32_t*)c->rank,
-                       n, h, wr, Gu, ukb1, gs, pr);
-    tm.end();
-    add_bytes(st, SA_K_PIVOT_KEYS, 20 * m);
-    tm.begin(SA_K_PIVOT_COUNT);
-    hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
-                       (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
-                       (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
-    hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
-    tm.end();
-    SA_HIP(hipGetLastError());
-    add_bytes(st, SA_K_PIVOT_COUNT, 8 * m);
+    if (merged) {
+        // the group starts came with the set: keys built and classes counted
+        // in one pass (MODE 1: k_pivot_keys + MODE 0)
+        tm.begin(SA_K_PIVOT_COUNT);
+        PivotKeySrc ks;
+        ks.rank = c->rank;
+        ks.n = n;
+        ks.h = h;
+        ks.keys_out = ukb1;
+        ks.pr_out = pr;
+        hipLaunchKernelGGL(k_pivot_pass<1>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)nullptr,
+                           (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                           (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{}, ks);
+        hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_PIVOT_COUNT, 20 * m);
+    } else {
+        tm.begin(SA_K_PIVOT_KEYS);
+        hipLaunchKernelGGL(k_pivot_keys,
+                           dim3((uint32_t)std::min<uint64_t>((m + kBlock * kPkItems - 1) / (kBlock * kPkItems), 8192)),
+                           dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], m,
+                           (const uint32_t*)c->rank, n, h, wr, Gu, ukb1, gs, pr);
+        tm.end();
+        add_bytes(st, SA_K_PIVOT_KEYS, 20 * m);
+        tm.begin(SA_K_PIVOT_COUNT);
+        hipLaunchKernelGGL(k_pivot_pass<0>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
+                           (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
+                           (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, nullptr, nullptr, TiedOut{});
+        hipLaunchKernelGGL(k_scan_rows, dim3(3), dim3(kBlock), 0, s, cc, cu.chunks, c->totals);
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_PIVOT_COUNT, 8 * m);
+    }
     SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
     const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
@@ -1115,11 +1173,14 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     uint32_t* const ridx = tied ? scr + sbase : c->u_idx[uo];
     uint64_t T = 0, Gt = 0, Dt = 0;
     if (tied) {
+        // the next set's group starts go with it (the next pivot round's MODE 1)
+        const int rg = ensure_gs(c, n);
+        if (rg) return rg;
         uint32_t* const toff = scr + 2 * G + 1;
         uint32_t* const tid = toff + G + 1;
         hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, Gu, toff, tid,
                            c->totals + 4);
-        const TiedOut to{c->u_pos[ui], toff, tid, c->rank, d_sa, c->u_pos[uo], c->u_idx[uo], c->u_g[uo]};
+        const TiedOut to{c->u_pos[ui], toff, tid, c->rank, d_sa, c->u_pos[uo], c->u_idx[uo], c->u_g[uo], c->u_gs[uo]};
         hipLaunchKernelGGL(k_pivot_pass<3>, dim3(cu.chunks), dim3(kBlock), 0, s, (const uint64_t*)ukb1,
                            (const uint32_t*)c->u_idx[ui], (const uint32_t*)c->u_g[ui], cu, (const uint32_t*)gs,
                            (const uint32_t*)pr, Gu, wr, cc, gP, nullptr, nullptr, kbA, ridx, to);
@@ -1173,12 +1234,13 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
         if (tied) {
             // the rest's segments, appended to the next set after the tied blocks
             rc = segments(c, rs, vfinal, plan_chunks(mr), PosArray{c->vals_u}, false, nullptr, d_sa, uo, s, tm, st,
-                          &Dr, &mrr, &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt);
+                          &Dr, &mrr, &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt, c->u_gs[uo]);
             if (rc) return rc;
         }
     }
     *P = 1 + Pr;
     if (tied) {
+        *gs_written = true;
         *segs_done = true;
         *Du = Dr + Dt;
         *m2 = mrr + T;
@@ -1197,7 +1259,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
 // fewer share it: the caller runs the LSD sort.
 static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_sa, hipStream_t s, Timer& tm,
                         sa_stats* st, bool* done, uint64_t* D, uint64_t* m, uint64_t* G, uint32_t* P) {
-    *done = false;
+    *done = false;   // (done: the set's group starts are in u_gs[0] too)
     const Chunking ch = plan_chunks(n);
     const uint64_t* keys = c->keys[1];
     uint32_t* const gs = c->u_pos[1];   // {0, n}: one group
@@ -1228,12 +1290,16 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     // next set goes to u_*[0]), key buffers keys_u / keys[0]
     uint64_t* const rk = c->keys[0];
     uint32_t* const ridx = c->u_idx[1];
+    {
+        const int rg = ensure_gs(c, n);   // the set's group starts, for round 2's MODE 1
+        if (rg) return rg;
+    }
     tm.begin(SA_K_PIVOT_WRITE);
     hipLaunchKernelGGL(k_pivot_gp, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gs, 1u, (const uint32_t*)cc, ch,
                        (const uint32_t*)c->totals, gP);
     hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, 1u, toff, tid,
                        c->totals + 4);
-    const TiedOut to{nullptr, toff, tid, c->rank, d_sa, c->u_pos[0], c->u_idx[0], c->u_g[0]};
+    const TiedOut to{nullptr, toff, tid, c->rank, d_sa, c->u_pos[0], c->u_idx[0], c->u_g[0], c->u_gs[0]};
     hipLaunchKernelGGL((k_pivot_pass<3, true>), dim3(ch.chunks), dim3(kBlock), 0, s, keys, nullptr, nullptr, ch,
                        (const uint32_t*)gs, nullptr, 1u, 0u, cc, gP, nullptr, nullptr, rk, ridx, to);
     tm.end();
@@ -1256,7 +1322,7 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
                             tm, st, &rs, &Pr);
         if (rc) return rc;
         rc = segments(c, rs, vfinal, plan_chunks(mr), PosGap{t0, t1}, false, nullptr, d_sa, 0, s, tm, st, &Dr, &mrr,
-                      &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt);
+                      &Gr, nullptr, 0, RankMap{}, T, (uint32_t)Gt, c->u_gs[0]);
         if (rc) return rc;
     }
     *done = true;
@@ -1358,15 +1424,19 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     }
     int uo = 0;
     bool sparse = false;
+    bool gs_ok[2] = {false, false};   // the set's group starts are in u_gs[set] (pivot rounds' MODE 1)
     if (r1_pivot) {   // pivot_round1 ran the segments (dense ranks)
+        gs_ok[0] = true;
     } else if (bucketed && fused) {   // segments came with the local sort (sparse ranks)
         D = seg1[0];
         m = seg1[1];
         G = seg1[2];
         sparse = true;
     } else {
-        rc = segments(c, keys1, d_sa, ch, PosIdentity{}, true, &sparse, nullptr, uo, s, tm, st, &D, &m, &G);
+        rc = segments(c, keys1, d_sa, ch, PosIdentity{}, true, &sparse, nullptr, uo, s, tm, st, &D, &m, &G, nullptr,
+                      0, RankMap{}, 0, 0, gs_buf(c, n, uo));
         if (rc) return rc;
+        gs_ok[uo] = gs_buf(c, n, uo) != nullptr;
     }
     // later rounds sort in the two buffers that do not hold the round-1 keys
     uint64_t* ukb0 = keys1 == c->keys[0] ? c->keys[1] : c->keys[0];
@@ -1434,9 +1504,11 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         }
         if (!sorted && pivot_ok(c, m, G, wr, sparse)) {
             uint64_t* kbA = ukb0 == c->keys[0] ? c->keys[1] : c->keys[0];   // the round-1 keys: dead with dense ranks
+            bool gsw = false;
             rc = pivot_round(c, ui, uo, n, m, G, h, wr, ukb0, ukb1, kbA, cu, d_sa, s, tm, st, &sorted, &P,
-                             &segs_done, &Du, &m2, &G2);
+                             &segs_done, &Du, &m2, &G2, gs_ok[ui], &gsw);
             if (rc) return rc;
+            if (segs_done) gs_ok[uo] = gsw;
         }
         if (sorted) {
             rc = SA_OK;
@@ -1471,8 +1543,9 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         if (rc) return rc;
         if (!segs_done) {
             rc = segments(c, sorted, c->vals_u, cu, PosArray{c->u_pos[ui]}, false, nullptr, d_sa, uo, s, tm, st, &Du,
-                          &m2, &G2);
+                          &m2, &G2, nullptr, 0, RankMap{}, 0, 0, gs_buf(c, n, uo));
             if (rc) return rc;
+            gs_ok[uo] = gs_buf(c, n, uo) != nullptr;
         }
         tm.round_mark();
         D = (n - m) + Du;

@@ -1178,7 +1178,8 @@ struct RankMap {
 //   sa[pos(s)]  = idx                               (when sa != nullptr)
 //   unsorted members are compacted, in order, to (u_pos, u_idx, u_g) with
 //   u_g the dense id of their group among unsorted groups (+ g_off: the
-//   tied-block round puts its tied groups first, sa_pivot.h).
+//   tied-block round puts its tied groups first, sa_pivot.h); gsn (when
+//   given) the first slot of each of those groups.
 template <class Pos>
 __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict__ keys,
                                                       const uint32_t* __restrict__ idx, Chunking ch, Pos pos,
@@ -1189,7 +1190,8 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                                                       uint32_t* __restrict__ u_pos, uint32_t* __restrict__ u_idx,
                                                       uint32_t* __restrict__ u_g, uint32_t* __restrict__ member,
                                                       int dense_rank, uint32_t rank_off, RankMap rm = RankMap{},
-                                                      uint32_t g_off = 0) {
+                                                      uint32_t g_off = 0, uint32_t* __restrict__ gsn = nullptr,
+                                                      uint32_t q_off = 0) {
     __shared__ uint64_t s_m[kWaves][kItems][3];
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
@@ -1276,7 +1278,11 @@ __global__ __launch_bounds__(kBlock) void k_seg_write(const uint64_t* __restrict
                     const uint32_t q = off_u + (uint32_t)__popcll(mu & lt);
                     u_pos[q] = p;
                     u_idx[q] = x;
-                    u_g[q] = g_off + off_uh + (uint32_t)__popcll(muh & le) - 1u;
+                    const uint32_t gl = off_uh + (uint32_t)__popcll(muh & le) - 1u;
+                    u_g[q] = g_off + gl;
+                    // the group's first slot, for the next round's pivot split
+                    // (gsn is offset by g_off, q by q_off: the set's slot)
+                    if (gsn && ((muh >> lane) & 1ull)) gsn[gl] = q_off + q;
                 }
             }
             off_u += __popcll(mu);

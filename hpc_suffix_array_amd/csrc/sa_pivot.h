@@ -98,6 +98,17 @@ struct TiedOut {
     uint32_t* __restrict__ u_pos = nullptr;
     uint32_t* __restrict__ u_idx = nullptr;
     uint32_t* __restrict__ u_g = nullptr;
+    uint32_t* __restrict__ gsn = nullptr;            // the next set's group starts (or null)
+};
+
+// MODE 1's key source: key(e) = u_g[e] << wr | rank[u_idx[e] + h] (0 past
+// the end), written to keys_out for the later passes; the pivot rank of
+// each group to pr_out at its start
+struct PivotKeySrc {
+    const uint32_t* __restrict__ rank = nullptr;
+    uint64_t n = 0, h = 0;
+    uint64_t* __restrict__ keys_out = nullptr;
+    uint32_t* __restrict__ pr_out = nullptr;
 };
 
 // MODE 0: cc[c * chunks + chunk] = members of class c in the chunk, and for
@@ -107,6 +118,9 @@ struct TiedOut {
 // MODE 2: tied members -> okeys / oidx at their final slots; the rest ->
 //         rkeys / ridx at (members of classes 0 and 2 before them).
 // MODE 3: the rest as MODE 2; tied members -> rank / sa / next set (TiedOut).
+// MODE 1: MODE 0 with the keys built here (PivotKeySrc) instead of read:
+//         k_pivot_keys and MODE 0 in one pass, when the group starts gs came
+//         with the previous round's set (k_seg_write / MODE 3 wrote them)
 // R1: round 1 (build_packed's pivot round 1): every suffix in one group, index
 //     e itself, keys the packed K-symbol keys, pivot keys[0]; the rest keeps
 //     its plain key (one group: key order already puts < p before > p).
@@ -119,14 +133,15 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                                                        uint32_t* __restrict__ cc, uint32_t* __restrict__ gP,
                                                        uint64_t* __restrict__ okeys, uint32_t* __restrict__ oidx,
                                                        uint64_t* __restrict__ rkeys, uint32_t* __restrict__ ridx,
-                                                       TiedOut to = TiedOut{}) {
+                                                       TiedOut to = TiedOut{}, PivotKeySrc ks = PivotKeySrc{}) {
+    constexpr bool COUNT = MODE == 0 || MODE == 1;
     __shared__ uint32_t s_w[3][kWaves];
     const uint32_t c = blockIdx.x;
     const uint64_t e0 = ch.begin(c), e1 = ch.end(c);
     const uint32_t wave = wave_id(), lane = lane_id();
     const uint64_t lt = lanemask_lt();
     uint32_t run[3] = {0, 0, 0};
-    if (MODE != 0)
+    if (!COUNT)
         for (int k = 0; k < 3; ++k) run[k] = cc[(uint64_t)k * ch.chunks + c];
     const uint64_t gstride = (uint64_t)G + 1;
     const uint64_t p1 = R1 ? keys[0] : 0ull;
@@ -139,9 +154,14 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
     auto group = [&](uint32_t gg) {
         if (gg == cg) return;
         cg = gg;
-        c_pr = R1 ? 0u : pr[gg];
         c_s0 = R1 ? 0u : gs[gg];
-        if (MODE != 0) {
+        if constexpr (MODE == 1) {   // the pivot: the key of the group's first member
+            const uint64_t x0 = u_idx[c_s0];
+            c_pr = x0 + ks.h < ks.n ? ks.rank[x0 + ks.h] : 0u;
+        } else {
+            c_pr = R1 ? 0u : pr[gg];
+        }
+        if (!COUNT) {
             c_cnt0 = gP[gg + 1] - gP[gg];
             c_b1 = gP[gstride + gg];
             c_cnt1 = gP[gstride + gg + 1] - c_b1;
@@ -160,12 +180,33 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
         // every row's key and index loaded before any store (vmcnt counts
         // loads and stores in order: a load issued between stores would make
         // its row wait for them)
+        if constexpr (MODE == 1) {
+            // every row's index and group, then the rank gathers, then the keys
 #pragma unroll
-        for (int j = 0; j < kItems; ++j) {
-            const uint64_t e = w0 + (uint64_t)j * kWave + lane;
-            key[j] = e < e1 ? keys[e] : 0ull;
-            xs[j] = (MODE != 0 && !R1 && e < e1) ? u_idx[e] : (uint32_t)e;
-            g[j] = (e < e1 && !R1) ? (uint32_t)(key[j] >> wr) : 0u;   // key = g << wr | rank
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                xs[j] = e < e1 ? u_idx[e] : 0u;
+                g[j] = e < e1 ? u_g[e] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                const uint64_t y = (uint64_t)xs[j] + ks.h;
+                key[j] = ((uint64_t)g[j] << wr) | (e < e1 && y < ks.n ? ks.rank[y] : 0u);
+            }
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                if (e < e1) ks.keys_out[e] = key[j];
+            }
+        } else {
+#pragma unroll
+            for (int j = 0; j < kItems; ++j) {
+                const uint64_t e = w0 + (uint64_t)j * kWave + lane;
+                key[j] = e < e1 ? keys[e] : 0ull;
+                xs[j] = (MODE != 0 && !R1 && e < e1) ? u_idx[e] : (uint32_t)e;
+                g[j] = (e < e1 && !R1) ? (uint32_t)(key[j] >> wr) : 0u;   // key = g << wr | rank
+            }
         }
         bool uni = true;
         if (!R1) {
@@ -220,11 +261,12 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                     const uint32_t P2 = off[2] + (uint32_t)__popcll(bm[2] & lt);
                     const uint32_t gg = g[j];
                     if (!decltype(uni_tag)::value) group(gg);
-                    if (MODE == 0) {
+                    if (COUNT) {
                         if (c_s0 == (uint32_t)e) {   // in-chunk counts before the group start
                             gP[gg] = P0;
                             gP[gstride + gg] = P1;
                             gP[2 * gstride + gg] = P2;
+                            if (MODE == 1) ks.pr_out[gg] = (uint32_t)(key[j] & ((1ull << wr) - 1ull));
                         }
                     } else {
                         const uint32_t x = xs[j];
@@ -238,6 +280,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
                                 to.u_pos[q] = c_bp + t;
                                 to.u_idx[q] = x;
                                 to.u_g[q] = c_tid;
+                                if (to.gsn && t == 0u) to.gsn[c_tid] = q;
                             }
                         } else if (cls[j] == 1u) {
                             const uint64_t ne = (uint64_t)c_s0 + c_cnt0 + (P1 - c_b1);
@@ -263,7 +306,7 @@ __global__ __launch_bounds__(kBlock) void k_pivot_pass(const uint64_t* __restric
         for (int k = 0; k < 3; ++k) run[k] += tot[k];
         __syncthreads();
     }
-    if (MODE == 0 && threadIdx.x == 0)
+    if (COUNT && threadIdx.x == 0)
         for (int k = 0; k < 3; ++k) cc[(uint64_t)k * ch.chunks + c] = run[k];
 }
 
