@@ -21,7 +21,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_pivot_pass<2", "pivot_write"),
+KINDS = [("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_pivot_pass<1", "pivot_count"), ("k_pivot_pass<2", "pivot_write"),
          ("k_pivot_pass<3", "pivot_write"), ("k_pivot_tied_scan", "pivot_write"),
          ("k_pivot_place", "pivot_place"), ("k_pivot_gp", "pivot_gp"), ("k_lsd_hist", "lsd_hist"),
          ("k_lsd_base", "lsd_base"), ("k_lsd<", "lsd"), ("k_perm_rank", "perm_rank"), ("k_perm_split", "perm_split"),
