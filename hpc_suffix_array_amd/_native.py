@@ -49,7 +49,7 @@ class SAError(RuntimeError):
 # tests force; every combination gives the same suffix array
 DEBUG_FLAGS = {"no_cmp": 0x1, "no_pk8": 0x2, "no_pad": 0x4, "pad_overflow": 0x8, "no_fast32": 0x10,
                "no_pivot": 0x20, "perm_always": 0x40, "no_xq": 0x80, "xq_overflow": 0x100,
-               "no_tied": 0x200}
+               "no_tied": 0x200, "no_key1_round": 0x400}
 
 
 def debug_bits(names) -> int:

@@ -1462,6 +1462,19 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         uint64_t* sorted = nullptr;
         bool segs_done = false;   // a tied-block pivot round ran its own segments
         uint64_t Du = 0, m2 = 0, G2 = 0;
+        // the first round after a bucketed round 1 with sparse ranks: the keys'
+        // ranks as key1 of x + K from the text (SrcUKey1) when group id and
+        // key1 + 1 fit 64 bits
+        uint32_t kb1 = 0;
+        if (bucketed && sparse && h == K && !(c->dbg & SA_DEBUG_NO_KEY1_ROUND)) {
+            unsigned __int128 dmax = 1;
+            for (uint32_t t = 0; t < bp.bs.s; ++t) dmax *= bp.bs.sigma;
+            const unsigned __int128 kmax = ((dmax - 1) << bp.bs.rb) | (((unsigned __int128)1 << bp.bs.rb) - 1);
+            uint32_t kw = 0;
+            for (unsigned __int128 x = kmax + 1; x; x >>= 1) ++kw;
+            kb1 = kw;
+        }
+        const bool key1_round = kb1 > 0 && kb1 + wg <= 64;
         if (c->radix == 0 && G > 0 && m <= kUsAvg * G) {
             // small groups on average: sort each group in registers, unless
             // one of them is larger than kUsLimit (then the radix sort below)
@@ -1472,7 +1485,10 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             // the keys first, one lane per suffix, then each group's lane sorts
             // them in place (ukb0 is read and written by that lane only)
             const uint32_t gk = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 65536);
-            if (sparse)
+            if (sparse && key1_round)
+                hipLaunchKernelGGL(k_usort_keys<SrcUKey1>, dim3(gk), dim3(kBlock), 0, s,
+                                   SrcUKey1{c->u_idx[ui], c->u_g[ui], rl, h, kb1}, m, ukb0);
+            else if (sparse)
                 hipLaunchKernelGGL(k_usort_keys<SrcU<true>>, dim3(gk), dim3(kBlock), 0, s,
                                    SrcU<true>{c->u_idx[ui], c->u_g[ui], rl, h, wr}, m, ukb0);
             else

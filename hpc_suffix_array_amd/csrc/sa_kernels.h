@@ -259,6 +259,32 @@ struct SrcU {
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
 };
 
+// The first unsorted-set round after a bucketed round 1 (h = K, sparse
+// ranks): rank[x + K] is the round-1 rank of suffix x + K, and round 1 sorted
+// every suffix by its K-symbol key1 -- equal key1 <=> one round-1 group <=>
+// equal rank, and key1 order = rank order.  So key1(x + K) + 1 (0 past the
+// end), rebuilt from the text (a few independent word loads), orders and
+// ties the members exactly as rank[x + K] does, without the sample search of
+// the SA that RankLookup::sparse needs for a suffix outside the unsorted set.
+// kb: bits of key1 + 1 (the host checks kb + bits of the group ids <= 64).
+struct SrcUKey1 {
+    const uint32_t* __restrict__ u_idx;
+    const uint32_t* __restrict__ u_g;
+    RankLookup rl;
+    uint64_t h;
+    uint32_t kb;
+    __device__ __forceinline__ uint64_t key(uint64_t e) const {
+        const uint64_t i = u_idx[e];
+        uint64_t r1 = 0;
+        if (i + h < rl.n) {
+            uint32_t D;
+            r1 = key1_words<true>(rl.text, rl.n, CodeMap{rl.code}, rl.bs, i + h, &D) + 1u;
+        }
+        return ((uint64_t)u_g[e] << kb) | r1;
+    }
+    __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
+};
+
 // An unsorted-set round whose groups are all small (most are pairs on
 // random text): each group -- a run of equal u_g, contiguous in SA order --
 // is sorted by its keys (g, rank[i + h]) in registers by the lane at its

@@ -91,6 +91,8 @@ enum sa_kernel_kind {
                                            queues and regions */
 #define SA_DEBUG_XQ_OVERFLOW 0x100u     /* per-XCD second pass with sub-regions of exactly 1/8 of each digit: a queue
                                            overflows and the round re-runs with the one-region pass */
+#define SA_DEBUG_NO_KEY1_ROUND 0x400u   /* the first round after a sparse bucketed round 1 takes its keys' ranks by
+                                           the sample search (RankLookup), not as key1 rebuilt from the text */
 #define SA_DEBUG_NO_TIED 0x200u         /* pivot rounds: tied blocks through the sorted output and segments(), not
                                            written straight to the next unsorted set (sa_pivot.h) */
 

@@ -104,6 +104,24 @@ def test_reference_lsd_queues(gpu, oracle, debug):
         assert st["rounds"] == rounds and st["distinct"] == dj, (kind, n, debug)
 
 
+@pytest.mark.parametrize("kind", ["dna", "alnum", "ascii127", "byte256"])
+def test_key1_round_two(gpu, oracle, kind):
+    """The first round after a sparse bucketed round 1 sorts its members by
+    key1(x + K) rebuilt from the text (SrcUKey1), which orders and ties them
+    as rank[x + K] does; debug "no_key1_round" takes the ranks by the sample
+    search instead.  Same SA, same D_j, as the oracle."""
+    from hpc_suffix_array_amd import build_suffix_array
+    n = 2_500_001
+    t = oracle.gen_text(kind, n, seed=17)
+    t[-40:] = t[:40]   # a repeat at the end: short suffixes in later rounds
+    ref = oracle.sa_c(t)
+    got, st = build_suffix_array(t, return_stats=True)
+    alt, st_alt = build_suffix_array(t, return_stats=True, debug=("no_key1_round",))
+    assert st["round1"] == "bucketed" and st["sparse_ranks"], st
+    assert (got == ref).all() and (alt == ref).all()
+    assert st["distinct"] == st_alt["distinct"]
+
+
 def test_alphabet_late_values(gpu, oracle):
     """The alphabet pass stops a wave once its lanes have seen all 256 byte
     values (k_alphabet): texts where some values appear only near the end,
