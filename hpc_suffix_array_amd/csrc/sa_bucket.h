@@ -874,6 +874,10 @@ struct SegOut {
     // rank map's slots are known only once the member bitmap is complete, so
     // k_u_gather places them
     uint32_t* tmp_rank = nullptr;
+    // 0: k_bucket_sort writes no key1 samples (one GPU: round 2 keys by key1
+    // from the text, SrcUKey1; a later round that searches the samples has
+    // them rebuilt first by k_key1_samples)
+    uint32_t samples = 1;
 };
 
 template <int BLOCK, int ITEMS>
@@ -1975,9 +1979,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 // positions, from the sorted words (a global load here would
                 // make the store phase wait for the next window's loads)
                 // (sa_search.h for_each_sample: exact up to a + hi = 2^32)
-                for_each_sample(a, lo, hi, so.ksh, [&](uint32_t q) {
-                    keys_out[(a + q) >> so.ksh] = mn + (((uint64_t)sb << low_bits) | (s_k[q] >> kSlotBits));
-                });
+                if (so.samples)
+                    for_each_sample(a, lo, hi, so.ksh, [&](uint32_t q) {
+                        keys_out[(a + q) >> so.ksh] = mn + (((uint64_t)sb << low_bits) | (s_k[q] >> kSlotBits));
+                    });
             }
             probe.mark(4);
             // 3. U / U-group offsets (one scan of both; heads = m - U + G)

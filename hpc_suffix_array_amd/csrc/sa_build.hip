@@ -157,6 +157,7 @@ struct sa_context {
     int32_t span_extra = 0;
     int32_t tune = 0;
     bool dna = false;   // the text's alphabet is exactly {A, C, G, T} (k_split_text<.., DNA>)
+    bool samples_pending = false;   // round 1 wrote no key1 samples (SegOut::samples = 0)
 };
 
 namespace sa {
@@ -1366,6 +1367,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const Chunking ch = plan_chunks(n);
     uint64_t* keys1 = nullptr;
     uint32_t ksh1 = 0;   // bucketed round 1: keys1 holds every 2^ksh1-th sorted key1
+    c->samples_pending = false;
     uint32_t P = 0;
 
     // round 1: sort every suffix by its first K symbols -- bucketed (two
@@ -1444,6 +1446,21 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const RankLookup rl{c->rank, c->member, keys1, d_text, (const uint16_t*)c->code, n, base, K,
                         bucketed ? 1u : 0u, bp.bs, bucketed ? c->segw + kBstartOff : nullptr, d_sa, ksh1};
     if (st) st->sparse_ranks = sparse ? 1 : 0;
+    // the key1 samples RankLookup::sparse searches, before the first round
+    // that looks a rank up through them (round 1 left them out: SegOut::samples)
+    auto ensure_samples = [&]() -> int {
+        if (!c->samples_pending) return SA_OK;
+        c->samples_pending = false;
+        const uint64_t ns = (n + (1ull << ksh1) - 1) >> ksh1;
+        const uint32_t g = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((ns + kBlock - 1) / kBlock, 8192));
+        tm.begin(SA_K_SORT_U);
+        hipLaunchKernelGGL(k_key1_samples, dim3(g), dim3(kBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,
+                           (const uint32_t*)d_sa, ksh1, keys1);
+        tm.end();
+        SA_HIP(hipGetLastError());
+        add_bytes(st, SA_K_SORT_U, 12 * ns);
+        return SA_OK;
+    };
     tm.round_mark();
     record_round(st, 0.f, D, P, n, K);
     SA_TRACE("  round 1: D=%llu unsorted=%llu groups=%llu", (unsigned long long)D, (unsigned long long)m,
@@ -1478,6 +1495,10 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
         if (c->radix == 0 && G > 0 && m <= kUsAvg * G) {
             // small groups on average: sort each group in registers, unless
             // one of them is larger than kUsLimit (then the radix sort below)
+            if (sparse && !(SA_US_TWO_PHASE && key1_round)) {
+                rc = ensure_samples();
+                if (rc) return rc;
+            }
             SA_HIP(hipMemsetAsync(c->words + kUsFlagWord, 0, 4, s));
             const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 8192);
             tm.begin(SA_K_SORT_U);
@@ -1535,6 +1556,10 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             if (rc) return rc;
             const uint32_t Pu = (bits + 7) / 8;
             const uint32_t grid = (uint32_t)std::min<uint64_t>((m + kBlock - 1) / kBlock, 2048);
+            if (sparse) {
+                rc = ensure_samples();
+                if (rc) return rc;
+            }
             tm.begin(SA_K_SORT_U);
             if (sparse)
                 hipLaunchKernelGGL(k_materialize<SrcU<true>>, dim3(grid), dim3(kBlock), 0, s,
@@ -1548,6 +1573,8 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             rc = radix_sort(c, SrcKeys{ukb1, c->u_idx[ui]}, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s,
                             tm, st, &sorted, &P, true, true);
         } else if (sparse) {
+            rc = ensure_samples();
+            if (rc) return rc;
             SrcU<true> su{c->u_idx[ui], c->u_g[ui], rl, h, wr};
             rc = radix_sort(c, su, 12 * m, cu, bits, c->vals_u, c->vals_alt, ukb0, ukb1, s, tm, st, &sorted, &P,
                             false, true);

@@ -285,6 +285,22 @@ struct SrcUKey1 {
     __device__ __forceinline__ uint32_t val(uint64_t e) const { return u_idx[e]; }
 };
 
+// The key1 samples of the sorted round-1 suffixes (every 2^ksh-th SA
+// position; RankLookup::sparse searches them), rebuilt from the SA and the
+// text when k_bucket_sort did not write them (SegOut::samples = 0).  Round 2
+// reorders only inside round-1 groups, whose members share key1, so the
+// samples are the same after it.
+__global__ __launch_bounds__(kBlock) void k_key1_samples(const uint8_t* __restrict__ text, uint64_t n,
+                                                         const uint16_t* __restrict__ code, BucketSpec bs,
+                                                         const uint32_t* __restrict__ sa, uint32_t ksh,
+                                                         uint64_t* __restrict__ keys1) {
+    const uint64_t ns = (n + (1ull << ksh) - 1) >> ksh;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t < ns; t += (uint64_t)gridDim.x * kBlock) {
+        uint32_t D;
+        keys1[t] = key1_words<true>(text, n, CodeMap{code}, bs, sa[t << ksh], &D);
+    }
+}
+
 // An unsorted-set round whose groups are all small (most are pairs on
 // random text): each group -- a run of equal u_g, contiguous in SA order --
 // is sorted by its keys (g, rank[i + h]) in registers by the lane at its

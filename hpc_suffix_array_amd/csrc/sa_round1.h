@@ -57,6 +57,9 @@
 #define SA_KEY_SAMPLE 4
 #endif
 constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
+#ifndef SA_LAZY_SAMPLES
+#define SA_LAZY_SAMPLES 1
+#endif
 // padded first-pass segments (k_bucket_sample) from 2^26 suffixes up to the
 // bucketed round's one-GPU maximum; their starts live in the onesweep base
 // scratch after the second pass's 2^hb (<= 1024) digit bases
@@ -630,6 +633,10 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // key1 below (segments() reads them all)
     SegOut so{rank_arr, member, br_.sa_off, c->u_pos[1], c->u_idx[1], c->u_g[1], cnt_u, cnt_g, kKeySample};
     so.tmp_rank = br_.prefix ? br_.tmp_rank : nullptr;
+    // one GPU: no samples now (round 2 keys by key1 from the text); a later
+    // round that needs them rebuilds them (build_packed, k_key1_samples).
+    // Range builds answer other ranks' look-ups from them: always written.
+    so.samples = (SA_LAZY_SAMPLES && !br_.always_u && !(c->dbg & SA_DEBUG_NO_KEY1_ROUND)) ? 0u : 1u;
     // fixed-span windows whose keys cluster, for a second launch with the
     // measured span (after the windows' first buckets: 7 nw + 4 <= capacity)
     uint32_t* const retry = cnt_g + 2 * nw + 2;
@@ -692,7 +699,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.begin(SA_K_LOCAL_SORT);
     local_sort(so);
     tm.end();
-    add_bytes(st, SA_K_LOCAL_SORT, 12 * m + (m >> kKeySample) * 8);
+    add_bytes(st, SA_K_LOCAL_SORT, 12 * m + (so.samples ? (m >> kKeySample) * 8 : 0));
     SA_HIP(hipGetLastError());
     // the unsorted set, in SA order, compacted before the counts are read
     // back (its launches overlap that round trip; a round that turns out
@@ -750,6 +757,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     } else {
         *ksh = kKeySample;
         *fused = true;
+        c->samples_pending = so.samples == 0u;
     }
     SA_TRACE("  bucketed round 1: s=%u R=%u rb=%u cmp=%u pk8=%d windows=%u (skewed %u) largest=%u", bp.bs.s, bp.bs.R,
              bp.bs.rb, bp.bs.cmp, pk8 ? 1 : 0, c->host_words[7], c->host_words[10], c->host_words[5]);

@@ -120,6 +120,21 @@ def test_key1_round_two(gpu, oracle, kind):
     assert st["round1"] == "bucketed" and st["sparse_ranks"], st
     assert (got == ref).all() and (alt == ref).all()
     assert st["distinct"] == st_alt["distinct"]
+    # round 1 leaves the key1 samples out unless a later round searches
+    # them (k_key1_samples): many planted repeats keep members after round 2,
+    # whose x + h land all over the text (mostly outside the set)
+    rng = np.random.default_rng(29)
+    u = oracle.gen_text(kind, n, seed=31)
+    src = rng.integers(0, n - 200, 300)
+    dst = rng.integers(0, n - 200, 300)
+    for a, b, ln in zip(src, dst, rng.integers(40, 160, 300)):
+        u[b:b + ln] = u[a:a + ln].copy()
+    ref = oracle.sa_c(u)
+    got, st = build_suffix_array(u, return_stats=True)
+    alt, st_alt = build_suffix_array(u, return_stats=True, debug=("no_key1_round",))
+    assert st["sparse_ranks"] and st["rounds"] > 2, st
+    assert (got == ref).all() and (alt == ref).all()
+    assert st["distinct"] == st_alt["distinct"]
 
 
 def test_alphabet_late_values(gpu, oracle):
