@@ -63,7 +63,7 @@ KERNEL_NAMES = {
     "scatter_first": "k_split_text<12,1024,POW2,PK8> (first bucket pass: key1 from the text, packed 8-byte items "
                      "scattered by atomic cursors) | k_onesweep<SrcKeysIota,1024,4> (LSD first round)",
     "local_sort": "k_bucket_sort<512,18> (per-window LDS sort: counting scatter + register sorting networks, "
-                  "largest sub-bucket first; SA + every 16th key1 written)",
+                  "largest sub-bucket first; SA written; every 16th key1 too only where a later round searches it)",
     "pack": "k_bucket_hist (first-pass digit totals) | k_pack_text (LSD first round keys)",
     "seg_count": "k_seg_count", "seg_write": "k_seg_write | k_wscan_* + k_u_gather",
     "sort_u": "unsorted-set sorts (k_materialize + k_onesweep<SrcKeys>)",
