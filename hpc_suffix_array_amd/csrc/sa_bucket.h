@@ -535,27 +535,21 @@ __global__ __launch_bounds__(kBlock) void k_window_list(const uint32_t* __restri
     const uint32_t lane = lane_id(), wave = wave_id();
     const uint64_t per = ((nw + gridDim.x - 1) / gridDim.x + kBlock - 1) / kBlock * kBlock;
     const uint64_t j0 = (uint64_t)blockIdx.x * per, j1 = j0 + per < nw ? j0 + per : nw;
-    uint32_t mx = 0;
-    for (uint64_t jb = j0; jb < j1; jb += kBlock) {
-        const uint64_t j = jb + threadIdx.x;
-        const uint32_t d = j < j1 ? ws[j + 1] - ws[j] : 0u;
+    // the workgroup's non-empty windows first, then its one claim (a claim
+    // per 256 windows serialised 4096 atomics on one word: 60 us at 2^30)
+    uint32_t mx = 0, cnt = 0;
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += kBlock) {
+        const uint32_t d = ws[j + 1] - ws[j];
         mx = d > mx ? d : mx;
-        const uint64_t bal = __ballot(d != 0);
-        if (lane == 0) s_n[wave] = (uint32_t)__popcll(bal);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t t = 0;
-            for (int x = 0; x < kWaves; ++x) {
-                const uint32_t c = s_n[x];
-                s_n[x] = t;
-                t += c;
-            }
-            s_base = t ? atomicAdd(&words[7], t) : 0u;
-        }
-        __syncthreads();
-        if (d) list[s_base + s_n[wave] + (uint32_t)__popcll(bal & lanemask_lt())] = (uint32_t)j;
-        __syncthreads();
+        cnt += d != 0;
     }
+    uint32_t tot;
+    uint32_t off = block_exclusive_sum(cnt, s_n, &tot);
+    if (threadIdx.x == 0) s_base = tot ? atomicAdd(&words[7], tot) : 0u;
+    __syncthreads();
+    off += s_base;
+    for (uint64_t j = j0 + threadIdx.x; j < j1; j += kBlock)
+        if (ws[j + 1] != ws[j]) list[off++] = (uint32_t)j;
 #pragma unroll
     for (int o = kWave / 2; o > 0; o >>= 1) {
         const uint32_t y = __shfl_xor(mx, o, kWave);
