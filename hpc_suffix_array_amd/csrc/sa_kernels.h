@@ -816,8 +816,9 @@ __global__ __launch_bounds__(kBlock) void k_rerank(const uint64_t* __restrict__ 
 // (no LDS atomics, so a 4-symbol text costs no bank conflicts), OR-reduced
 // over the wave, one atomicOr per word per wave.
 // (one LDS atomic per 16-byte chunk inside one 32-symbol block instead of 16
-// measured equal at 1 GiB DNA, profiles/r02_bd_ab_alpha_fast.txt: the kernel
-// is not bound by its LDS atomics)
+// measured equal at 1 GiB DNA in r02, profiles/r02_bd_ab_alpha_fast.txt; in
+// r05 0.255-0.263 -> 0.235-0.243 ms, profiles/r05_am_ab_alpha_chunk_*.txt;
+// two chunks per lane in flight instead of one made no further difference)
 __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__ text, uint64_t n,
                                                      uint32_t* __restrict__ present) {
     // a private 256-bit mask per lane in LDS, set by one atomic OR per byte
@@ -859,10 +860,27 @@ __global__ __launch_bounds__(kBlock) void k_alphabet(const uint8_t* __restrict__
         if (in < n && whole(in)) vn = *reinterpret_cast<const uint4*>(text + in);
         if (whole(i)) {
             const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+            // the 16 bytes in one 32-value word of the mask (DNA, one case of
+            // letters: every chunk): their bits OR-ed in registers, one LDS
+            // atomic per chunk instead of one per byte
+            uint32_t o = v.x | v.y | v.z | v.w, a = v.x & v.y & v.z & v.w;
+            o |= o >> 16;
+            o |= o >> 8;
+            a &= a >> 16;
+            a &= a >> 8;
+            if (((o ^ a) & 0xE0u) == 0u) {
+                uint32_t bits = 0;
 #pragma unroll
-            for (int q = 0; q < 4; ++q)
+                for (int q = 0; q < 4; ++q)
 #pragma unroll
-                for (int b = 0; b < 4; ++b) add((w4[q] >> (8 * b)) & 0xFFu);
+                    for (int b = 0; b < 4; ++b) bits |= 1u << ((w4[q] >> (8 * b)) & 31u);
+                atomicOr(&m[(o & 0xFFu) >> 5], bits);
+            } else {
+#pragma unroll
+                for (int q = 0; q < 4; ++q)
+#pragma unroll
+                    for (int b = 0; b < 4; ++b) add((w4[q] >> (8 * b)) & 0xFFu);
+            }
         } else {
             for (uint64_t j = i; j < n && j < i + 16; ++j) add(text[j]);
         }

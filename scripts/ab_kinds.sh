@@ -8,7 +8,7 @@ for k in alnum ascii127 byte256 dna; do
 import json,sys
 d=json.loads([l for l in open(sys.argv[3]) if l.startswith('{')][0])
 k=d['kernels_ms_per_step']
-print(sys.argv[1], sys.argv[2], d['ms_per_step'], d['verified'], 'first', k['scatter_first'], 'second', k['scatter_keys'], 'local', k['local_sort'], 'u', k['sort_u'], 'rounds', d['rounds'])
+print(sys.argv[1], sys.argv[2], d['ms_per_step'], d['verified'], 'alpha', k['alphabet'], 'first', k['scatter_first'], 'second', k['scatter_keys'], 'local', k['local_sort'], 'u', k['sort_u'], 'rounds', d['rounds'])
 PY
   done
 done
