@@ -86,6 +86,8 @@ def parse():
     ap.add_argument("--no-reference-schedule", action="store_true",
                     help="skip the companion build with the north-star schedule (N = 1, packed runs only)")
     ap.add_argument("--no-profile", action="store_true", help="no per-launch HIP events")
+    ap.add_argument("--no-lcp", action="store_true",
+                    help="skip the timed LCP + O(n) check after the build (N = 1: post_build)")
     ap.add_argument("--schedule", default="packed", choices=["packed", "reference"])
     ap.add_argument("--init-chars", type=int, default=0)
     ap.add_argument("--radix", default="onesweep", choices=["onesweep", "reduce_scan"])
@@ -221,6 +223,35 @@ def reference_schedule(b, d_text, n, d_sa, sptr, a, torch, dev, reps: int = 2) -
             "verified": b.check(d_text, n, d_sa, stream=sptr)}
 
 
+def post_build(b, d_text, n, d_sa, sptr, torch, dev, reps: int = 3) -> dict:
+    """The reference caller's flow after build_suffix_array
+    (main_sequential.c:108-120): build_lcp_array + the longest repeated
+    substring (LCP_TIME, manber_myers.c:135-182) and is_valid_suffix_array
+    (:184-202), each on the GPU from the SA in HBM: one warm-up, then the
+    median wall time of `reps` (stream-synchronised) calls.  Not part of the
+    headline `value`."""
+    d_lcp = torch.empty(n, dtype=torch.int32, device=dev)
+
+    def clock(fn):
+        fn()
+        ts, res = [], None
+        for _ in range(reps):
+            torch.cuda.synchronize(dev)
+            t0 = time.perf_counter()
+            res = fn()
+            torch.cuda.synchronize(dev)
+            ts.append(time.perf_counter() - t0)
+        return 1e3 * statistics.median(ts), res
+
+    lcp_ms, (lrs_len, lrs_pos) = clock(lambda: b.lcp(d_text, n, d_sa, d_lcp, stream=sptr))
+    check_ms, ok = clock(lambda: b.check(d_text, n, d_sa, stream=sptr))
+    del d_lcp
+    return {"lcp_ms": round(lcp_ms, 3), "lrs_len": lrs_len, "lrs_sa_pos": lrs_pos,
+            "check_ms": round(check_ms, 3), "check_ok": ok,
+            "check_bytes_per_suffix": 77,
+            "check_gbs": round(77 * n / (check_ms / 1e3) / 1e9, 1) if check_ms > 0 else None}
+
+
 def model_rounds(n: int, distinct, round_ms) -> list:
     """SURVEY.md 8(d)'s per-round model against the measured round times:
     B_j = n (3 rb + 2 S (P_j + 1)), P_j = ceil(2 w_j / 8), w_j = bit width
@@ -252,6 +283,7 @@ def run_single(a, torch, dev, world, rank, barrier):
                round1=a.round1)
     elapsed, stats = timed(a.steps, a.warmup, lambda: b.build(d_text, n, d_sa, **bkw), barrier)
     verified = b.check(d_text, n, d_sa, stream=sptr)
+    post = post_build(b, d_text, n, d_sa, sptr, torch, dev) if (world == 1 and not a.no_lcp) else None
     ref_sched = None
     if world == 1 and a.schedule == "packed" and not a.no_reference_schedule:
         ref_sched = reference_schedule(b, d_text, n, d_sa, sptr, a, torch, dev)
@@ -316,7 +348,17 @@ def run_single(a, torch, dev, world, rank, barrier):
         "init_chars": stats[-1]["init_chars"],
         "sigma": stats[-1]["sigma"],
         "sparse_ranks": stats[-1]["sparse_ranks"],
-        "model_bytes": stats[-1]["model_bytes"],
+        # SURVEY.md 8(d)'s byte model of the REFERENCE-shaped schedule (12-B
+        # records through P_j LSD passes per round) for this text: what the
+        # reference's algorithm would move, NOT the bytes of the packed
+        # schedule measured here (bytes_per_packed_round / build_roofline)
+        "reference_model_bytes": stats[-1]["reference_model_bytes"],
+        # the packed schedule's own algorithmic bytes per round (the kernels
+        # launched between the round's boundaries) and their rate over the
+        # round's HIP-event time
+        "bytes_per_packed_round": stats[-1]["round_bytes"],
+        "gbs_per_packed_round": [round(b / (ms / 1e3) / 1e9, 1) if ms > 0 else None
+                                 for b, ms in zip(stats[-1]["round_bytes"], round_ms)],
         "round1": stats[-1].get("round1"),
         "largest_window": stats[-1].get("largest_window"),
         "verified": verified,
@@ -324,6 +366,9 @@ def run_single(a, torch, dev, world, rank, barrier):
         "kernels_gbs": per_kernel,
         "kernels_ms_per_step": {k: round(v["ms"] / a.steps, 3) for k, v in kern.items()} if profile else None,
         "reference_schedule": ref_sched,
+        # the calls every reference caller makes after the build
+        # (main_sequential.c:108-120), timed outside `value`
+        "post_build": post,
         # the packed schedule's round 1 covers the reference's rounds h = 1 ..
         # K/2 at once, so its ms_per_round are not per doubling: the build's
         # time over the reference's own round count for this text

@@ -91,6 +91,7 @@ class SaStats(ctypes.Structure):
         ("kern_bytes", ctypes.c_uint64 * SA_K_COUNT),
         ("round1_segments", ctypes.c_int32),
         ("round1_layout", ctypes.c_int32),
+        ("round_bytes", ctypes.c_uint64 * SA_MAX_ROUNDS),
     ]
 
     def to_dict(self) -> dict:
@@ -115,7 +116,8 @@ class SaStats(ctypes.Structure):
                                 4: "striped-records-overflow"}.get(self.round1_segments, "exact"),
             "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2),
                               "xq": bool(self.round1_layout & 4)},
-            "model_bytes": int(self.model_bytes),
+            "reference_model_bytes": int(self.model_bytes),
+            "round_bytes": [int(x) for x in self.round_bytes[:r]],
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),
                             "bytes": int(self.kern_bytes[i])} for i, k in enumerate(KERNEL_KINDS)},
         }

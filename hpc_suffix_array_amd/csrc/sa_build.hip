@@ -34,8 +34,10 @@
 #endif
 
 #include "sa_bucket.h"
+#include "sa_check.h"
 #include "sa_kernels.h"
 #include "sa_lcp.h"
+#include "sa_limits.h"
 #include "sa_onesweep.h"
 #include "sa_permute.h"
 #include "sa_pivot.h"
@@ -62,6 +64,13 @@ static int set_err(int code, const char* fmt, ...) {
         if (e_ != hipSuccess)                                                                \
             return set_err(SA_E_HIP, "%s failed: %s (%s:%d)", #call, hipGetErrorString(e_),  \
                            __FILE__, __LINE__);                                              \
+    } while (0)
+
+// propagate a non-zero status (variadic: template arguments carry commas)
+#define SA_TRY(...)                      \
+    do {                                 \
+        const int rc_ = (__VA_ARGS__);   \
+        if (rc_) return rc_;             \
     } while (0)
 
 static bool trace_on() {
@@ -172,19 +181,26 @@ static uint64_t pad_elems(uint64_t n) {
     return (n >= (1ull << 26) && n <= (1ull << 31)) ? align_up(pad_capacity(n), 64) : m;
 }
 
-// Device memory a context holds for n symbols: rank + 2 key + 1 index buffer
-// (the reference schedule; keys[0] and the index buffer padded, pad_elems),
-// plus 7 u32 arrays for the unsorted set (packed).
-static uint64_t ws_bytes(uint64_t n) {
-    const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
-    return m * 4 + 2 * m * 8 + m * 4 + (pad_elems(n) - m) * 12 + 7 * m * 4 + m * 8 + m / 8 +
-           (uint64_t)kRadix * kMaxChunks * 4 + 8192;
-}
-
 // tile states for the widest digit (the bucketed first round's high pass
 // uses up to 10 bits)
 constexpr uint64_t kMaxRadix = 1024;
 static uint64_t tile_states_bytes(uint64_t n) { return ((n + kTile - 1) / kTile + 1) * kMaxRadix * 8; }
+
+// Device memory a context holds for n symbols: rank + 2 key + 1 index buffer
+// (the reference schedule; keys[0] and the index buffer padded, pad_elems),
+// plus 7 u32 arrays for the unsorted set (packed), keys_u with the per-XCD
+// regions' slack (ensure_u_capacity), the group starts of pivot rounds
+// (ensure_gs, 2 x (n/2 + 64) words) and the second pass's queue workspace
+// (sa_round1.h: xq_words(1024) + 1032 + 2 x 8 x 2^19 bucket-table words at
+// most) and the single-pass radix tile states.
+static uint64_t ws_bytes(uint64_t n) {
+    const uint64_t m = align_up(std::max<uint64_t>(n, 1), 64);
+    const uint64_t ku_slack = n >= (1ull << 26) ? n / 16 + 8ull * 1024 * kXqSlack + 64 : 0;
+    const uint64_t gs = 2 * (n / 2 + 64) * 4;
+    const uint64_t segx = (xq_words(1024) + 1032 + 2ull * kXq * (1ull << 19)) * 4;
+    return m * 4 + 2 * m * 8 + m * 4 + (pad_elems(n) - m) * 12 + 7 * m * 4 + (m + ku_slack) * 8 + m / 8 + gs +
+           segx + tile_states_bytes(n) + (uint64_t)kRadix * kMaxChunks * 4 + 8192;
+}
 
 static void free_ctx_buffers(sa_context* c) {
     hipFree(c->rank);
@@ -300,6 +316,16 @@ static int ensure_gs(sa_context* c, uint64_t n) {
     return SA_OK;
 }
 
+// ensure_gs for a path that has an alternative: false (the HIP error and
+// the message cleared) when the buffers cannot be allocated
+static bool gs_available(sa_context* c, uint64_t n) {
+    if (ensure_gs(c, n) == SA_OK) return true;
+    (void)hipGetLastError();
+    g_err.clear();
+    SA_TRACE("group-start buffers unavailable: pivot rounds without tied blocks");
+    return false;
+}
+
 // set i's group-start buffer when it holds an n-suffix build's groups
 static uint32_t* gs_buf(const sa_context* c, uint64_t n, int i) { return n <= c->gscap ? c->u_gs[i] : nullptr; }
 
@@ -326,8 +352,15 @@ struct Timer {
     // read when the build has finished (round_times), so no round waits for
     // the GPU to drain before the next one is launched
     int nr = 0;
+    uint64_t mark_bytes[kRoundEv] = {};   // the stats' algorithmic bytes at each boundary
     void round_mark() {
-        if (nr < kRoundEv) hipEventRecord(c->ev[kEvPool + nr], s);
+        if (nr < kRoundEv) {
+            hipEventRecord(c->ev[kEvPool + nr], s);
+            uint64_t b = 0;
+            if (st)
+                for (int k = 0; k < SA_K_COUNT; ++k) b += st->kern_bytes[k];
+            mark_bytes[nr] = b;
+        }
         ++nr;
     }
     void round_times() {
@@ -338,6 +371,7 @@ struct Timer {
             float ms = 0.f;
             hipEventElapsedTime(&ms, c->ev[kEvPool + r], c->ev[kEvPool + r + 1]);
             st->round_ms[r] = ms;
+            st->round_bytes[r] = mark_bytes[r + 1] - mark_bytes[r];
         }
     }
     void flush() {
@@ -656,7 +690,7 @@ static int blocks_per_cu(K kernel, int block) {
 // the pass's 8 queue tickets, next_hist = the next pass's per-queue counts;
 // the grid is whole XCDs (every queue served)
 template <class Src, bool PACKED, bool XQ = false>
-static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits, const uint32_t* base,
+static int lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, uint32_t nbits, const uint32_t* base,
                      uint32_t* ticket, uint64_t* ok, uint32_t* ov, hipStream_t s, uint32_t nshift, uint32_t nnbits,
                      uint32_t* next_hist, QDiv qd = QDiv{}, uint32_t tpq = 0) {
     const uint32_t epoch = next_epoch(c, s);
@@ -678,7 +712,9 @@ static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, 
     } while (0)
     if (nbits <= 8) SA_LSD_LAUNCH(8);
     else if (nbits == 9) SA_LSD_LAUNCH(9);
-    else if constexpr (PACKED || !XQ) SA_LSD_LAUNCH(10);   // (unpacked XQ passes: <= 9 bits, lsd_sort)
+    else if constexpr (PACKED || !XQ) SA_LSD_LAUNCH(10);
+    else   // unpacked XQ passes take <= 9 bits (lsd_xq_ok): a wider one would write nothing
+        return set_err(SA_E_INTERNAL, "unpacked per-XCD LSD pass of %u bits", nbits);
 #undef SA_LSD_LAUNCH
     if (SA_LSD_PROF) {
         unsigned long long h[5];
@@ -690,6 +726,7 @@ static void lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, 
                      (unsigned long long)n, nbits, (int)PACKED, tot / (double)tiles,
                      100 * h[0] / tot, 100 * h[1] / tot, 100 * h[2] / tot, 100 * h[3] / tot, 100 * h[4] / tot);
     }
+    return SA_OK;
 }
 
 // per-XCD queues of 8192-pair tiles (sa_lsd.h XQ): whether a sort takes
@@ -759,18 +796,19 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
             uint32_t* tk = qt + p * 8 * 32;
             if (p == 0) {
                 tm.begin(SA_K_SCATTER_FIRST);
-                lsd_pass<Src0, PACKED, true>(c, first, n, pl.shift[0], pl.bits[0], qb, tk, kb[0], vb[0], s, nsh, nnb,
-                                             nh, qd, tpq);
+                SA_TRY(lsd_pass<Src0, PACKED, true>(c, first, n, pl.shift[0], pl.bits[0], qb, tk, kb[0], vb[0], s, nsh,
+                                                    nnb, nh, qd, tpq));
                 tm.end();
                 add_bytes(st, SA_K_SCATTER_FIRST, (8 + pair) * n);
             } else {
                 tm.begin(SA_K_SCATTER_KEYS);
                 if constexpr (PACKED)
-                    lsd_pass<SrcItems, true, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], qb, tk,
-                                                   kb[p & 1], nullptr, s, nsh, nnb, nh, qd, tpq);
+                    SA_TRY(lsd_pass<SrcItems, true, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], qb,
+                                                          tk, kb[p & 1], nullptr, s, nsh, nnb, nh, qd, tpq));
                 else
-                    lsd_pass<SrcKeys, false, true>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p],
-                                                   pl.bits[p], qb, tk, kb[p & 1], vb[p & 1], s, nsh, nnb, nh, qd, tpq);
+                    SA_TRY(lsd_pass<SrcKeys, false, true>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p],
+                                                          pl.bits[p], qb, tk, kb[p & 1], vb[p & 1], s, nsh, nnb, nh,
+                                                          qd, tpq));
                 tm.end();
                 add_bytes(st, SA_K_SCATTER_KEYS, 2 * pair * n);
             }
@@ -797,18 +835,19 @@ static int lsd_sort(sa_context* c, const Src0& first, uint64_t n, const LsdPlan&
         uint32_t* nh = more ? lsd_ghist(c) + (p + 1) * kLsdMaxRadix : nullptr;
         if (p == 0) {
             tm.begin(SA_K_SCATTER_FIRST);
-            lsd_pass<Src0, PACKED>(c, first, n, pl.shift[0], pl.bits[0], base, lsd_tickets(c), kb[0], vb[0], s, nsh,
-                                   nnb, nh);
+            SA_TRY(lsd_pass<Src0, PACKED>(c, first, n, pl.shift[0], pl.bits[0], base, lsd_tickets(c), kb[0], vb[0], s,
+                                          nsh, nnb, nh));
             tm.end();
             add_bytes(st, SA_K_SCATTER_FIRST, (8 + pair) * n);
         } else {
             tm.begin(SA_K_SCATTER_KEYS);
             if constexpr (PACKED)
-                lsd_pass<SrcItems, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], base,
-                                         lsd_tickets(c) + p, kb[p & 1], nullptr, s, nsh, nnb, nh);
+                SA_TRY(lsd_pass<SrcItems, true>(c, SrcItems{kb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p], base,
+                                                lsd_tickets(c) + p, kb[p & 1], nullptr, s, nsh, nnb, nh));
             else
-                lsd_pass<SrcKeys, false>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p], pl.bits[p],
-                                         base, lsd_tickets(c) + p, kb[p & 1], vb[p & 1], s, nsh, nnb, nh);
+                SA_TRY(lsd_pass<SrcKeys, false>(c, SrcKeys{kb[(p - 1) & 1], vb[(p - 1) & 1]}, n, pl.shift[p],
+                                                pl.bits[p], base, lsd_tickets(c) + p, kb[p & 1], vb[p & 1], s, nsh,
+                                                nnb, nh));
             tm.end();
             add_bytes(st, SA_K_SCATTER_KEYS, 2 * pair * n);
         }
@@ -1115,7 +1154,11 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     const uint64_t scap = 2 * align_up(c->cap, 64);
     const uint64_t sbase = align_up(4 * G + 3, 64);
     const uint64_t ra_max = align_up(m / 2, 64);
-    const bool tied = !(c->dbg & SA_DEBUG_NO_TIED) && G <= kPivotTiedMaxG && sbase + 3 * ra_max <= scap;
+    // tied blocks write the next set's group starts: u_gs is allocated here,
+    // and a workspace too tight for it takes the split path (k_pivot_pass<2>,
+    // no extra memory) instead of failing the build
+    const bool tied = !(c->dbg & SA_DEBUG_NO_TIED) && G <= kPivotTiedMaxG && sbase + 3 * ra_max <= scap &&
+                      gs_available(c, n);
     uint32_t* const scr = reinterpret_cast<uint32_t*>(ukb0);
     const bool merged = SA_PIVOT_MERGED && tied && have_gs;
     uint32_t* const gs = merged ? c->u_gs[ui] : tied ? scr : c->u_pos[uo];   // G (+ 1) group starts
@@ -1174,9 +1217,8 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     uint32_t* const ridx = tied ? scr + sbase : c->u_idx[uo];
     uint64_t T = 0, Gt = 0, Dt = 0;
     if (tied) {
-        // the next set's group starts go with it (the next pivot round's MODE 1)
-        const int rg = ensure_gs(c, n);
-        if (rg) return rg;
+        // the next set's group starts go with it (the next pivot round's MODE 1;
+        // u_gs allocated by gs_available above)
         uint32_t* const toff = scr + 2 * G + 1;
         uint32_t* const tid = toff + G + 1;
         hipLaunchKernelGGL(k_pivot_tied_scan, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gP, Gu, toff, tid,
@@ -1291,10 +1333,9 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     // next set goes to u_*[0]), key buffers keys_u / keys[0]
     uint64_t* const rk = c->keys[0];
     uint32_t* const ridx = c->u_idx[1];
-    {
-        const int rg = ensure_gs(c, n);   // the set's group starts, for round 2's MODE 1
-        if (rg) return rg;
-    }
+    // the set's group starts, for round 2's MODE 1; without room for them
+    // round 1 keeps the LSD sort (*done = false: nothing written yet)
+    if (!gs_available(c, n)) return SA_OK;
     tm.begin(SA_K_PIVOT_WRITE);
     hipLaunchKernelGGL(k_pivot_gp, dim3(1), dim3(kBlock), 0, s, (const uint32_t*)gs, 1u, (const uint32_t*)cc, ch,
                        (const uint32_t*)c->totals, gP);
@@ -1651,58 +1692,78 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
 // ---------------------------------------------------------------------------
 // O(n) checker (replaces is_valid_suffix_array, manber_myers.c:184-202)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kBlock) void k_fill_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t v) {
-    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock)
-        p[i] = v;
+// bin shifts of a checker pass with sub-bins of 2^s2 (plan_perm's shape)
+static PermPlan plan_check(uint64_t n, uint32_t s2) {
+    PermPlan p;
+    const uint32_t lg = bit_width(n > 1 ? n - 1 : 1);
+    p.s2 = s2;
+    p.s1 = std::max<uint32_t>(s2, lg > 8 ? lg - 8 : 0);
+    p.nb1 = (uint32_t)((n + (1ull << p.s1) - 1) >> p.s1);
+    p.nsub = 1u << (p.s1 - p.s2);
+    p.tpb = (uint32_t)(((1ull << p.s1) + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems));
+    return p;
 }
 
-// isa[sa[r]] = r; flags bit0 = index out of range, bit1 = duplicate
-__global__ __launch_bounds__(kBlock) void k_check_isa(const uint32_t* __restrict__ sa, uint64_t n,
-                                                      uint32_t* __restrict__ isa, uint32_t* flags) {
-    uint32_t bad = 0;
-    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t x = sa[r];
-        if (x >= n) { bad |= 1u; continue; }
-        const uint32_t old = atomicExch(&isa[x], (uint32_t)r);
-        if (old != 0xFFFFFFFFu) bad |= 2u;
-    }
-    if (bad) atomicOr(flags, bad);
-}
-
-// adjacent pairs: text[a] < text[b], or equal and ISA[a+1] < ISA[b+1] (ISA[n] = -1)
-__global__ __launch_bounds__(kBlock) void k_check_pairs(const uint8_t* __restrict__ text,
-                                                        const uint32_t* __restrict__ sa, uint64_t n,
-                                                        const uint32_t* __restrict__ isa, uint32_t* flags) {
-    uint32_t bad = 0;
-    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x + 1; r < n; r += (uint64_t)gridDim.x * kBlock) {
-        const uint64_t a = sa[r - 1], b = sa[r];
-        const uint32_t ta = text[a], tb = text[b];
-        if (ta > tb) { bad |= 4u; continue; }
-        if (ta == tb) {
-            const int64_t ia = (a + 1 < n) ? (int64_t)isa[a + 1] : -1;
-            const int64_t ib = (b + 1 < n) ? (int64_t)isa[b + 1] : -1;
-            if (!(ia < ib)) bad |= 8u;
-        }
-    }
-    if (bad) atomicOr(flags, bad);
-}
-
+// sa_check.h: pass A (ISA' by permutation) and pass B (adjacent keys compared
+// in LDS per sorted sub-bin); one host sync at the end.  Workspace: ISA' in
+// rank, pairs in keys[0] / keys[1], cursors in hist, sub-bin end keys in
+// vals_alt.  Returns 1 valid, 0 invalid, < 0 an error.
 static int check_device(sa_context* c, const uint8_t* d_text, uint64_t n, const uint32_t* d_sa, hipStream_t s) {
     if (n == 0) return 1;
     if (n > 0xFFFFFFFFull) return set_err(SA_E_INVALID, "n too large");
+    if (!d_text || !d_sa) return set_err(SA_E_INVALID, "NULL device pointer");
     SA_HIP(hipSetDevice(c->device));
     int rc = ensure_capacity(c, n);
     if (rc) return rc;
     uint32_t* isa = c->rank;
-    const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 8192);
-    hipLaunchKernelGGL(k_fill_u32, dim3(grid), dim3(kBlock), 0, s, isa, n, 0xFFFFFFFFu);
-    SA_HIP(hipMemsetAsync(c->words + 3, 0, 4, s));
-    hipLaunchKernelGGL(k_check_isa, dim3(grid), dim3(kBlock), 0, s, d_sa, n, isa, c->words + 3);
-    hipLaunchKernelGGL(k_check_pairs, dim3(grid), dim3(kBlock), 0, s, d_text, d_sa, n, (const uint32_t*)isa,
-                       c->words + 3);
+    uint32_t* err = c->words + 3;
+    uint32_t* cur1 = c->hist;
+    uint32_t* cur2 = c->hist + 256;
+    uint64_t* pa = c->keys[0];
+    uint64_t* pb = c->keys[1];
+    uint64_t* ends = reinterpret_cast<uint64_t*>(c->vals_alt);
+    const uint64_t T = (uint64_t)kChkBlock * kChkItems;
+    const uint32_t tiles = (uint32_t)((n + T - 1) / T);
+    SA_HIP(hipMemsetAsync(err, 0, 4, s));
+    for (int pass = 0; pass < 2; ++pass) {
+        const PermPlan p = plan_check(n, pass ? kChkSubB : kChkSubA);
+        if (p.nb1 > 256 || p.nsub > kPermMaxSub || p.s1 > 24)
+            return set_err(SA_E_INTERNAL, "checker plan out of range (n=%llu)", (unsigned long long)n);
+        SA_HIP(hipMemsetAsync(c->hist, 0, (256ull + (uint64_t)p.nb1 * p.nsub) * 4, s));
+        if (pass == 0)
+            hipLaunchKernelGGL((k_chk_bin<kChkBlock, kChkItems, ChkSrcA>), dim3(tiles), dim3(kChkBlock), 0, s,
+                               ChkSrcA{d_sa}, n, p.s1, cur1, pa, err);
+        else
+            hipLaunchKernelGGL((k_chk_bin<kChkBlock, kChkItems, ChkSrcB>), dim3(tiles), dim3(kChkBlock), 0, s,
+                               ChkSrcB{isa, d_text}, n, p.s1, cur1, pa, err);
+        const uint64_t* placed = pa;
+        if (p.s1 > p.s2) {
+            const dim3 g((p.nb1 + 7) / 8 * 8 * p.tpb);
+            if (pass == 0)
+                hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems, 32, true>), g, dim3(kPermBlock), 0, s,
+                                   (const uint64_t*)pa, n, p.s1, p.s2, p.tpb, cur2, pb);
+            else
+                hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems, 40, true>), g, dim3(kPermBlock), 0, s,
+                                   (const uint64_t*)pa, n, p.s1, p.s2, p.tpb, cur2, pb);
+            placed = pb;
+        }
+        hipLaunchKernelGGL(k_chk_cursors, dim3((uint32_t)std::min<uint64_t>(((uint64_t)p.nb1 * (p.nsub + 1) + kBlock - 1) / kBlock, 1024)),
+                           dim3(kBlock), 0, s, (const uint32_t*)cur1, (const uint32_t*)cur2, n, p.s1, p.s2, p.nb1, err);
+        const uint64_t nsb = (n + (1ull << p.s2) - 1) >> p.s2;
+        if (pass == 0) {
+            hipLaunchKernelGGL((k_perm_place<kPermBlock, false, 1>), dim3((uint32_t)nsb), dim3(kPermBlock), 0, s, placed, n, isa,
+                               err);
+        } else {
+            hipLaunchKernelGGL((k_chk_place<kChkBlock>), dim3((uint32_t)nsb), dim3(kChkBlock), 0, s, placed, n, p.s1,
+                               ends, err);
+            hipLaunchKernelGGL(k_chk_tiles, dim3((uint32_t)std::min<uint64_t>((nsb + kBlock - 1) / kBlock, 1024)),
+                               dim3(kBlock), 0, s, (const uint64_t*)ends, nsb, err);
+        }
+    }
     SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words + 3, c->words + 3, 4, hipMemcpyDeviceToHost, s));
+    SA_HIP(hipMemcpyAsync(c->host_words + 3, err, 4, hipMemcpyDeviceToHost, s));
     SA_HIP(hipStreamSynchronize(s));
+    SA_TRACE("check: error bits %#x", c->host_words[3]);
     return c->host_words[3] == 0 ? 1 : 0;
 }
 

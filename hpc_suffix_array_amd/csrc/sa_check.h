@@ -1,0 +1,243 @@
+// sa_check.h -- the O(n) suffix-array checker (replaces is_valid_suffix_array,
+// manber_myers.c:184-202, which every caller runs after a build,
+// main_sequential.c:120) as two coalesced permutations.
+//
+// The reference compares each adjacent pair of sorted suffixes.  The same
+// verdict, in O(n):  SA is a permutation of 0..n-1, and for every r >= 1 with
+// a = SA[r-1], b = SA[r]:  (text[a], ISA[a+1]) < (text[b], ISA[b+1])
+// (ISA[n] = -1: the empty suffix is the smallest; equal first bytes are
+// ordered by the rest of the suffix, whose position ISA gives).
+//
+// As two random scatters / gathers over n-entry arrays (ISA[SA[r]] = r, then
+// ISA[SA[r] + 1] twice per r) that cost 111 ms at 1 GiB (r05: 38.7 and 358 GB
+// of traffic for ~24 GB of algorithmic bytes).  Here each random access is an
+// MSD permutation by destination, as the reference schedule's re-rank
+// (sa_permute.h): a level-1 pass bins (destination, value) pairs into <= 256
+// bins of 2^s1 destinations (the slots of bin b are known from b: the
+// destinations of a permutation are exactly [b 2^s1, (b+1) 2^s1)), a split
+// pass bins each bin again into sub-bins of 2^s2, and one workgroup per
+// sub-bin places its pairs in LDS and writes or checks them whole.
+//
+//   pass A  pairs (SA[r], r + 1), read sequentially from SA -> ISA'[x] = r + 1
+//           (k_perm_place, the re-rank's own placement: 0 = a hole).  SA is a
+//           permutation iff no SA[r] >= n, every bin and sub-bin cursor ends
+//           at its exact size, and no placed slot is a hole or out of place.
+//   pass B  pairs (ISA'[i] - 1, text[i], ISA'[i+1]) read sequentially (ISA'[n]
+//           = 0) -> at sorted position r = ISA[i] the key (text[SA[r]],
+//           ISA'[SA[r]+1]), placed in LDS per 2^13-entry sub-bin, where
+//           adjacent keys are compared in place; each sub-bin's first and
+//           last key go to a small table that k_chk_tiles compares across
+//           sub-bins.  Nothing else is written.
+//
+// Bytes per suffix: A 4 + 8, 8 + 8, 8 + 4; B 5 + 8, 8 + 8, 8 = 77 B, all
+// streamed (or runs of ~32 pairs), against ~24 B read at random before.
+// Error bits (err word): 1 SA entry >= n, 2 / 4 pass A pair out of place /
+// hole, 8 pass B pair out of place, 16 a cursor off its bin's size, 32 / 64
+// adjacent keys out of order inside / across sub-bins.
+#pragma once
+#include "sa_kernels.h"
+#include "sa_permute.h"
+
+namespace sa {
+
+constexpr uint32_t kChkSubA = kPermSub;   // pass A sub-bins: 2^14 u32 slots in LDS
+constexpr uint32_t kChkSubB = 13;         // pass B sub-bins: 2^13 u32 values + 2^13 text bytes
+constexpr int kChkBlock = 1024;
+constexpr int kChkItems = 8;
+
+// pass A source: element r -> destination SA[r], pair (SA[r] << 32 | r + 1)
+struct ChkSrcA {
+    const uint32_t* __restrict__ sa;
+    static constexpr int DSH = 32;
+    __device__ __forceinline__ uint64_t dest(uint64_t r, uint64_t n, uint32_t& bad) const {
+        const uint32_t x = sa[r];
+        if (x >= n) {
+            bad |= 1u;
+            return ~0ull;
+        }
+        return x;
+    }
+    __device__ __forceinline__ uint64_t pair(uint64_t r, uint64_t d, uint64_t, uint32_t) const {
+        return (d << 32) | (uint32_t)(r + 1);
+    }
+};
+
+// pass B source: element i -> destination ISA'[i] - 1, pair (destination's
+// low s1 bits << 40 | text[i] << 32 | ISA'[i + 1]) (s1 <= 24)
+struct ChkSrcB {
+    const uint32_t* __restrict__ isa;
+    const uint8_t* __restrict__ text;
+    static constexpr int DSH = 40;
+    __device__ __forceinline__ uint64_t dest(uint64_t i, uint64_t n, uint32_t& bad) const {
+        const uint32_t x = isa[i];
+        if (x == 0u || x > n) {   // (only after pass A failed)
+            bad |= 8u;
+            return ~0ull;
+        }
+        return x - 1u;
+    }
+    __device__ __forceinline__ uint64_t pair(uint64_t i, uint64_t d, uint64_t n, uint32_t s1) const {
+        const uint32_t nx = i + 1 < n ? isa[i + 1] : 0u;
+        return ((d & ((1ull << s1) - 1ull)) << 40) | ((uint64_t)text[i] << 32) | nx;
+    }
+};
+
+// Level 1: tile of BLOCK x ITEMS elements -> pairs staged in LDS by bin
+// (d >> s1), each bin's slots claimed from its cursor (one device-scope
+// atomic per tile and bin) and written as runs.  A slot at or past its bin's
+// size (a non-permutation) is dropped; the cursor test flags it.
+template <int BLOCK, int ITEMS, class Src>
+__global__ __launch_bounds__(BLOCK) void k_chk_bin(Src src, uint64_t n, uint32_t s1, uint32_t* __restrict__ cur,
+                                                    uint64_t* __restrict__ out, uint32_t* __restrict__ err) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int NB = 256;
+    static_assert(BLOCK >= NB, "one thread per bin");
+    __shared__ uint64_t s_pair[T];
+    __shared__ uint8_t s_bin[T];
+    __shared__ uint32_t s_cnt[NB];
+    __shared__ uint32_t s_start[NB + 1];
+    __shared__ uint32_t s_gofs[NB];
+    __shared__ uint32_t s_tmp[NB / kWave];
+    const uint32_t tid = threadIdx.x;
+    const uint64_t tb = (uint64_t)blockIdx.x * T;
+    if (tid < (uint32_t)NB) s_cnt[tid] = 0;
+    __syncthreads();
+    uint32_t bad = 0;
+    uint64_t d[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+        d[j] = e < n ? src.dest(e, n, bad) : ~0ull;
+    }
+    uint64_t p[ITEMS];
+    uint32_t slot[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+        p[j] = d[j] != ~0ull ? src.pair(e, d[j], n, s1) : 0ull;
+        slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
+    }
+    __syncthreads();
+    const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
+    const uint32_t st = perm_scan<NB>(cnt, s_tmp);
+    if (tid < (uint32_t)NB) {
+        s_start[tid] = st;
+        if (tid == NB - 1) s_start[NB] = st + cnt;
+        s_gofs[tid] = cnt ? atomicAdd(&cur[tid], cnt) : 0u;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j)
+        if (d[j] != ~0ull) {
+            const uint32_t b = (uint32_t)(d[j] >> s1);
+            const uint32_t q = s_start[b] + slot[j];
+            s_pair[q] = p[j];
+            s_bin[q] = (uint8_t)b;
+        }
+    __syncthreads();
+    const uint32_t tot = s_start[NB];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + tid;
+        if (q < tot) {
+            const uint32_t b = s_bin[q];
+            const uint64_t g = (uint64_t)s_gofs[b] + (q - s_start[b]);
+            const uint64_t b0 = (uint64_t)b << s1;
+            const uint64_t bsz = (n - b0) < (1ull << s1) ? n - b0 : (1ull << s1);
+            if (g < bsz) out[b0 + g] = s_pair[q];
+        }
+    }
+    if (bad) atomicOr(err, bad);
+}
+
+// every cursor at its bin's / sub-bin's exact size (else bit 16)
+__global__ __launch_bounds__(kBlock) void k_chk_cursors(const uint32_t* __restrict__ cur1,
+                                                        const uint32_t* __restrict__ cur2, uint64_t n, uint32_t s1,
+                                                        uint32_t s2, uint32_t nb1, uint32_t* __restrict__ err) {
+    const uint32_t nsub = 1u << (s1 - s2);
+    const uint64_t total = (uint64_t)nb1 * (s1 > s2 ? nsub + 1 : 1);
+    bool bad = false;
+    for (uint64_t k = (uint64_t)blockIdx.x * kBlock + threadIdx.x; k < total; k += (uint64_t)gridDim.x * kBlock) {
+        uint64_t lo, width;
+        uint32_t got;
+        if (k < nb1) {
+            lo = k << s1;
+            width = 1ull << s1;
+            got = cur1[k];
+        } else {
+            const uint64_t t = k - nb1;
+            lo = (t / nsub << s1) + ((t % nsub) << s2);
+            width = 1ull << s2;
+            got = cur2[t];
+        }
+        const uint64_t want = lo >= n ? 0 : (n - lo < width ? n - lo : width);
+        bad |= got != want;
+    }
+    if (bad) atomicOr(err, 16u);
+}
+
+// pass B level 3: one workgroup per 2^kChkSubB sorted positions.  The keys
+// (text[SA[r]] << 32 | ISA'[SA[r] + 1]) land in LDS by r; adjacent ones must
+// rise strictly (bit 32); the sub-bin's first and last key go to ends[2 sb],
+// ends[2 sb + 1] for k_chk_tiles.  A pair whose destination is not in this
+// sub-bin raises bit 8 (only after a failed pass A).
+template <int BLOCK>
+__global__ __launch_bounds__(BLOCK) void k_chk_place(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
+                                                      uint64_t* __restrict__ ends, uint32_t* __restrict__ err) {
+    constexpr uint32_t S = 1u << kChkSubB;
+    constexpr int ITEMS = S / BLOCK;
+    static_assert(ITEMS * BLOCK == (int)S, "whole sub-bins per workgroup");
+    __shared__ uint32_t s_v[S];
+    __shared__ uint8_t s_t[S];
+    const uint32_t sb = blockIdx.x;
+    const uint64_t base = (uint64_t)sb << kChkSubB;
+    const uint32_t valid = (uint32_t)((n - base) < (uint64_t)S ? (n - base) : (uint64_t)S);
+    const uint32_t rel = (uint32_t)(base & ((1ull << s1) - 1ull));   // the sub-bin's offset in its bin
+    uint64_t p[ITEMS];
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + threadIdx.x;
+        p[j] = in[base + (q < valid ? q : valid - 1)];
+    }
+    uint32_t bad = 0;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + threadIdx.x;
+        if (q < valid) {
+            const uint32_t dl = (uint32_t)(p[j] >> 40);
+            const uint32_t x = dl - rel;
+            if (x >= valid) {
+                bad |= 8u;
+                continue;
+            }
+            s_v[x] = (uint32_t)p[j];
+            s_t[x] = (uint8_t)(p[j] >> 32);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+        const uint32_t q = j * BLOCK + threadIdx.x;
+        if (q + 1 < valid) {
+            const uint64_t a = ((uint64_t)s_t[q] << 32) | s_v[q];
+            const uint64_t b = ((uint64_t)s_t[q + 1] << 32) | s_v[q + 1];
+            if (!(a < b)) bad |= 32u;
+        }
+    }
+    if (threadIdx.x == 0) {
+        ends[2 * (uint64_t)sb] = ((uint64_t)s_t[0] << 32) | s_v[0];
+        ends[2 * (uint64_t)sb + 1] = ((uint64_t)s_t[valid - 1] << 32) | s_v[valid - 1];
+    }
+    if (bad) atomicOr(err, bad);
+}
+
+// the last key of each sub-bin below the first key of the next (else bit 64)
+__global__ __launch_bounds__(kBlock) void k_chk_tiles(const uint64_t* __restrict__ ends, uint64_t nsb,
+                                                      uint32_t* __restrict__ err) {
+    bool bad = false;
+    for (uint64_t t = (uint64_t)blockIdx.x * kBlock + threadIdx.x; t + 1 < nsb; t += (uint64_t)gridDim.x * kBlock)
+        bad |= !(ends[2 * t + 1] < ends[2 * t + 2]);
+    if (bad) atomicOr(err, 64u);
+}
+
+}  // namespace sa

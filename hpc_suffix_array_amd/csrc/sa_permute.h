@@ -198,7 +198,12 @@ __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict_
 // where consecutive tiles' runs of a sub-bin meet (~8 pairs per sub-bin and
 // tile) -- one bin per XCD at a time instead of each bin's tiles dealt over
 // all eight.  grid = 8 ceil(nb1 / 8) tpb.
-template <int BLOCK, int ITEMS>
+// DSH: the pair's destination (absolute, or relative to its bin: only its
+// low s1 bits are read) sits at bit DSH (the checker's pass B packs a text
+// byte between it and the value, sa_check.h).  CLAMP: a slot past its
+// sub-bin (a non-permutation; the checker's cursor test flags it) is dropped
+// instead of written into the next sub-bin.
+template <int BLOCK, int ITEMS, int DSH = 32, bool CLAMP = false>
 __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
                                                        uint32_t s2, uint32_t tpb, uint32_t* __restrict__ cur,
                                                        uint64_t* __restrict__ out) {
@@ -231,7 +236,7 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
 #pragma unroll
     for (int j = 0; j < ITEMS; ++j) {
         const uint32_t q = j * BLOCK + tid;
-        sub[j] = q < valid ? ((uint32_t)(p[j] >> 32) >> s2) & (nsub - 1u) : NB;
+        sub[j] = q < valid ? ((uint32_t)(p[j] >> DSH) >> s2) & (nsub - 1u) : NB;
         slot[j] = sub[j] < (uint32_t)NB ? atomicAdd(&s_cnt[sub[j]], 1u) : 0u;
     }
     __syncthreads();
@@ -251,9 +256,14 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
         const uint32_t q = j * BLOCK + tid;
         if (q < valid) {
             const uint64_t v = s_pair[q];
-            const uint32_t sb = ((uint32_t)(v >> 32) >> s2) & (nsub - 1u);
+            const uint32_t sb = ((uint32_t)(v >> DSH) >> s2) & (nsub - 1u);
             const uint64_t g = (uint64_t)s_gofs[sb] + (q - s_start[sb]);
-            if (g < n) out[g] = v;
+            if (CLAMP) {
+                const uint64_t s0 = bin0 + ((uint64_t)sb << s2);
+                if (g < n && g < s0 + (1ull << s2)) out[g] = v;
+            } else if (g < n) {
+                out[g] = v;
+            }
         }
     }
 }
@@ -281,7 +291,8 @@ struct NextHist {
 // sub-bins (spb of them), whose positions lie in at most two queues of the
 // next round, counted in LDS (2 x 1024 words: two workgroups per CU still)
 // and added to the global counts once.
-template <int BLOCK, bool HIST = false>
+// TAG: 1 for the checker's pass A (sa_check.h), so profiles tell it apart
+template <int BLOCK, bool HIST = false, int TAG = 0>
 __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict__ in, uint64_t n,
                                                        uint32_t* __restrict__ rank, uint32_t* __restrict__ err,
                                                        NextHist nh = NextHist{}, uint32_t spb = 1) {

@@ -386,8 +386,11 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // fixed-span local sort (which loads a one-bucket window's 8 chunks), a
     // grid of whole XCDs, the regions' slack in keys_u (ensure_u_capacity:
     // 2^26 entries and up; one GPU or a rank's range)
+    // The regions' offsets are 32-bit (k_split_seg<.., XQ>, k_bucket_starts_xq,
+    // load_items_xq): the whole region space must stay below 2^32
+    static_assert(kXqQueues == kXq && kXqRegionSlack == kXqSlack, "sa_limits.h mirrors sa_split.h");
     const bool xq = SA_SEG_XQ && allow_xq && fast32 && c->cus % (int)kXq == 0 && !(c->dbg & SA_DEBUG_NO_XQ) &&
-                    c->kucap >= m + m / 16 + 8ull * 1024 * kXqSlack;
+                    c->kucap >= xq_region_space(m) && xq_offsets_fit(m);
     if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0);
     // XQ workspace: queue cursors / bases / claim counts / tickets, the digit
     // sub-region starts, the per-region chunk starts and counts per bucket

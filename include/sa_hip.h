@@ -127,7 +127,9 @@ typedef struct {
     int32_t sparse_ranks;                /* 1: round-1 ranks kept for unsorted suffixes only */
     int32_t round1;                      /* SA_ROUND1_LSD, _BUCKETED or _PIVOT: first round taken */
     int32_t largest_window;              /* bucketed round 1: largest window (suffixes) */
-    uint64_t model_bytes;                /* SURVEY.md 8(d) model, summed */
+    uint64_t model_bytes;                /* SURVEY.md 8(d)'s model of the REFERENCE-shaped schedule (12-B records
+                                            through P_j LSD passes per round), summed; not the bytes of the
+                                            packed schedule (round_bytes / kern_bytes are) */
     double kern_ms[SA_K_COUNT];          /* profile only */
     uint64_t kern_launches[SA_K_COUNT];  /* profile only */
     uint64_t kern_bytes[SA_K_COUNT];     /* algorithmic bytes moved per kind */
@@ -138,6 +140,8 @@ typedef struct {
     int32_t round1_layout;               /* bucketed round 1: bit 0 compact key1 low (BucketSpec.cmp),
                                             bit 1 packed 8-byte first-pass items (PK8), bit 2 the second
                                             pass by per-XCD queues and regions (XQ) */
+    uint64_t round_bytes[SA_MAX_ROUNDS]; /* algorithmic bytes of the kernels launched in round j (the kern_bytes
+                                            added between its boundaries; the schedule actually run) */
 } sa_stats;
 
 typedef struct sa_context sa_context;

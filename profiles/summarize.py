@@ -21,7 +21,14 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_pivot_pass<1", "pivot_count"), ("k_pivot_pass<2", "pivot_write"),
+KINDS = [("k_chk_bin<1024, 8, sa::ChkSrcA", "check_bin_a"), ("k_chk_bin<1024, 8, sa::ChkSrcB", "check_bin_b"),
+         ("k_perm_split<1024, 8, 32, true", "check_split_a"), ("k_perm_split<1024, 8, 40, true", "check_split_b"),
+         ("k_perm_place<1024, false, 1", "check_place_a"), ("k_chk_place", "check_place_b"),
+         ("k_chk_cursors", "check_small"), ("k_chk_tiles", "check_small"),
+         ("k_phi", "lcp_phi"), ("k_plcp_irreducible", "lcp_irreducible"), ("k_plcp_long", "lcp_long"),
+         ("k_plcp_settle", "lcp_long"), ("k_chunk_max", "lcp_scan"), ("k_scan_chunk_max", "lcp_scan"),
+         ("k_plcp_apply", "lcp_scan"), ("k_lcp_gather", "lcp_gather"),
+         ("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_pivot_pass<1", "pivot_count"), ("k_pivot_pass<2", "pivot_write"),
          ("k_pivot_pass<3", "pivot_write"), ("k_pivot_tied_scan", "pivot_write"),
          ("k_pivot_place", "pivot_place"), ("k_pivot_gp", "pivot_gp"), ("k_lsd_hist", "lsd_hist"),
          ("k_lsd_base", "lsd_base"), ("k_lsd<", "lsd"), ("k_perm_rank", "perm_rank"), ("k_perm_split", "perm_split"),
@@ -45,8 +52,7 @@ KINDS = [("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_
          ("k_global_hist", "global_hist"), ("k_digit_base", "digit_base"), ("k_alphabet", "alphabet"),
          ("k_heads", "heads"), ("k_scan_heads", "heads_scan"),
          ("k_rerank", "rerank"), ("k_seg_count", "seg_count"), ("k_seg_scan", "seg_scan"),
-         ("k_seg_write", "seg_write"), ("k_gen_text", "gen_text"),
-         ("k_check_isa", "check_isa"), ("k_check_pairs", "check_pairs"), ("k_fill_u32", "fill")]
+         ("k_seg_write", "seg_write"), ("k_gen_text", "gen_text")]
 
 
 def kind_of(name):

@@ -41,7 +41,11 @@ def test_library_loads_and_reports(sa_lib):
     L = sa_lib.lib()
     assert b"gfx950" in L.sa_version()
     assert L.sa_device_count() >= 0
-    assert L.sa_workspace_bytes(1 << 30) >= 24 * (1 << 30)  # rank + 2 keys + 1 index buffer
+    # rank + 2 keys + index buffer + the unsorted-set arrays, keys_u with the
+    # per-XCD regions' slack, pivot group starts, tile states: ~68 B/suffix
+    # at 1 GiB (DESIGN.md section 3 lists the buffers)
+    w = L.sa_workspace_bytes(1 << 30)
+    assert 66 * (1 << 30) <= w <= 80 * (1 << 30), w / (1 << 30)
 
 
 def test_code_object_targets_gfx950(sa_lib):

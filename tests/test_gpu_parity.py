@@ -287,6 +287,45 @@ def test_checker_detects_corruption(gpu, oracle):
     assert not check_suffix_array(t, oob)
 
 
+@pytest.mark.parametrize("n", [1, 2, 3, 100, 8191, 8192, 8193, 16383, 16384, 16385, 1 << 21, (1 << 22) + 5,
+                               5_000_011])
+def test_checker_permutation_passes(gpu, oracle, n):
+    """The permutation checker (sa_check.h) at sizes around its sub-bins
+    (2^13 / 2^14) and bins (one level up to 2^21 / 2^22, two above), against
+    corruptions placed inside a sub-bin, across a sub-bin boundary, at both
+    ends, and whole-array permutations that keep SA a permutation."""
+    from hpc_suffix_array_amd import check_suffix_array
+    rng = np.random.default_rng(n)
+    t = oracle.gen_text("dna" if n > 3 else "alnum", n, seed=n)
+    sa = oracle.sa_c(t)
+    assert check_suffix_array(t, sa)
+    if n == 1:
+        assert not check_suffix_array(t, np.array([1], np.uint32))
+        return
+    cases = {"swap_first": (0, 1), "swap_last": (n - 2, n - 1)}
+    for k in (8191, 8192, 16383, 16384):   # sub-bin boundaries of pass B / pass A
+        if k < n:
+            cases[f"swap_{k}"] = (k - 1, k)
+    for name, (i, j) in cases.items():
+        bad = sa.copy()
+        bad[[i, j]] = bad[[j, i]]
+        assert not check_suffix_array(t, bad), name
+    dup = sa.copy()
+    dup[rng.integers(0, n)] = dup[rng.integers(0, n)] if n > 2 else dup[0]
+    if not (dup == sa).all():
+        assert not check_suffix_array(t, dup)
+    oob = sa.copy()
+    oob[rng.integers(0, n)] = n + int(rng.integers(0, 1000))
+    assert not check_suffix_array(t, oob)
+    assert not check_suffix_array(t, sa[::-1].copy())
+    assert not check_suffix_array(t, np.arange(n, dtype=np.uint32)) or (sa == np.arange(n)).all()
+    if n > 64:
+        sh = sa.copy()
+        k = int(rng.integers(0, n - 32))
+        sh[k:k + 32] = rng.permutation(sh[k:k + 32])
+        assert check_suffix_array(t, sh) == (sh == sa).all()
+
+
 def test_device_builder_torch(gpu, oracle):
     """Device-resident path (what bench.py times), torch buffers in HBM."""
     import torch
