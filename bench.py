@@ -454,37 +454,40 @@ def distributed_summary(recs: list, n: int) -> dict:
 
 def run_distributed(a, torch, dev, world, rank, barrier):
     """One string over all ranks: the range-partitioned build
-    (hpc_suffix_array_amd/distributed.py; every rank holds the text, each
-    sorts the suffixes of its bucket range, rank look-ups cross xGMI by RCCL
-    all_to_all).  Per-phase times are HIP-event spans on the build stream."""
+    (hpc_suffix_array_amd/distributed.py).  Each rank starts a step from its
+    slice of the text only (rank r: text[r C, (r + 1) C), C = n / G), as
+    north_star partitions the string; the step gathers the text to every
+    rank (one RCCL all_gather, INSIDE the timed step -- the reference times
+    its text MPI_Bcast too, main_mpi.c:40-51), then each rank sorts the
+    suffixes of its bucket range from its text copy, rank look-ups crossing
+    xGMI by RCCL all_to_all between doubling rounds.  Per-phase times are HIP
+    events on the build stream."""
     import torch.distributed as dist
-    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa
+    from hpc_suffix_array_amd.distributed import DistributedSA, HipRangeOps, gather_sa, text_chunk
     n = a.n
-    ops = HipRangeOps(n, dev.index)
+    # the workspace of a build (range buffers, the gathered text) reserved
+    # once, as DeviceBuilder(n) does for one GPU -- not inside the first build
+    ops = HipRangeOps(n, dev.index, world=world)
     ops.profile = not a.no_profile   # round 1's per-kernel HIP events (sa_dist_round1 sa_stats)
     sptr = torch.cuda.current_stream(dev).cuda_stream
-    d_text = torch.empty(n, dtype=torch.uint8, device=dev)
+    C = text_chunk(n, world)
+    lo, hi = min(n, rank * C), min(n, (rank + 1) * C)
+    # this rank's slice of the seeded text: generated whole (same seed on
+    # every rank), sliced, the rest freed -- outside the timed region, as the
+    # single-GPU bench's text is generated in HBM before it
+    full = torch.empty(n, dtype=torch.uint8, device=dev)
     if a.kind == "degenerate":
-        d_text.fill_(ord("a"))
+        full.fill_(ord("a"))
     else:
-        ops.b.generate_text(d_text, n, ALPHABETS[a.kind], seed=a.seed, stream=sptr)   # same text on every rank
+        ops.b.generate_text(full, n, ALPHABETS[a.kind], seed=a.seed, stream=sptr)
+    d_slice = full[lo:hi].clone()
+    del full
     torch.cuda.synchronize(dev)
-    # the text replicated to every rank, as an RCCL broadcast from rank 0 would
-    # do it (reported, not part of the build: inputs are resident in HBM)
-    bcast_ms = None
-    if world > 1:
-        tmp = d_text.clone()
-        barrier()
-        t0 = time.perf_counter()
-        dist.broadcast(tmp, 0)
-        torch.cuda.synchronize(dev)
-        bcast_ms = 1e3 * (time.perf_counter() - t0)
-        del tmp
     holder = {}
 
     def step():
         d = DistributedSA(ops)
-        holder["sa"] = d.build(d_text, n)
+        holder["sa"] = d.build_sliced(d_slice, n)
         torch.cuda.synchronize(dev)
         return d.stats
 
@@ -497,6 +500,7 @@ def run_distributed(a, torch, dev, world, rank, barrier):
     else:
         recs = [rec]
     sa_local, sa_off = holder["sa"]
+    d_text = ops.textbuf[:n] if world > 1 else d_slice   # the text as the last build gathered it
     # verification: the full SA gathered to every rank, O(n) check on rank 0
     verified = None
     if n <= 0xFFFFFFFF:
@@ -514,10 +518,20 @@ def run_distributed(a, torch, dev, world, rank, barrier):
              "init_chars": st.get("K"), "sigma": st.get("sigma"), "bucket_bits": st.get("bucket_bits"),
              "path": st.get("path"),
              "phase_ms": {k: round(v, 3) for k, v in rec["phase_ms"].items()},
-             "text_broadcast_ms": round(bcast_ms, 3) if bcast_ms else None, "verified": verified,
-             "note": "range-partitioned build: each rank sorts the suffixes of its bucket range from its text "
-                     "copy; rank requests/answers by RCCL all_to_all between doubling rounds; roofline = the "
-                     "slowest rank's dominant round-1 kernel"}
+             # the text all_gather, part of every timed step (phase "text_gather")
+             "text_gather_ms": round(rec["phase_ms"].get("text_gather", 0.0), 3) if world > 1 else None,
+             "input_partition": f"rank r holds text[r*{C}, (r+1)*{C}) at the start of each step",
+             # per build, rank 0: collectives (RCCL calls, each all_to_all
+             # slice counted) and host waits (the driver's read-backs and
+             # libsa_hip's own stream syncs / blocking copies)
+             "collectives_per_build": st.get("collectives"),
+             "host_syncs_per_build": st.get("host_syncs"),
+             "host_syncs_driver_per_build": st.get("host_syncs_driver"),
+             "host_syncs_native_per_build": st.get("host_syncs_native"),
+             "verified": verified,
+             "note": "range-partitioned build from a range-partitioned string: the text all_gather, then each rank "
+                     "sorts the suffixes of its bucket range from its text copy; rank requests/answers by RCCL "
+                     "all_to_all between doubling rounds; roofline = the slowest rank's dominant round-1 kernel"}
     extra.update(summ)
     return elapsed, extra
 

@@ -36,9 +36,9 @@ EXT_SYMBOLS = ["sa_context_create", "sa_context_destroy", "sa_context_set_debug"
                "sa_alphabet_device", "sa_pack_keys_device", "sa_sort_pairs_device", "sa_scatter_u64_device",
                "sa_gather_u64_device", "sa_running_max_i64_device", "sa_inclusive_sum_i64_device",
                "sa_count_below_u64_device", "sa_select_u8_device",
-               "sa_dist_begin", "sa_dist_cuts", "sa_dist_plan_cuts", "sa_dist_release", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
+               "sa_dist_begin", "sa_dist_cuts", "sa_dist_plan_cuts", "sa_dist_reserve", "sa_dist_release", "sa_dist_round1", "sa_dist_req_count", "sa_dist_req_fill",
                "sa_dist_answer", "sa_dist_refine",
-               "sa_last_error", "sa_device_count", "sa_version", "sa_struct_size"]
+               "sa_last_error", "sa_host_syncs", "sa_device_count", "sa_version", "sa_struct_size"]
 
 
 class SAError(RuntimeError):
@@ -221,18 +221,22 @@ def lib() -> ctypes.CDLL:
     L.sa_dist_plan_cuts.argtypes = [i32, u64, i32, ctypes.POINTER(u64), ctypes.POINTER(ctypes.c_uint32),
                                     ctypes.POINTER(u64)]
     L.sa_dist_release.argtypes = [vp]
+    L.sa_dist_reserve.argtypes = [vp, u64, i32]
     L.sa_dist_round1.argtypes = [vp, vp, vp, DI, ctypes.POINTER(SaStats)]
     L.sa_dist_req_count.argtypes = [vp, u64, ctypes.POINTER(u64), vp, DI]
     L.sa_dist_req_fill.argtypes = [vp, u64, vp, vp]
     L.sa_dist_answer.argtypes = [vp, vp, u64, vp, vp]
     L.sa_dist_refine.argtypes = [vp, u64, vp, vp, vp, DI]
-    for f in (L.sa_dist_begin, L.sa_dist_cuts, L.sa_dist_plan_cuts, L.sa_dist_release, L.sa_dist_round1, L.sa_dist_req_count, L.sa_dist_req_fill,
+    for f in (L.sa_dist_begin, L.sa_dist_cuts, L.sa_dist_plan_cuts, L.sa_dist_reserve, L.sa_dist_release,
+              L.sa_dist_round1, L.sa_dist_req_count, L.sa_dist_req_fill,
               L.sa_dist_answer, L.sa_dist_refine):
         f.restype = i32
     L.sa_generate_text_device.argtypes = [vp, u64, u64, ctypes.c_char_p, ctypes.c_uint32, vp]
     L.sa_generate_text_device.restype = i32
     L.sa_last_error.argtypes = []
     L.sa_last_error.restype = ctypes.c_char_p
+    L.sa_host_syncs.argtypes = []
+    L.sa_host_syncs.restype = ctypes.c_uint64
     L.sa_device_count.argtypes = []
     L.sa_device_count.restype = i32
     L.sa_version.argtypes = []

@@ -66,6 +66,19 @@ static int set_err(int code, const char* fmt, ...) {
                            __FILE__, __LINE__);                                              \
     } while (0)
 
+// Every host wait of the library goes through these two (a stream sync, or
+// a blocking copy): sa_host_syncs() reports their count, so a driver can
+// show how many times a build stops the host (bench.py host_syncs_per_build).
+static std::atomic<uint64_t> g_host_syncs{0};
+static hipError_t host_sync(hipStream_t s) {
+    g_host_syncs.fetch_add(1, std::memory_order_relaxed);
+    return hipStreamSynchronize(s);
+}
+static hipError_t host_memcpy(void* dst, const void* src, size_t bytes, hipMemcpyKind kind) {
+    g_host_syncs.fetch_add(1, std::memory_order_relaxed);
+    return hipMemcpy(dst, src, bytes, kind);
+}
+
 // propagate a non-zero status (variadic: template arguments carry commas)
 #define SA_TRY(...)                      \
     do {                                 \
@@ -719,7 +732,7 @@ static int lsd_pass(sa_context* c, const Src& src, uint64_t n, uint32_t shift, u
     if (SA_LSD_PROF) {
         unsigned long long h[5];
         hipMemcpyAsync(h, prof, sizeof h, hipMemcpyDeviceToHost, s);
-        hipStreamSynchronize(s);
+        host_sync(s);
         double tot = 0;
         for (double x : h) tot += x;
         std::fprintf(stderr, "[lsd-prof] n=%llu bits=%u packed=%d clk/tile %.0f: rank %.1f%% scan %.1f%% lookback %.1f%% stage %.1f%% write %.1f%%\n",
@@ -879,7 +892,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     add_bytes(st, SA_K_ALPHABET, n);
     SA_HIP(hipMemcpyAsync(h_alpha, c->alpha, 8 * 4, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
@@ -959,7 +972,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         // (with the permutation re-rank's error word: the previous round's
         // placement is checked before this round's ranks are used)
         SA_HIP(hipMemcpyAsync(c->host_words, c->words, 4 * (kPermErrWord + 1), hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
         if (used_perm && c->host_words[kPermErrWord])
             return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix (flags %u)", c->host_words[kPermErrWord]);
@@ -1015,7 +1028,7 @@ static int build_reference(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     }
     if (used_perm) {
         SA_HIP(hipMemcpyAsync(c->host_words + kPermErrWord, c->words + kPermErrWord, 4, hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         if (c->host_words[kPermErrWord])
             return set_err(SA_E_INTERNAL, "re-rank permutation lost a suffix (flags %u)", c->host_words[kPermErrWord]);
     }
@@ -1098,7 +1111,7 @@ static int segments(sa_context* c, const uint64_t* keys, const uint32_t* idx, co
     tm.end();
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 20, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
     *D = c->host_words[0];
     *m = c->host_words[1];
@@ -1201,7 +1214,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
         add_bytes(st, SA_K_PIVOT_COUNT, 8 * m);
     }
     SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
     if (t0 + t1 + t2 != m) return set_err(SA_E_INTERNAL, "pivot classes %llu + %llu + %llu != %llu",
                                           (unsigned long long)t0, (unsigned long long)t1, (unsigned long long)t2,
@@ -1237,7 +1250,7 @@ static int pivot_round(sa_context* c, int ui, int uo, uint64_t n, uint64_t m, ui
     add_bytes(st, SA_K_PIVOT_WRITE, tied ? 12 * m + 16 * t1 + 12 * mr : 12 * m + 12 * m);
     if (tied) {
         SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         T = c->host_words[20];
         Gt = c->host_words[21];
         Dt = c->host_words[22];
@@ -1321,7 +1334,7 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_PIVOT_COUNT, 8 * n);
     SA_HIP(hipMemcpyAsync(c->host_words + 16, c->totals, 12, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     const uint64_t t0 = c->host_words[16], t1 = c->host_words[17], t2 = c->host_words[18];
     if (t0 + t1 + t2 != n) return set_err(SA_E_INTERNAL, "round-1 pivot classes %llu + %llu + %llu != %llu",
                                           (unsigned long long)t0, (unsigned long long)t1, (unsigned long long)t2,
@@ -1348,7 +1361,7 @@ static int pivot_round1(sa_context* c, uint64_t n, uint32_t bits1, uint32_t* d_s
     SA_HIP(hipGetLastError());
     add_bytes(st, SA_K_PIVOT_WRITE, 8 * n + 16 * t1 + 12 * mr);
     SA_HIP(hipMemcpyAsync(c->host_words + 20, c->totals + 4, 12, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     const uint64_t T = c->host_words[20], Gt = c->host_words[21], Dt = c->host_words[22];
     if (T > t1 || Gt > 1 || Dt > 1)
         return set_err(SA_E_INTERNAL, "round-1 tied block %llu / %llu / %llu out of range", (unsigned long long)T,
@@ -1398,7 +1411,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     const uint32_t tail_n = (uint32_t)std::min<uint64_t>(n, (uint64_t)kMaxK);
     uint8_t* h_tail = reinterpret_cast<uint8_t*>(c->host_words + 2048);
     SA_HIP(hipMemcpyAsync(h_tail, d_text + (n - tail_n), tail_n, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     uint32_t sigma = 0;
     for (int b = 0; b < 256; ++b) h_code[b] = ((h_alpha[b >> 5] >> (b & 31)) & 1u) ? (uint16_t)(++sigma) : 0;
     SA_HIP(hipMemcpyAsync(c->code, h_code, 256 * 2, hipMemcpyHostToDevice, s));
@@ -1571,7 +1584,7 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
             tm.end();
             SA_HIP(hipGetLastError());
             SA_HIP(hipMemcpyAsync(c->host_words + kUsFlagWord, c->words + kUsFlagWord, 4, hipMemcpyDeviceToHost, s));
-            SA_HIP(hipStreamSynchronize(s));
+            SA_HIP(host_sync(s));
             add_bytes(st, SA_K_SORT_U, 28 * m);
             if (c->host_words[kUsFlagWord] == 0) {
                 sorted = ukb0;
@@ -1762,7 +1775,7 @@ static int check_device(sa_context* c, const uint8_t* d_text, uint64_t n, const 
     }
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words + 3, err, 4, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     SA_TRACE("check: error bits %#x", c->host_words[3]);
     return c->host_words[3] == 0 ? 1 : 0;
 }
@@ -1811,7 +1824,7 @@ static int lcp_device(sa_context* c, const uint8_t* d_text, uint64_t n, const ui
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words + 8, best, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipMemcpyAsync(c->host_words + 16, cnt, (kLongRounds + 1) * 4, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     // every pair resolves by the last window (it reaches n); a pair left over is a bug
     uint64_t lo_end = kDirect;
     int rounds = 0;
@@ -1825,7 +1838,7 @@ static int lcp_device(sa_context* c, const uint8_t* d_text, uint64_t n, const ui
     if (len) {
         const uint64_t r = 0xFFFFFFFFull - (b & 0xFFFFFFFFull);
         uint32_t pos = 0;
-        SA_HIP(hipMemcpy(&pos, d_sa + r, 4, hipMemcpyDeviceToHost));
+        SA_HIP(host_memcpy(&pos, d_sa + r, 4, hipMemcpyDeviceToHost));
         if (lrs_len) *lrs_len = len;
         if (lrs_pos) *lrs_pos = pos;
     }
@@ -1929,7 +1942,7 @@ static int copy_h2d(void* d_dst, const void* h_src, size_t bytes, hipStream_t s)
         SA_HIP(hipMemcpyAsync((char*)d_dst + off, st.buf[b], len, hipMemcpyHostToDevice, s));
         SA_HIP(hipEventRecord(st.ev[b], s));
     }
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     return SA_OK;
 }
 
@@ -1939,7 +1952,7 @@ static int copy_d2h(void* h_dst, const uint32_t* d_src, uint64_t count, int widt
     if (count == 0) return SA_OK;
     if (width == 4 && (bytes <= kStageChunk || host_is_pinned(h_dst))) {
         SA_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         return SA_OK;
     }
     Staging st;
@@ -1992,6 +2005,8 @@ using namespace sa;
 extern "C" {
 
 const char* sa_last_error(void) { return g_err.c_str(); }
+
+uint64_t sa_host_syncs(void) { return g_host_syncs.load(std::memory_order_relaxed); }
 
 const char* sa_version(void) { return "sa_hip gfx950 " __DATE__; }
 
@@ -2132,7 +2147,7 @@ int sa_lcp(const uint8_t* text, uint64_t n, const void* sa, int sa_width, void* 
         return set_err(SA_E_NOMEM, "device allocation failed");
     }
     if (copy_h2d(d_text, text, n, nullptr) != SA_OK || copy_h2d(d_sa, src, n * 4, nullptr) != SA_OK ||
-        hipStreamSynchronize(nullptr) != hipSuccess)
+        host_sync(nullptr) != hipSuccess)
         rc = set_err(SA_E_HIP, "H2D copy failed: %s", g_err.c_str());
     // the checker rejects a non-permutation before PHI would scatter through it
     if (rc == SA_OK) {
@@ -2177,7 +2192,7 @@ int sa_build_ex(const uint8_t* text, uint64_t n, void* sa_out, int sa_width, con
     // with the DMA; sa_stats reports them apart from total_ms)
     auto t0 = std::chrono::steady_clock::now();
     rc = copy_h2d(d_text, text, n, s);
-    if (rc == SA_OK) SA_HIP(hipStreamSynchronize(s));
+    if (rc == SA_OK) SA_HIP(host_sync(s));
     auto t1 = std::chrono::steady_clock::now();
     const double h2d = std::chrono::duration<double, std::milli>(t1 - t0).count();
     if (rc == SA_OK) rc = build_device(c, d_text, n, d_sa, s, opts, stats);
@@ -2225,7 +2240,7 @@ int sa_scatter_u64_device(uint64_t* d_dst, uint64_t dst_n, const int64_t* d_idx,
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipFreeAsync(d_bad, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (bad) return set_err(SA_E_INVALID, "%llu scatter indices outside [%lld, %lld)", bad, (long long)base,
                             (long long)(base + (int64_t)dst_n));
     return SA_OK;
@@ -2260,7 +2275,7 @@ int sa_gather_u64_device(uint64_t* d_dst, const uint64_t* d_src, uint64_t src_n,
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(&bad, d_bad, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipFreeAsync(d_bad, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (bad) return set_err(SA_E_INVALID, "%llu gather indices outside [%lld, %lld)", bad, (long long)base,
                             (long long)(base + (int64_t)src_n));
     return SA_OK;
@@ -2463,7 +2478,7 @@ int sa_select_u8_device(const uint8_t* d_mask, uint64_t m, int64_t* d_out, uint6
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(&total, d_t + tiles, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipFreeAsync(d_t, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     *count = (uint64_t)total;
     return SA_OK;
 }
@@ -2482,7 +2497,7 @@ int sa_alphabet_device(const uint8_t* d_text, uint64_t n, uint32_t present_out[8
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(present_out, d_mask, 32, hipMemcpyDeviceToHost, s));
     SA_HIP(hipFreeAsync(d_mask, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     return SA_OK;
 }
 
@@ -2503,7 +2518,7 @@ int sa_pack_keys_device(sa_context* ctx, const uint8_t* d_text, uint64_t n, uint
     uint16_t* h_code = reinterpret_cast<uint16_t*>(ctx->host_words + 320);
     std::memcpy(h_code, code, 512);
     SA_HIP(hipMemcpyAsync(ctx->code, h_code, 512, hipMemcpyHostToDevice, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     uint64_t top = 1;
     for (uint32_t t = 1; t < K; ++t) top *= base;
     const Chunking ch = plan_chunks(hi - lo);
@@ -2538,7 +2553,7 @@ int sa_sort_pairs_device(sa_context* ctx, const uint64_t* d_keys_in, const uint3
     if (rc) return rc;
     if (sorted != d_keys_out) SA_HIP(hipMemcpyAsync(d_keys_out, sorted, m * 8, hipMemcpyDeviceToDevice, s));
     SA_HIP(hipMemcpyAsync(ctx->host_words, ctx->words, 20, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (ctx->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
     return SA_OK;
 }
@@ -2566,6 +2581,11 @@ int sa_dist_begin(sa_context* ctx, const uint8_t* d_text, uint64_t n, int world,
 int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info) {
     if (!ctx || !info) return set_err(SA_E_INVALID, "NULL argument");
     return dist_cuts(ctx, h_coarse, info);
+}
+
+int sa_dist_reserve(sa_context* ctx, uint64_t max_n, int world) {
+    if (!ctx) return set_err(SA_E_INVALID, "NULL argument");
+    return dist_reserve(ctx, max_n, world);
 }
 
 int sa_dist_release(sa_context* ctx) {
@@ -2644,7 +2664,7 @@ int sa_check(const uint8_t* text, uint64_t n, const void* sa, int sa_width) {
     }
     rc = SA_OK;
     if (copy_h2d(d_text, text, n, nullptr) != SA_OK || copy_h2d(d_sa, src, n * 4, nullptr) != SA_OK ||
-        hipStreamSynchronize(nullptr) != hipSuccess)
+        host_sync(nullptr) != hipSuccess)
         rc = set_err(SA_E_HIP, "H2D copy failed: %s", g_err.c_str());
     if (rc == SA_OK) rc = check_device(c, d_text, n, d_sa, nullptr);
     hipFree(d_text);

@@ -126,6 +126,23 @@ static int ensure_dist_n(sa_context* c, uint64_t n) {
     return SA_OK;
 }
 
+static int ensure_dist_m(sa_context* c, uint64_t m);
+
+// Everything a range build of up to max_n symbols over `world` ranks
+// allocates (the n-entry member map and its prefix, the range's workspace
+// for the largest range plan_cuts accepts: n/W + n/(2W) + 65536 suffixes),
+// ahead of the first build: the first 8-rank build spent 2.68 s in cuts
+// allocating it.
+static int dist_reserve(sa_context* c, uint64_t max_n, int world) {
+    if (world < 1 || world > kDistMaxWorld) return set_err(SA_E_INVALID, "world %d", world);
+    SA_HIP(hipSetDevice(c->device));
+    int rc = ensure_dist_n(c, max_n);
+    if (rc) return rc;
+    const uint64_t w = (uint64_t)world;
+    const uint64_t m = std::min<uint64_t>(max_n, max_n / w + max_n / (2 * w) + 65536);
+    return ensure_dist_m(c, std::max<uint64_t>(m, 1));
+}
+
 static int ensure_dist_m(sa_context* c, uint64_t m) {
     DistState* d = dist_of(c);
     int rc = ensure_capacity(c, m);
@@ -342,7 +359,7 @@ static int dist_begin(sa_context* c, const uint8_t* d_text, uint64_t n, int worl
     const uint32_t tail_n = (uint32_t)std::min<uint64_t>(n, (uint64_t)kMaxK);
     uint8_t* h_tail = reinterpret_cast<uint8_t*>(c->host_words + 2048);
     SA_HIP(hipMemcpyAsync(h_tail, d_text + (n - tail_n), tail_n, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     d->sigma = sigma;
     const uint32_t K = choose_chars(sigma, n, 0);
     info->sigma = (int32_t)sigma;
@@ -482,7 +499,7 @@ static int dist_cuts(sa_context* c, const uint64_t* h_coarse, sa_dist_info* info
     if (rc) return rc;
     rc = ensure_dist_m(c, std::max<uint64_t>(d->m, 1));
     if (rc) return rc;
-    SA_HIP(hipMemcpy(d->owner_tab, tab.data(), kCoarse * 2, hipMemcpyHostToDevice));
+    SA_HIP(host_memcpy(d->owner_tab, tab.data(), kCoarse * 2, hipMemcpyHostToDevice));
     return SA_OK;
 }
 
@@ -555,7 +572,7 @@ static int dist_req_count(sa_context* c, uint64_t h, uint64_t* h_counts, hipStre
         SA_HIP(hipGetLastError());
         uint32_t* hc = c->host_words + 1024;   // pinned scratch (W <= kDistMaxWorld)
         SA_HIP(hipMemcpyAsync(hc, d->cnt, W * 4, hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         for (int q = 0; q < W; ++q) {
             d->send[q] = hc[q];
             d->nsend += hc[q];
@@ -565,25 +582,29 @@ static int dist_req_count(sa_context* c, uint64_t h, uint64_t* h_counts, hipStre
     return SA_OK;
 }
 
+// the owners' first request slots: exclusive prefix of the per-owner counts
+// k_dist_owner left in cnt[0, W), into the fill cursors cnt[kDistMaxWorld ..]
+// (on the device: no host round trip, no wait)
+__global__ void k_dist_cursors(uint32_t* __restrict__ cnt, uint32_t W) {
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t q = 0; q < W; ++q) {
+            cnt[kDistMaxWorld + q] = run;
+            run += cnt[q];
+        }
+    }
+}
+
 static int dist_req_fill(sa_context* c, uint64_t h, uint32_t* d_req, hipStream_t s) {
     DistState* d = c->dist;
     if (!d) return set_err(SA_E_INVALID, "no distributed state");
     if (d->nsend == 0) return SA_OK;
     if (!d_req) return set_err(SA_E_INVALID, "NULL request buffer");
-    const int W = d->world;
-    uint32_t* hc = c->host_words + 1024;
-    uint64_t run = 0;
-    for (int q = 0; q < W; ++q) {
-        hc[q] = (uint32_t)run;
-        run += d->send[q];
-    }
-    SA_HIP(hipMemcpyAsync(d->cnt + kDistMaxWorld, hc, W * 4, hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(k_dist_cursors, dim3(1), dim3(64), 0, s, d->cnt, (uint32_t)d->world);
     const uint32_t grid = (uint32_t)std::min<uint64_t>((d->mu + kBlock - 1) / kBlock, 8192);
     hipLaunchKernelGGL(k_dist_fill, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)c->u_idx[d->uo], d->mu, h,
                        (const uint32_t*)d->owner, d->cnt + kDistMaxWorld, d_req, d->perm);
     SA_HIP(hipGetLastError());
-    // the cursor upload reads pinned scratch the next round rewrites
-    SA_HIP(hipStreamSynchronize(s));
     return SA_OK;
 }
 
@@ -609,7 +630,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
     // a request outside this rank's range (k_dist_answer) is a bug
     uint32_t* hc = c->host_words + 1024;
     SA_HIP(hipMemcpyAsync(hc, d->cnt + 2 * kDistMaxWorld, 4, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (hc[0]) return set_err(SA_E_INTERNAL, "rank request outside this rank's bucket range");
     if (d->mu == 0) {
         info->unsorted = 0;
@@ -654,7 +675,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
                            c->vals_u, c->words + kUsFlagWord);
         SA_HIP(hipGetLastError());
         SA_HIP(hipMemcpyAsync(c->host_words + kUsFlagWord, c->words + kUsFlagWord, 4, hipMemcpyDeviceToHost, s));
-        SA_HIP(hipStreamSynchronize(s));
+        SA_HIP(host_sync(s));
         if (c->host_words[kUsFlagWord] == 0) sorted = ukb0;
     }
     if (!sorted) {
@@ -673,7 +694,7 @@ static int dist_refine(sa_context* c, uint64_t h, const uint64_t* d_ans, uint32_
                       nullptr, &Du, &m2, &G2, d->crank, d->sa_off, RankMap{d->gmember, d->gprefix});
     if (rc) return rc;
     if (d->world == 1) {   // the local look-ups' range check (segments() synchronised the stream)
-        SA_HIP(hipMemcpy(hc, d->cnt + 2 * kDistMaxWorld, 4, hipMemcpyDeviceToHost));
+        SA_HIP(host_memcpy(hc, d->cnt + 2 * kDistMaxWorld, 4, hipMemcpyDeviceToHost));
         if (hc[0]) return set_err(SA_E_INTERNAL, "rank look-up outside the bucket range");
     }
     d->mu = m2;

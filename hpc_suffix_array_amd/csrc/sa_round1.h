@@ -333,7 +333,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             else SA_HIST_G(rgrid, false, 3, rcur);
             // an overflowed stripe dropped records: stop before any pass reads them
             SA_HIP(hipMemcpyAsync(c->host_words + 11, c->words + 11, 4, hipMemcpyDeviceToHost, s));
-            SA_HIP(hipStreamSynchronize(s));
+            SA_HIP(host_sync(s));
             if (c->host_words[11]) {
                 SA_TRACE("  bucketed round 1: a record stripe overflowed, again with the counting scan");
                 tm.end();
@@ -597,7 +597,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     add_bytes(st, SA_K_WINDOWS, 8 * nw);
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 48, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (c->host_words[4]) return set_err(SA_E_INTERNAL, "radix look-back did not complete");
     if (padded && c->host_words[11]) {   // a digit outgrew its sampled segment: exact totals
         SA_TRACE("  bucketed round 1: padded segment overflow, again with exact digit totals");
@@ -736,7 +736,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     tm.end();
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words, c->words, 44, hipMemcpyDeviceToHost, s));
-    SA_HIP(hipStreamSynchronize(s));
+    SA_HIP(host_sync(s));
     if (c->host_words[6]) {
         SA_TRACE("  bucketed round 1: local sort flags %u, full sort instead", c->host_words[6]);
         return SA_OK;

@@ -91,6 +91,33 @@ def _all_to_all_single(out: torch.Tensor, inp: torch.Tensor, rs=None, ss=None, g
         dist.all_to_all_single(out, inp, rs, ss, group=group)
 
 
+def _all_gather_into(out: torch.Tensor, inp: torch.Tensor, group=None) -> None:
+    """out = the ranks' equal-size inputs back to back, in rank order
+    (RCCL all_gather_into_tensor: no copy; gloo: rows of out)."""
+    G = dist.get_world_size(group)
+    if _staged(inp, group):
+        ho = torch.empty(out.shape, dtype=out.dtype)
+        dist.all_gather(list(ho.view(G, -1).unbind(0)), inp.cpu(), group=group)
+        out.copy_(ho)
+    elif dist.get_backend(group) == "gloo":
+        dist.all_gather(list(out.view(G, -1).unbind(0)), inp, group=group)
+    else:
+        dist.all_gather_into_tensor(out, inp, group=group)
+
+
+# bytes of text one all_gather moves in total at most: larger texts (configs[3],
+# 4 GiB) are gathered in pieces (a 2 GiB all_to_all_single returned garbage on
+# this ROCm stack, see alltoallv)
+TEXT_PIECE = 1 << 30
+
+
+def text_chunk(n: int, world: int) -> int:
+    """Symbols per rank of the input partition: rank r holds
+    text[r C, min(n, (r + 1) C)) with C = ceil(n / world) (n / world each when
+    it divides, as every bench size does)."""
+    return -(-n // world) if world > 0 else n
+
+
 def alltoallv(tensors: List[torch.Tensor], send: List[int], recv: Optional[List[int]] = None,
               group=None, slices: Optional[int] = None) -> Tuple[List[torch.Tensor], List[int]]:
     """all_to_all_v of each tensor (send[j] elements to rank j, in rank order).
@@ -160,7 +187,7 @@ class HipRangeOps:
     """One rank's local phases of the range-partitioned build on its GPU
     (include/sa_hip.h sa_dist_*; kernels in csrc/sa_dist.h)."""
 
-    def __init__(self, max_n: int, device: int):
+    def __init__(self, max_n: int, device: int, world: Optional[int] = None):
         from .builder import DeviceBuilder
         self.dev = torch.device("cuda", device)
         self.b = DeviceBuilder(0, device=device)
@@ -169,6 +196,15 @@ class HipRangeOps:
         self.coarse = torch.zeros(COARSE, dtype=I64, device=self.dev)
         self.round1_stats = N.SaStats()
         self.profile = False
+        self.textbuf = None
+        if world:   # everything a build allocates, ahead of the first one
+            N.check(self.L.sa_dist_reserve(self.b.ctx, max_n, world), "sa_dist_reserve")
+            # the gathered text: world equal chunks (DistributedSA.build_sliced)
+            self.textbuf = torch.empty(world * text_chunk(max_n, world), dtype=torch.uint8, device=self.dev)
+
+    def host_syncs(self) -> int:
+        """Host waits libsa_hip has made so far (sa_host_syncs)."""
+        return int(self.L.sa_host_syncs())
 
     def _s(self):
         return ctypes.c_void_p(torch.cuda.current_stream(self.dev).cuda_stream)
@@ -254,9 +290,25 @@ def _trace(*a):
 class DistributedSA:
     """Range-partitioned build over an initialised process group.
 
-    ``build(text, n)`` -> (sa_local, sa_off): this rank's slice of the SA,
-    SA positions [sa_off, sa_off + len(sa_local)) (uint32 values stored as
-    int32 by the HIP path; int64 from the sample-sort fallback)."""
+    ``build_sliced(text_slice, n)`` -> (sa_local, sa_off): the input as
+    north_star partitions it -- rank r holds only text[r C, (r + 1) C) (C =
+    text_chunk(n, G)) -- gathered to every rank by one RCCL all_gather (part
+    of the build, as the reference times its text MPI_Bcast,
+    main_mpi.c:40-51), then the build.  ``build(text, n)`` starts from the
+    whole text on every rank.  sa_local is this rank's slice of the SA, SA
+    positions [sa_off, sa_off + len(sa_local)) (uint32 values stored as
+    int32 by the HIP path; int64 from the sample-sort fallback).
+
+    Failure agreement rides on the collectives the build needs anyway: a
+    phase that raises on one rank (a libsa_hip SAError -- NOMEM, a request
+    outside the range --, a torch OOM, ...) is recorded, the rank carries on
+    with placeholder buffers of the agreed sizes, and its error flag travels
+    in the next all_reduce / all_gather of the build (the alphabet flags, the
+    coarse histogram, the per-round count rows), where every rank raises --
+    no extra collective or host wait per phase.  So are the range plan's
+    fallback decisions (unbalanced cuts, a window over the LDS tile).
+    stats: "collectives" and "host_syncs" per build (the driver's reads of
+    device data and blocking uploads, plus libsa_hip's own waits)."""
 
     def __init__(self, ops, group=None):
         self.ops = ops
@@ -277,118 +329,242 @@ class DistributedSA:
         out = {}
         if len(self._events) > 1:
             self._events[-1][1].synchronize()
+            self._syncs += 1
             for (a, ea), (_, eb) in zip(self._events, self._events[1:]):
                 out[a] = round(out.get(a, 0.0) + ea.elapsed_time(eb), 4)
         return out
 
-    def _phase(self, name: str, dev, fn, *args):
-        """Run one native phase and agree on its outcome: an error on one rank
-        (a libsa_hip SAError -- NOMEM, a request outside the range --, a
-        torch OOM, a binding error, ...) makes EVERY rank raise here, instead
-        of leaving the others blocked in the next collective until its
-        timeout (one all_reduce MAX per phase, G > 1); the failing rank
-        re-raises its own exception."""
-        err, res = None, None
+    # -- failure agreement and counting --------------------------------------
+    def _run(self, name: str, fn, *args, default=None):
+        """One local phase; at G > 1 an exception is recorded (raised at the
+        next agreement point) and `default` stands in for the result."""
         try:
-            res = fn(*args)
+            return fn(*args)
         except Exception as e:   # noqa: BLE001 -- agreed on, then re-raised
-            err = e
-        if self.G > 1:
-            t = torch.tensor([1 if err is not None else 0], dtype=I64, device=dev)
-            _all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)
-            if int(t.item()) and err is None:
-                raise N.SAError(f"sa_dist {name}: failed on another rank")
-        if err is not None:
-            raise err
-        return res
+            if self.G == 1:
+                raise
+            if self._err is None:
+                self._err = (name, e)
+            _trace("phase failed", name, e)
+            return default() if callable(default) else default
 
-    def _min_all(self, x: int, dev) -> int:
-        if self.G == 1:
-            return int(x)
-        t = torch.tensor([int(x)], dtype=I64, device=dev)
-        _all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-        return int(t.item())
+    def _raise_agreed(self, flagged: bool) -> None:
+        """An agreement point: some rank flagged an error -> every rank raises
+        (the failing rank its own exception)."""
+        if self._err is not None:
+            raise self._err[1]
+        if flagged:
+            raise N.SAError("sa_dist: a phase failed on another rank")
+
+    def _coll(self, fn, *args, **kw):
+        self._ncoll += 1
+        return fn(*args, **kw)
+
+    def _to_host(self, t: torch.Tensor) -> List:
+        self._syncs += 1   # a device read-back on the GPU (counted on CPU too: the same program points)
+        return t.cpu().tolist()
+
+    @staticmethod
+    def _upload(vals: List[int], dev, dtype=I64) -> torch.Tensor:
+        """A small row on the device through a pinned host buffer, without a
+        host wait (torch keeps the buffer until the copy has run)."""
+        if dev.type != "cuda":
+            return torch.tensor(vals, dtype=dtype)
+        return torch.tensor(vals, dtype=dtype).pin_memory().to(dev, non_blocking=True)
+
+    def _reset(self) -> None:
+        self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": [], "cross_requests": []}
+        self._events = []
+        self._err = None
+        self._ncoll = 0
+        self._syncs = 0
+        self._native0 = self.ops.host_syncs() if hasattr(self.ops, "host_syncs") else 0
+
+    def _finish(self) -> None:
+        native = (self.ops.host_syncs() - self._native0) if hasattr(self.ops, "host_syncs") else 0
+        self.stats["collectives"] = self._ncoll
+        self.stats["host_syncs_driver"] = self._syncs
+        self.stats["host_syncs_native"] = native
+        self.stats["host_syncs"] = self._syncs + native
+
+    # -- the input partition ----------------------------------------------------
+    def gather_text(self, text_slice: torch.Tensor, n: int, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """The whole text on every rank from the ranks' slices (rank r:
+        text[r C, min(n, (r + 1) C)), C = text_chunk(n, G)) by all_gather into
+        `out` (>= G C bytes; allocated when None); slices of more than
+        TEXT_PIECE / G bytes are gathered piecewise."""
+        G, r = self.G, self.r
+        C = text_chunk(n, G)
+        want = min(n, (r + 1) * C) - min(n, r * C)
+        if text_slice.numel() != want:
+            raise ValueError(f"rank {r} holds {text_slice.numel()} symbols, the partition gives it {want}")
+        if G == 1:
+            return text_slice
+        dev = text_slice.device
+        if out is None or out.numel() < G * C:
+            out = torch.empty(G * C, dtype=torch.uint8, device=dev)
+        P = max(1, TEXT_PIECE // G)
+        if C <= P:
+            send = text_slice
+            if want < C:   # the last ranks' short slices, padded
+                send = torch.zeros(C, dtype=torch.uint8, device=dev)
+                send[:want] = text_slice
+            self._coll(_all_gather_into, out[: G * C], send, self.group)
+            return out[:n]
+        view = out[: G * C].view(G, C)
+        for a in range(0, C, P):
+            b = min(C, a + P)
+            send = torch.zeros(b - a, dtype=torch.uint8, device=dev)
+            e = min(b, want)
+            if e > a:
+                send[: e - a] = text_slice[a:e]
+            got = torch.empty(G * (b - a), dtype=torch.uint8, device=dev)
+            self._coll(_all_gather_into, got, send, self.group)
+            view[:, a:b] = got.view(G, b - a)
+        return out[:n]
+
+    def build_sliced(self, text_slice: torch.Tensor, n: int, out: Optional[torch.Tensor] = None):
+        self._reset()
+        dev = text_slice.device
+        self._mark("text_gather", dev)
+        text = self.gather_text(text_slice, n, out if out is not None else getattr(self.ops, "textbuf", None))
+        return self._build(text, n)
 
     def build(self, text: torch.Tensor, n: int):
+        self._reset()
+        return self._build(text, n)
+
+    # -- the build ----------------------------------------------------------------
+    def _build(self, text: torch.Tensor, n: int):
         G, r = self.G, self.r
         dev = text.device
         lo, hi = n * r // G, n * (r + 1) // G
-        self.stats = {"path": "range", "rounds": 0, "unsorted": [], "requests": [], "cross_requests": []}
-        self._events = []
         self._mark("alphabet", dev)
         # alphabet of the whole text: OR of the slices' masks (MAX of flags;
-        # the NCCL backend has no bitwise-or reduction)
+        # the NCCL backend has no bitwise-or reduction); flag 256 = an error
         _trace("alphabet", r, G, n)
-        words = self.ops.alphabet(text[lo:hi])
-        flags = torch.tensor([(words[b >> 5] >> (b & 31)) & 1 for b in range(256)], dtype=I32, device=dev)
+        words = self._run("alphabet", self.ops.alphabet, text[lo:hi], default=[0] * 8)
+        flags = self._upload([(words[b >> 5] >> (b & 31)) & 1 for b in range(256)] + [1 if self._err else 0], dev,
+                             I32)
         if G > 1:
-            _all_reduce(flags, op=dist.ReduceOp.MAX, group=self.group)
-        present = _present_words(flags.tolist())
+            self._coll(_all_reduce, flags, op=dist.ReduceOp.MAX, group=self.group)
+        fl = self._to_host(flags)
+        self._raise_agreed(bool(fl[256]))
+        present = _present_words(fl[:256])
         if n < 2:
             return self._fallback(text, n, "n < 2")
         _trace("begin")
         self._mark("begin", dev)
-        info, coarse = self._phase("begin", dev, self.ops.begin, text, n, G, r, present)
+        res = self._run("begin", self.ops.begin, text, n, G, r, present)
+        info, coarse = res if res is not None else (None, None)
+        ch = None
+        if G > 1:
+            # the coarse histograms summed, with the begin phase's error flag
+            self._mark("coarse_allreduce", dev)
+            agg = torch.zeros(COARSE + 1, dtype=I64, device=dev)
+            if coarse is not None:
+                agg[:COARSE] = coarse.to(dev)
+            if self._err is not None:
+                agg[COARSE] = 1
+            self._coll(_all_reduce, agg, group=self.group)
+            self._syncs += 1
+            ch = agg.cpu()
+            self._raise_agreed(bool(ch[COARSE]))
+            ch = ch[:COARSE]
         self.stats.update(sigma=info["sigma"], K=info["K"], bucket_bits=info["bucket_bits"])
         if info["status"] != N.DIST_OK:   # identical on every rank (global alphabet and n)
             return self._fallback(text, n, "unsupported alphabet / size")
-        ch = None
-        if G > 1:
-            self._mark("coarse_allreduce", dev)
-            _all_reduce(coarse, group=self.group)
-            ch = coarse.cpu()
         _trace("cuts")
-        self._mark("cuts", dev)   # the cut plan and the range's workspace (first build: allocation)
-        info = self._phase("cuts", dev, self.ops.cuts, ch)
-        _trace("cut", info)
-        self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
-        if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
-            return self._fallback(text, n, "unbalanced bucket ranges")
-        self._mark("sa_local", dev)
-        sa_local = self._phase("sa_local", dev, self.ops.empty, info["m"], I32)
-        self._mark("round1", dev)
-        info = self._phase("round1", dev, self.ops.round1, sa_local)
-        _trace("round1", info)
-        if self._min_all(info["round1_ok"], dev) == 0:
-            return self._fallback(text, n, "a bucket window exceeds the LDS tile")
-        sa_off = info["sa_off"] if "sa_off" in info else self.stats["sa_off"]
+        self._mark("cuts", dev)   # the cut plan (the workspace: reserved by HipRangeOps(max_n, device, world))
+        info = self._run("cuts", self.ops.cuts, ch)
+        fallback = None
+        sa_local = None
+        if info is not None:
+            _trace("cut", info)
+            self.stats.update(m=info["m"], sa_off=info["sa_off"], m_max=info["m_max"])
+            if info["status"] != N.DIST_OK:   # identical on every rank (same global histogram)
+                fallback = "unbalanced bucket ranges"
+            else:
+                self._mark("sa_local", dev)
+                sa_local = self._run("sa_local", self.ops.empty, info["m"], I32)
+                if sa_local is not None:
+                    self._mark("round1", dev)
+                    info = self._run("round1", self.ops.round1, sa_local)
+                    _trace("round1", info)
+                    if info is not None and info["round1_ok"] == 0:
+                        fallback = "a bucket window exceeds the LDS tile"
         self.stats["rounds"] = 1
-        self.stats["heads_round1"] = info["heads"]
-        h = self.stats["K"]
+        if info is not None and "heads" in info:
+            self.stats["heads_round1"] = info["heads"]
+        h = self.stats.get("K") or 1
+        first = True
         while True:
+            # the round's one agreement point: every rank's [error, fallback,
+            # unsorted, requests per owner], gathered by all ranks
             self._mark("requests", dev)
-            counts, info = self._phase("req_count", dev, self.ops.req_count, h, G)
+            counts, uns = [0] * G, 0
+            if self._err is None and fallback is None:
+                res = self._run("req_count", self.ops.req_count, h, G)
+                if res is not None:
+                    counts, info = res
+                    uns = info["unsorted"]
             _trace("req_count", h, counts)
-            mat = _all_gather_rows(torch.tensor([info["unsorted"]] + counts, dtype=I64, device=dev), self.group)
-            total_u = sum(row[0] for row in mat)
+            row = [1 if self._err else 0, 1 if fallback else 0, uns] + counts
+            mat = self._gather_rows(self._upload(row, dev))
+            self._raise_agreed(any(x[0] for x in mat))
+            if any(x[1] for x in mat):
+                if not first:
+                    raise RuntimeError("sa_dist: fallback requested after round 1")
+                return self._fallback(text, n, fallback or "a bucket window exceeds the LDS tile on another rank")
+            first = False
+            total_u = sum(x[2] for x in mat)
             self.stats["unsorted"].append(total_u)
             if total_u == 0:
                 break
             if h >= 2 * n:
                 raise RuntimeError("distributed doubling did not converge")
-            recv_counts = [row[1 + r] for row in mat]
-            self.stats["requests"].append(sum(sum(row[1:]) for row in mat))
+            recv_counts = [x[3 + r] for x in mat]
+            self.stats["requests"].append(sum(sum(x[3:]) for x in mat))
             # look-ups answered by another rank (they cross xGMI under RCCL)
-            self.stats["cross_requests"].append(sum(row[1 + q] for p, row in enumerate(mat) for q in range(G) if q != p))
+            self.stats["cross_requests"].append(sum(x[3 + q] for p, x in enumerate(mat) for q in range(G) if q != p))
             # every rank holds the whole count matrix: the slice count of both
             # exchanges needs no extra collective
-            slices = max([0] + [(x + XCHUNK - 1) // XCHUNK for row in mat for x in row[1:]])
-            req = self._phase("req_fill", dev, self.ops.req_fill, h, sum(counts))
+            slices = max([0] + [(y + XCHUNK - 1) // XCHUNK for x in mat for y in x[3:]])
+            nreq = sum(counts)
+            req = self._run("req_fill", self.ops.req_fill, h, nreq,
+                            default=lambda: torch.zeros(nreq, dtype=I32, device=dev))
             self._mark("exchange", dev)
-            (got,), _ = alltoallv([req], counts, recv_counts, self.group, slices)
+            (got,), _ = self._alltoallv([req], counts, recv_counts, slices)
             _trace("requests in", got.numel())
             self._mark("answer", dev)
-            ans = self._phase("answer", dev, self.ops.answer, got)
+            ans = self._run("answer", self.ops.answer, got,
+                            default=lambda: torch.zeros(got.numel(), dtype=I64, device=dev))
             self._mark("exchange", dev)
-            (back,), _ = alltoallv([ans], recv_counts, counts, self.group, slices)
+            (back,), _ = self._alltoallv([ans], recv_counts, counts, slices)
             self._mark("refine", dev)
-            self._phase("refine", dev, self.ops.refine, h, back, sa_local)
+            if self._err is None:
+                self._run("refine", self.ops.refine, h, back, sa_local)
             _trace("refined", h)
             self.stats["rounds"] += 1
             h *= 2
         self._mark("end", dev)
         self.stats["phase_ms"] = self._phase_ms()
+        self._finish()
         return sa_local, self.stats["sa_off"]
+
+    def _gather_rows(self, row: torch.Tensor) -> List[List[int]]:
+        if self.G == 1:
+            return [self._to_host(row)]
+        out = [torch.empty_like(row) for _ in range(self.G)]
+        self._coll(_all_gather, out, row.contiguous(), group=self.group)
+        return self._to_host(torch.stack(out))
+
+    def _alltoallv(self, tensors, send, recv, slices):
+        if self.G == 1:
+            return list(tensors), list(send)
+        T = max(1, int(slices))
+        self._ncoll += T * len(tensors)
+        return alltoallv(tensors, send, recv, self.group, slices)
 
     def _fallback(self, text, n, why):
         self.stats["path"] = "sample-sort"
@@ -398,6 +574,7 @@ class DistributedSA:
         sa = d.build(text, n)
         self.stats.update(d.stats)
         self.stats["path"] = "sample-sort"
+        self._finish()
         return sa, n * self.r // self.G
 
 

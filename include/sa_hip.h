@@ -277,6 +277,10 @@ int sa_dist_cuts(sa_context* ctx, const uint64_t* h_coarse, sa_dist_info* info);
 /* Frees the range-partitioned build's per-rank buffers of ctx (rank and
  * member arrays, request buffers); the context stays usable (a fallback
  * driver reuses its workspace).  Synchronises the device first. */
+/* Allocate ahead of the first build everything a range build of up to
+ * max_n symbols over `world` ranks needs (sa_dist_cuts would otherwise do it
+ * inside the first build). */
+int sa_dist_reserve(sa_context* ctx, uint64_t max_n, int world);
 int sa_dist_release(sa_context* ctx);
 /* The cut plan sa_dist_cuts applies (host only, no device): world + 1 cuts
  * into the 4096 coarse buckets of h_coarse (summing to n) at bucket width
@@ -308,6 +312,10 @@ const char* sa_last_error(void);
 int sa_device_count(void);
 /* library build identification, e.g. "sa_hip gfx950 <date>" */
 const char* sa_version(void);
+/* Host waits (stream synchronisations and blocking copies) the library has
+ * made in this process so far; a driver differences it around a build. */
+uint64_t sa_host_syncs(void);
+
 /* sizeof(sa_stats) (which = 0) / sizeof(sa_opts) (which = 1), for bindings */
 uint64_t sa_struct_size(int which);
 

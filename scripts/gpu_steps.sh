@@ -9,6 +9,7 @@
 #   smoke        __graft_entry__.smoke()
 #   bench        bench.py (1 GiB DNA, CPU baseline, reference schedule)
 #   bench_quick  bench.py without the CPU baseline and the reference schedule
+#   dist1        bench.py --mode distributed (the range-partitioned driver at N = 1)
 #   degenerate   bench.py --kind degenerate
 #   kinds        bench.py for alnum / ascii127 / byte256
 
@@ -35,6 +36,7 @@ for s in "$@"; do
     smoke) run 120 smoke.log python -u -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run 300 bench_dna1g.log python -u bench.py ;;
     bench_quick) run 200 bench_quick.log python -u bench.py --no-cpu-baseline --no-reference-schedule ;;
+    dist1) run 300 bench_dist1.log python -u bench.py --mode distributed --no-cpu-baseline ;;
     degenerate) run 300 bench_degenerate1g.log python -u bench.py --kind degenerate --no-cpu-baseline --no-reference-schedule ;;
     kinds) for k in alnum ascii127 byte256; do
                run 200 bench_$k.log python -u bench.py --kind $k --no-cpu-baseline --no-reference-schedule

@@ -37,7 +37,7 @@ def _texts():
     }
 
 
-def _worker(rank, world, port, q, chunks=None, driver="range"):
+def _worker(rank, world, port, q, chunks=None, driver="range", piece=None):
     import sys
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -49,6 +49,8 @@ def _worker(rank, world, port, q, chunks=None, driver="range"):
     from hpc_suffix_array_amd.distributed import DistributedSA, SampleSortSA, gather_sa
     if chunks:
         D.XCHUNK, D.CHUNK = chunks
+    if piece:
+        D.TEXT_PIECE = piece
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         res = {}
@@ -57,6 +59,13 @@ def _worker(rank, world, port, q, chunks=None, driver="range"):
             if driver == "range":
                 d = DistributedSA(CpuRangeOps())
                 sa_local, sa_off = d.build(text, len(t))
+            elif driver == "sliced":
+                # rank r starts from its slice only; the build gathers the rest
+                C = D.text_chunk(len(t), world)
+                sl = text[min(len(t), rank * C): min(len(t), (rank + 1) * C)].clone()
+                del text
+                d = DistributedSA(CpuRangeOps())
+                sa_local, sa_off = d.build_sliced(sl, len(t))
             else:
                 d = SampleSortSA(CpuOps())
                 sa_local, sa_off = d.build(text, len(t)), len(t) * rank // world
@@ -68,11 +77,11 @@ def _worker(rank, world, port, q, chunks=None, driver="range"):
         dist.destroy_process_group()
 
 
-def _run(oracle, world, chunks=None, driver="range"):
+def _run(oracle, world, chunks=None, driver="range", piece=None):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks, driver)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, chunks, driver, piece)) for r in range(world)]
     for p in procs:
         p.start()
     res = q.get(timeout=300)
@@ -83,7 +92,7 @@ def _run(oracle, world, chunks=None, driver="range"):
         sa, st = res[name]
         want = oracle.sa_c(t)
         assert (sa == want.astype(np.int64)).all(), (name, world, driver)
-        if driver == "range":
+        if driver in ("range", "sliced"):
             # one repeated symbol (sigma = 1) has no bucket layout: sample sort
             want_path = "sample-sort" if len(np.unique(t)) < 2 else "range"
             assert st["path"] == want_path, (name, st)
@@ -100,6 +109,95 @@ def test_distributed_gloo(oracle, world):
     rank requests / answers by all_to_all, several doubling rounds (K = 3)."""
     res = _run(oracle, world)
     assert max(len(st["unsorted"]) for _, st in res.values()) >= 3
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_distributed_gloo_sliced(oracle, world):
+    """The N > 1 bench's input: rank r holds only text[r C, (r + 1) C); the
+    build gathers the text (one all_gather, inside the build) and agrees on
+    failures at the collectives it needs anyway.  Pins the collectives and
+    host read-backs per build: text gather 1 + alphabet 1 + coarse 1 + per
+    round one count gather (+ two exchanges in every round but the last);
+    read-backs: alphabet 1 + coarse 1 + one per round."""
+    res = _run(oracle, world, driver="sliced")
+    for name, (_, st) in res.items():
+        if st["path"] != "range":
+            continue
+        R = len(st["unsorted"])   # count gathers (the last finds nothing unsorted)
+        assert st["collectives"] == 3 + R + 2 * (R - 1), (name, st)
+        assert st["host_syncs_driver"] == 2 + R, (name, st)
+        assert st["host_syncs_native"] == 0 and st["host_syncs"] == st["host_syncs_driver"]
+
+
+def test_distributed_gloo_sliced_pieces(oracle):
+    """The text gathered in pieces (TEXT_PIECE tiny: configs[3]'s 4 GiB path)."""
+    _run(oracle, 3, driver="sliced", piece=3000)
+
+
+def _fail_worker(rank, world, port, q, where):
+    import sys
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch.distributed as dist
+    from dist_cpu_ops import CpuRangeOps
+    from hpc_suffix_array_amd.distributed import DistributedSA
+
+    class Failing(CpuRangeOps):
+        rounds = 0
+
+        def begin(self, *a):
+            if where == "begin" and rank == 1:
+                raise MemoryError("injected begin failure")
+            return super().begin(*a)
+
+        def answer(self, req):
+            if where == "answer" and rank == 0:
+                raise RuntimeError("injected answer failure")
+            return super().answer(req)
+
+        def refine(self, h, ans, sa_local):
+            Failing.rounds += 1
+            if where == "refine" and rank == world - 1 and Failing.rounds == 2:
+                raise RuntimeError("injected refine failure")
+            return super().refine(h, ans, sa_local)
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t = _texts()["periodic"]
+        try:
+            DistributedSA(Failing()).build(torch.from_numpy(t.copy()), len(t))
+            q.put((rank, "ok"))
+        except Exception as e:   # noqa: BLE001
+            q.put((rank, type(e).__name__ + ": " + str(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("where", ["begin", "answer", "refine"])
+def test_distributed_failure_agreement(where):
+    """A phase failing on one rank makes every rank raise at the build's next
+    collective (the failing rank its own error), instead of leaving the others
+    blocked: no per-phase agreement collective is needed."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = 3
+    procs = [ctx.Process(target=_fail_worker, args=(r, world, port, q, where)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = dict(q.get(timeout=120) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    failing = {"begin": 1, "answer": 0, "refine": world - 1}[where]
+    for rank, msg in got.items():
+        assert msg != "ok", got
+        if rank == failing:
+            assert "injected" in msg, got
+        else:
+            assert "another rank" in msg, got
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -515,7 +515,8 @@ def _multi_rank_worker(rank, world, port, q, large=False):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     say("group up")
     try:
-        ops = HipRangeOps(0, 0)
+        # the workspace reserved up front (sa_dist_reserve) for the largest case
+        ops = HipRangeOps(3_000_017, 0, world=world) if not large else HipRangeOps(0, 0)
         ops.profile = True   # round 1's sa_stats: which record path ran
         res = {}
         if large:
@@ -569,7 +570,17 @@ def _multi_rank_worker(rank, world, port, q, large=False):
                 t = O.gen_text(kind, n, seed=seed)
             say("build", name)
             d = DistributedSA(ops)
-            sa_local, sa_off = d.build(torch.from_numpy(t).cuda(), len(t))
+            if name in ("dna", "alnum", "periodic", "degenerate"):
+                # the bench's input: this rank's slice only, gathered by the build
+                from hpc_suffix_array_amd.distributed import text_chunk
+                C = text_chunk(len(t), world)
+                sl = torch.from_numpy(t[min(len(t), rank * C): min(len(t), (rank + 1) * C)].copy()).cuda()
+                sa_local, sa_off = d.build_sliced(sl, len(t))
+                if d.stats["path"] == "range":
+                    R = len(d.stats["unsorted"])
+                    assert d.stats["collectives"] >= 3 + R + 2 * (R - 1), d.stats
+            else:
+                sa_local, sa_off = d.build(torch.from_numpy(t).cuda(), len(t))
             say("built", name, d.stats)
             sa = gather_sa(sa_local, sa_off, len(t))
             say("gathered", name)
