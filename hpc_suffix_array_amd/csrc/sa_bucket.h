@@ -1633,22 +1633,49 @@ __global__ __launch_bounds__(kBlock) void k_window_gather(const uint32_t* __rest
 // Sort one sub-bucket of u32 words s_k[lo, lo + cnt) (cnt <= N) in
 // registers; equal key bits (above the slot) = one group: U members and U
 // groups added to nu / ng
-template <int N>
-__device__ __forceinline__ void sort_sub_words(uint32_t* __restrict__ s_k, uint32_t lo, uint32_t cnt, uint32_t& nu,
-                                               uint32_t& ng) {
+// LSV (local-sort variant, k_bucket_sort's VAR): bit 0 reads the N words
+// unconditionally (s_k padded by kNet words; the words past the sub-bucket
+// are masked by a select instead of an exec-masked load per word), bit 1
+// writes back, for a sub-bucket without equal keys, the suffix index of
+// each sorted word (s_x[slot]) instead of the word, so the store phase reads
+// one sequential word per position (sub-buckets holding groups keep their
+// sorted words for the U walk, which converts them).  Returns whether the
+// sub-bucket holds a group.
+template <int N, int LSV = 0>
+__device__ __forceinline__ bool sort_sub_words(uint32_t* __restrict__ s_k, const uint32_t* __restrict__ s_x,
+                                               uint32_t lo, uint32_t cnt, uint32_t& nu, uint32_t& ng) {
     uint32_t v[N];
 #pragma unroll
-    for (int t = 0; t < N; ++t) v[t] = (uint32_t)t < cnt ? s_k[lo + t] : ~0u;
+    for (int t = 0; t < N; ++t) {
+        if constexpr (LSV & 1) {
+            const uint32_t x = s_k[lo + t];
+            v[t] = (uint32_t)t < cnt ? x : ~0u;
+        } else {
+            v[t] = (uint32_t)t < cnt ? s_k[lo + t] : ~0u;
+        }
+    }
     sort_net32<N>(v);
     uint32_t eqm = 0;
 #pragma unroll
     for (int t = 0; t + 1 < N; ++t) eqm |= ((v[t] ^ v[t + 1]) <= kSlotMask ? 1u : 0u) << t;
     eqm &= (1u << (cnt - 1)) - 1u;
+    if constexpr (LSV & 2) {
+        if (eqm == 0u) {
+            uint32_t xi[N];
+#pragma unroll
+            for (int t = 0; t < N; ++t) xi[t] = s_x[min(v[t] & kSlotMask, (uint32_t)kBsCap - 1u)];   // (padding: clamped)
+#pragma unroll
+            for (int t = 0; t < N; ++t)
+                if ((uint32_t)t < cnt) s_k[lo + t] = xi[t];
+            return false;
+        }
+    }
 #pragma unroll
     for (int t = 0; t < N; ++t)
         if ((uint32_t)t < cnt) s_k[lo + t] = v[t];
     nu += (uint32_t)__popc(eqm | (eqm << 1));
     ng += (uint32_t)__popc(eqm & ~(eqm << 1));
+    return eqm != 0u;
 }
 
 // a sub-bucket above kNet words (rare): insertion sort in LDS
@@ -1783,7 +1810,7 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
 #ifndef SA_LS_WFULL
 #define SA_LS_WFULL 1
 #endif
-template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false>
+template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false, int LSV = 0>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
                                                        uint32_t ib, uint32_t* __restrict__ words,
@@ -1792,7 +1819,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     static_assert(CAP <= (1 << kSlotBits), "load slots");
-    __shared__ uint32_t s_k[CAP];                 // (key bits below the sub-bucket) << kSlotBits | load slot
+    // LSV bit 0: kNet words of padding (unconditional network reads)
+    __shared__ uint32_t s_k[CAP + ((LSV & 1) ? kNet : 0)];   // (key bits below the sub-bucket) << kSlotBits | load slot
     __shared__ uint32_t s_x[CAP];                 // index of each load slot
     __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
     __shared__ uint32_t s_tmp[WAVES];
@@ -1973,12 +2001,27 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                            wide12 = __ballot(cnt > 12u) != 0ull;   // uniform
                 if (cnt == 0) continue;
                 const uint32_t nu0 = nu;
-                if (!wide4) sort_sub_words<4>(s_k, lo, cnt, nu, ng);
-                else if (!wide8) sort_sub_words<8>(s_k, lo, cnt, nu, ng);
-                else if (!wide12) sort_sub_words<12>(s_k, lo, cnt, nu, ng);
-                else if (cnt <= (uint32_t)kNet) sort_sub_words<kNet>(s_k, lo, cnt, nu, ng);
-                else sort_sub_words_lds(s_k, lo, hi, nu, ng);
-                if (nu != nu0) umask |= 1u << (sb - sb0);
+                // (LSV & 2 with key samples: words written back, the samples read them)
+                constexpr int LW = LSV & 1;
+                bool grp;
+                if ((LSV & 2) && !so.samples) {
+                    if (!wide4) grp = sort_sub_words<4, LSV>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (!wide8) grp = sort_sub_words<8, LSV>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (!wide12) grp = sort_sub_words<12, LSV>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (cnt <= (uint32_t)kNet) grp = sort_sub_words<kNet, LSV>(s_k, s_x, lo, cnt, nu, ng);
+                    else {
+                        sort_sub_words_lds(s_k, lo, hi, nu, ng);
+                        grp = true;   // the U walk converts its words (with or without groups)
+                    }
+                } else {
+                    if (!wide4) sort_sub_words<4, LW>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (!wide8) sort_sub_words<8, LW>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (!wide12) sort_sub_words<12, LW>(s_k, s_x, lo, cnt, nu, ng);
+                    else if (cnt <= (uint32_t)kNet) sort_sub_words<kNet, LW>(s_k, s_x, lo, cnt, nu, ng);
+                    else sort_sub_words_lds(s_k, lo, hi, nu, ng);
+                    grp = nu != nu0;
+                }
+                if (grp) umask |= 1u << (sb - sb0);
                 // the sorted key1 of this sub-bucket's every-2^ksh-th SA
                 // positions, from the sorted words (a global load here would
                 // make the store phase wait for the next window's loads)
@@ -2007,47 +2050,65 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 bu = (oug & 0xFFFFu) + (iug & 0xFFFFu) - nu;
                 bg = (oug >> 16) + (iug >> 16) - ng;
             }
-            if (so.rank) {
-                if (threadIdx.x == 0) {
-                    so.cnt_u[j] = tu_w;
-                    so.cnt_g[j] = tg_w;
-                    s_tot[0] += m - tu_w + tg_w;
-                    s_tot[1] += tu_w;
-                    s_tot[2] += tg_w;
-                }
-                // the unsorted members of this thread's sub-buckets (rare)
-                if (umask) {
-                    uint32_t ku = bu, kg = bg;
-                    for (uint32_t um = umask; um; um &= um - 1u) {
-                        const uint32_t sb = sb0 + (uint32_t)__builtin_ctz(um);
-                        const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
-                        uint32_t head = lo, pr = ~0u;
-                        for (uint32_t k = lo; k < hi; ++k) {
-                            const uint32_t v = s_k[k], r = v >> kSlotBits;
-                            const uint32_t nx = k + 1 < hi ? (s_k[k + 1] >> kSlotBits) : ~0u;
-                            const bool eqp = k > lo && pr == r, eqn = k + 1 < hi && nx == r;
-                            if (!eqp) head = k;
-                            if (!eqp && eqn) ++kg;
-                            if (eqp || eqn) {
-                                const uint32_t xi = s_x[v & kSlotMask];
-                                const uint32_t rv = (uint32_t)(so.rank_off + a + head + 1u);
-                                if (so.tmp_rank) so.tmp_rank[a + ku] = rv;
-                                else so.rank[xi] = rv;
-                                atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
-                                so.tmp_pos[a + ku] = (uint32_t)(a + k);
-                                so.tmp_idx[a + ku] = xi;
-                                so.tmp_g[a + ku] = kg - 1u;
-                                ++ku;
-                            }
-                            pr = r;
+            // LSV bit 1 (no key samples): s_k holds suffix indices except in
+            // the sub-buckets with groups, which the U walk converts
+            const bool idx_back = (LSV & 2) && !so.samples;   // uniform
+            if (so.rank && threadIdx.x == 0) {
+                so.cnt_u[j] = tu_w;
+                so.cnt_g[j] = tg_w;
+                s_tot[0] += m - tu_w + tg_w;
+                s_tot[1] += tu_w;
+                s_tot[2] += tg_w;
+            }
+            // the unsorted members of this thread's sub-buckets (rare)
+            if (umask && (so.rank || idx_back)) {
+                uint32_t ku = bu, kg = bg;
+                for (uint32_t um = umask; um; um &= um - 1u) {
+                    const uint32_t sb = sb0 + (uint32_t)__builtin_ctz(um);
+                    const uint32_t lo = sb ? end_of(sb - 1) : 0u, hi = end_of(sb);
+                    uint32_t head = lo, pr = ~0u;
+                    for (uint32_t k = lo; k < hi; ++k) {
+                        const uint32_t v = s_k[k], r = v >> kSlotBits;
+                        const uint32_t nx = k + 1 < hi ? (s_k[k + 1] >> kSlotBits) : ~0u;
+                        const bool eqp = k > lo && pr == r, eqn = k + 1 < hi && nx == r;
+                        const uint32_t xi = s_x[v & kSlotMask];
+                        if (idx_back) s_k[k] = xi;   // (s_k[k + 1] already read)
+                        if (!eqp) head = k;
+                        if (!eqp && eqn) ++kg;
+                        if (so.rank && (eqp || eqn)) {
+                            const uint32_t rv = (uint32_t)(so.rank_off + a + head + 1u);
+                            if (so.tmp_rank) so.tmp_rank[a + ku] = rv;
+                            else so.rank[xi] = rv;
+                            atomicOr(&so.member[xi >> 5], 1u << (xi & 31));
+                            so.tmp_pos[a + ku] = (uint32_t)(a + k);
+                            so.tmp_idx[a + ku] = xi;
+                            so.tmp_g[a + ku] = kg - 1u;
+                            ++ku;
                         }
+                        pr = r;
                     }
                 }
             }
             probe.mark(5);
             // 4. the SA, coalesced: the index of each sorted word's load slot
-            // (the U / G scan's barrier follows every thread's sort)
-            if (wfull) {
+            // (the U / G scan's barrier follows every thread's sort; with
+            // idx_back one more waits for the U walk's conversions)
+            if (idx_back) {
+                __syncthreads();
+                if (wfull) {
+#pragma unroll 2
+                    for (int i = 0; i < ITEMS; ++i) {
+                        const uint32_t le = l0 + i * kWave;
+                        sa_out[a + le] = s_k[le];
+                    }
+                } else {
+#pragma unroll 2
+                    for (int i = 0; i < ITEMS; ++i) {
+                        const uint32_t le = l0 + i * kWave;
+                        if (le < m) sa_out[a + le] = s_k[le];
+                    }
+                }
+            } else if (wfull) {
 #pragma unroll 2
                 for (int i = 0; i < ITEMS; ++i) {
                     const uint32_t le = l0 + i * kWave;

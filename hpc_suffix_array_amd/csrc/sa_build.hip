@@ -1706,15 +1706,100 @@ static int build_device(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
 // O(n) checker (replaces is_valid_suffix_array, manber_myers.c:184-202)
 // ---------------------------------------------------------------------------
 // bin shifts of a checker pass with sub-bins of 2^s2 (plan_perm's shape)
-static PermPlan plan_check(uint64_t n, uint32_t s2) {
+static PermPlan plan_check(uint64_t n, uint32_t s2, uint32_t b1 = 8) {
     PermPlan p;
     const uint32_t lg = bit_width(n > 1 ? n - 1 : 1);
     p.s2 = s2;
-    p.s1 = std::max<uint32_t>(s2, lg > 8 ? lg - 8 : 0);
+    p.s1 = std::max<uint32_t>(s2, lg > b1 ? lg - b1 : 0);
     p.nb1 = (uint32_t)((n + (1ull << p.s1) - 1) >> p.s1);
     p.nsub = 1u << (p.s1 - p.s2);
     p.tpb = (uint32_t)(((1ull << p.s1) + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems));
     return p;
+}
+
+// level-1 stripes of a permutation (sa_check.h BinStripes): `want` per bin
+// when keys[0] holds the regions with their slack (2^s1 / 128, >= 2048:
+// ~45 standard deviations of a stripe's fill at 1 GiB), else one
+static BinStripes plan_stripes(const sa_context* c, uint64_t n, const PermPlan& p, uint32_t want) {
+    BinStripes bs;
+    if (want <= 1 || n < (1ull << 24)) return bs;
+    const uint64_t per = ((1ull << p.s1) + want - 1) / want;
+    const uint64_t scap = per + std::max<uint64_t>(2048, (1ull << p.s1) / 128);
+    if ((uint64_t)p.nb1 * want * scap > c->cap_pad) return bs;
+    bs.st = want;
+    bs.scap = scap;
+    return bs;
+}
+
+constexpr uint32_t kChkStripes = 8;   // one per XCD
+constexpr uint32_t kCur2 = 1024 * kChkStripes;   // hist: level-1 cursors [stripe][bin], then level 2's
+
+// the checker's level-1 bin bits (sa_check.h k_chk_bin NB): 8 by default;
+// sa_context_set_debug's tune bits 20-23 = 1 / 2 select 10 / 9 (A/B runs)
+static uint32_t chk_stride(const PermPlan& p) { return p.nb1 <= 256 ? 256u : p.nb1 <= 512 ? 512u : 1024u; }
+
+static uint32_t chk_bin_bits(const sa_context* c) {
+    const uint32_t v = ((uint32_t)c->tune >> 20) & 0xFu;
+    return v == 1 ? 10u : v == 2 ? 9u : 8u;
+}
+
+// Levels 1 and 2 of a permutation: (dest, value) pairs of `src` binned by
+// dest (level-1 cursors per stripe and bin) and split into 2^s2-entry
+// sub-bins of the final layout (keys[1], or keys[0] when s1 == s2); returns
+// the pairs' buffer.  Cursors in hist (zeroed here).
+template <class Src, int DSH, int TAG>
+static const uint64_t* permute_levels(sa_context* c, const Src& src, uint64_t n, const PermPlan& p,
+                                      const BinStripes& bs, uint32_t* err, hipStream_t s, int* rc) {
+    *rc = SA_OK;
+    if (hipMemsetAsync(c->hist, 0, ((uint64_t)kCur2 + (uint64_t)p.nb1 * p.nsub) * 4, s) != hipSuccess) {
+        *rc = set_err(SA_E_HIP, "hipMemsetAsync failed");
+        return nullptr;
+    }
+    const uint32_t fstride = chk_stride(p);   // cursors per stripe: k_chk_bin's NB
+    if (fstride == 256) {
+        constexpr uint64_t T = (uint64_t)kChkBlock * kChkItems;
+        hipLaunchKernelGGL((k_chk_bin<kChkBlock, kChkItems, Src, 256>), dim3((uint32_t)((n + T - 1) / T)),
+                           dim3(kChkBlock), 0, s, src, n, p.s1, c->hist, c->keys[0], err, bs);
+    } else if (fstride == 512) {   // 16-bit bin tags: 7 items per lane keep two workgroups per CU
+        constexpr uint64_t T = (uint64_t)kChkBlock * 7;
+        hipLaunchKernelGGL((k_chk_bin<kChkBlock, 7, Src, 512>), dim3((uint32_t)((n + T - 1) / T)), dim3(kChkBlock),
+                           0, s, src, n, p.s1, c->hist, c->keys[0], err, bs);
+    } else {
+        constexpr uint64_t T = (uint64_t)kChkBlock * 7;
+        hipLaunchKernelGGL((k_chk_bin<kChkBlock, 7, Src, 1024>), dim3((uint32_t)((n + T - 1) / T)), dim3(kChkBlock),
+                           0, s, src, n, p.s1, c->hist, c->keys[0], err, bs);
+    }
+    if (p.s1 == p.s2 && bs.st == 1) return c->keys[0];
+    if (bs.st > 1) {
+        const uint32_t tps = (uint32_t)((bs.scap + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems));
+        hipLaunchKernelGGL((k_chk_split<kPermBlock, kPermItems, DSH, TAG>), dim3((p.nb1 + 7) / 8 * 8 * bs.st * tps),
+                           dim3(kPermBlock), 0, s, (const uint64_t*)c->keys[0], n, p.s1, p.s2, bs, tps,
+                           (const uint32_t*)c->hist, fstride, c->hist + kCur2, c->keys[1]);
+    } else {
+        hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems, DSH, true, TAG>), dim3((p.nb1 + 7) / 8 * 8 * p.tpb),
+                           dim3(kPermBlock), 0, s, (const uint64_t*)c->keys[0], n, p.s1, p.s2, p.tpb,
+                           c->hist + kCur2, c->keys[1]);
+    }
+    return c->keys[1];
+}
+
+// (dest, value) pairs of `src` placed by dest into out[0, n) by the
+// coalesced permutation: LCP's PHI.  Holes (0) and misplaced pairs set bits
+// of *err; *err bit 128: a stripe overflowed (the caller runs it again with
+// stripes = 1).
+template <class Src, int TAG>
+static int place_by_permutation(sa_context* c, const Src& src, uint64_t n, uint32_t* out, uint32_t* err,
+                                hipStream_t s, uint32_t stripes) {
+    const PermPlan p = plan_check(n, kChkSubA);
+    if (p.nb1 > 256 || p.nsub > kPermMaxSub || p.s1 > 24)
+        return set_err(SA_E_INTERNAL, "permutation plan out of range (n=%llu)", (unsigned long long)n);
+    int rc = SA_OK;
+    const uint64_t* placed = permute_levels<Src, 32, TAG>(c, src, n, p, plan_stripes(c, n, p, stripes), err, s, &rc);
+    if (rc) return rc;
+    hipLaunchKernelGGL((k_perm_place<kPermBlock, false, TAG>), dim3((uint32_t)((n + (1ull << kPermSub) - 1) >> kPermSub)),
+                       dim3(kPermBlock), 0, s, placed, n, out, err);
+    SA_HIP(hipGetLastError());
+    return SA_OK;
 }
 
 // sa_check.h: pass A (ISA' by permutation) and pass B (adjacent keys compared
@@ -1731,52 +1816,48 @@ static int check_device(sa_context* c, const uint8_t* d_text, uint64_t n, const 
     uint32_t* isa = c->rank;
     uint32_t* err = c->words + 3;
     uint32_t* cur1 = c->hist;
-    uint32_t* cur2 = c->hist + 256;
-    uint64_t* pa = c->keys[0];
-    uint64_t* pb = c->keys[1];
+    uint32_t* cur2 = c->hist + kCur2;
     uint64_t* ends = reinterpret_cast<uint64_t*>(c->vals_alt);
-    const uint64_t T = (uint64_t)kChkBlock * kChkItems;
-    const uint32_t tiles = (uint32_t)((n + T - 1) / T);
-    SA_HIP(hipMemsetAsync(err, 0, 4, s));
-    for (int pass = 0; pass < 2; ++pass) {
-        const PermPlan p = plan_check(n, pass ? kChkSubB : kChkSubA);
-        if (p.nb1 > 256 || p.nsub > kPermMaxSub || p.s1 > 24)
-            return set_err(SA_E_INTERNAL, "checker plan out of range (n=%llu)", (unsigned long long)n);
-        SA_HIP(hipMemsetAsync(c->hist, 0, (256ull + (uint64_t)p.nb1 * p.nsub) * 4, s));
-        if (pass == 0)
-            hipLaunchKernelGGL((k_chk_bin<kChkBlock, kChkItems, ChkSrcA>), dim3(tiles), dim3(kChkBlock), 0, s,
-                               ChkSrcA{d_sa}, n, p.s1, cur1, pa, err);
-        else
-            hipLaunchKernelGGL((k_chk_bin<kChkBlock, kChkItems, ChkSrcB>), dim3(tiles), dim3(kChkBlock), 0, s,
-                               ChkSrcB{isa, d_text}, n, p.s1, cur1, pa, err);
-        const uint64_t* placed = pa;
-        if (p.s1 > p.s2) {
-            const dim3 g((p.nb1 + 7) / 8 * 8 * p.tpb);
-            if (pass == 0)
-                hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems, 32, true>), g, dim3(kPermBlock), 0, s,
-                                   (const uint64_t*)pa, n, p.s1, p.s2, p.tpb, cur2, pb);
-            else
-                hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems, 40, true>), g, dim3(kPermBlock), 0, s,
-                                   (const uint64_t*)pa, n, p.s1, p.s2, p.tpb, cur2, pb);
-            placed = pb;
+    for (uint32_t stripes : {kChkStripes, 1u}) {
+        SA_HIP(hipMemsetAsync(err, 0, 4, s));
+        for (int pass = 0; pass < 2; ++pass) {
+            // pass B's sub-bins: 2^13, or 2^14 once a bin would split into more
+            // than the split pass's kPermMaxSub (n > 2^31)
+            const uint32_t lg = bit_width(n > 1 ? n - 1 : 1);
+            const uint32_t s2b = (lg > 8 && lg - 8 > kChkSubB + 10) ? kChkSubB + 1 : kChkSubB;
+            const PermPlan p = plan_check(n, pass ? s2b : kChkSubA, chk_bin_bits(c));
+            if (p.nb1 > 1024 || p.nsub > kPermMaxSub || p.s1 > 24)
+                return set_err(SA_E_INTERNAL, "checker plan out of range (n=%llu)", (unsigned long long)n);
+            const BinStripes bs = plan_stripes(c, n, p, stripes);
+            const uint64_t* placed =
+                pass == 0 ? permute_levels<ChkSrcA, 32, 1>(c, ChkSrcA{d_sa}, n, p, bs, err, s, &rc)
+                          : permute_levels<ChkSrcB, 40, 1>(c, ChkSrcB{isa, d_text}, n, p, bs, err, s, &rc);
+            if (rc) return rc;
+            hipLaunchKernelGGL(k_chk_cursors,
+                               dim3((uint32_t)std::min<uint64_t>(((uint64_t)p.nb1 * (p.nsub + 1) + kBlock - 1) / kBlock, 1024)),
+                               dim3(kBlock), 0, s, (const uint32_t*)cur1, (const uint32_t*)cur2, n, p.s1, p.s2, p.nb1,
+                               err, bs.st, chk_stride(p));
+            const uint64_t nsb = (n + (1ull << p.s2) - 1) >> p.s2;
+            if (pass == 0) {
+                hipLaunchKernelGGL((k_perm_place<kPermBlock, false, 1>), dim3((uint32_t)nsb), dim3(kPermBlock), 0, s,
+                                   placed, n, isa, err);
+            } else {
+                if (p.s2 == kChkSubB)
+                    hipLaunchKernelGGL((k_chk_place<kChkBlock>), dim3((uint32_t)nsb), dim3(kChkBlock), 0, s, placed, n,
+                                       p.s1, ends, err);
+                else
+                    hipLaunchKernelGGL((k_chk_place<kChkBlock, kChkSubB + 1>), dim3((uint32_t)nsb), dim3(kChkBlock), 0,
+                                       s, placed, n, p.s1, ends, err);
+                hipLaunchKernelGGL(k_chk_tiles, dim3((uint32_t)std::min<uint64_t>((nsb + kBlock - 1) / kBlock, 1024)),
+                                   dim3(kBlock), 0, s, (const uint64_t*)ends, nsb, err);
+            }
         }
-        hipLaunchKernelGGL(k_chk_cursors, dim3((uint32_t)std::min<uint64_t>(((uint64_t)p.nb1 * (p.nsub + 1) + kBlock - 1) / kBlock, 1024)),
-                           dim3(kBlock), 0, s, (const uint32_t*)cur1, (const uint32_t*)cur2, n, p.s1, p.s2, p.nb1, err);
-        const uint64_t nsb = (n + (1ull << p.s2) - 1) >> p.s2;
-        if (pass == 0) {
-            hipLaunchKernelGGL((k_perm_place<kPermBlock, false, 1>), dim3((uint32_t)nsb), dim3(kPermBlock), 0, s, placed, n, isa,
-                               err);
-        } else {
-            hipLaunchKernelGGL((k_chk_place<kChkBlock>), dim3((uint32_t)nsb), dim3(kChkBlock), 0, s, placed, n, p.s1,
-                               ends, err);
-            hipLaunchKernelGGL(k_chk_tiles, dim3((uint32_t)std::min<uint64_t>((nsb + kBlock - 1) / kBlock, 1024)),
-                               dim3(kBlock), 0, s, (const uint64_t*)ends, nsb, err);
-        }
+        SA_HIP(hipGetLastError());
+        SA_HIP(hipMemcpyAsync(c->host_words + 3, err, 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(host_sync(s));
+        SA_TRACE("check (%u stripes): error bits %#x", stripes, c->host_words[3]);
+        if (!(c->host_words[3] & 128u)) break;   // else a stripe overflowed: again with one
     }
-    SA_HIP(hipGetLastError());
-    SA_HIP(hipMemcpyAsync(c->host_words + 3, err, 4, hipMemcpyDeviceToHost, s));
-    SA_HIP(host_sync(s));
-    SA_TRACE("check: error bits %#x", c->host_words[3]);
     return c->host_words[3] == 0 ? 1 : 0;
 }
 
@@ -1804,7 +1885,17 @@ static int lcp_device(sa_context* c, const uint8_t* d_text, uint64_t n, const ui
     const uint32_t grid = (uint32_t)std::min<uint64_t>((n + kBlock - 1) / kBlock, 16384);
     SA_HIP(hipMemsetAsync(cnt, 0, (kLongRounds + 1) * 4, s));
     SA_HIP(hipMemsetAsync(best, 0, 8, s));
-    hipLaunchKernelGGL(k_phi, dim3(grid), dim3(kBlock), 0, s, d_sa, n, phi);
+    // PHI' = PHI + 1 (0: none) by the coalesced permutation (its hole flag for
+    // the smallest suffix, which has no predecessor, is expected: words[12])
+    for (uint32_t stripes : {kChkStripes, 1u}) {
+        SA_HIP(hipMemsetAsync(c->words + 12, 0, 4, s));
+        SA_TRY(place_by_permutation<PhiSrc, 2>(c, PhiSrc{d_sa}, n, phi, c->words + 12, s, stripes));
+        if (stripes == 1) break;
+        // a level-1 stripe that overflowed (only an adversarial SA) lost pairs
+        SA_HIP(hipMemcpyAsync(c->host_words + 12, c->words + 12, 4, hipMemcpyDeviceToHost, s));
+        SA_HIP(host_sync(s));
+        if (!(c->host_words[12] & 128u)) break;
+    }
     hipLaunchKernelGGL(k_plcp_irreducible, dim3(grid), dim3(kBlock), 0, s, d_text, n, (const uint32_t*)phi, v,
                        c->keys[0], c->vals_alt, cnt);
     uint64_t lo = kDirect;

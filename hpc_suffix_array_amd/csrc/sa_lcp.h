@@ -3,7 +3,9 @@
 // find_longest_repeated_substring, :159-182).
 //
 // Kasai's loop (:146-155) is sequential through h.  The same values come from
-// the permuted LCP array PLCP[i] = lcp(i, PHI[i]), PHI[SA[r]] = SA[r-1]:
+// the permuted LCP array PLCP[i] = lcp(i, PHI[i]), PHI[SA[r]] = SA[r-1]
+// (placed by the checker's coalesced permutation, sa_check.h PhiSrc, not a
+// random scatter):
 //   * i is *reducible* when text[i-1] == text[PHI[i]-1]; then
 //     PHI[i-1] = PHI[i]-1 and PLCP[i] = PLCP[i-1] - 1 (Kasai's own invariant);
 //   * the other (irreducible) positions are compared directly; their lcp values
@@ -57,29 +59,22 @@ __device__ __forceinline__ uint64_t mismatch8(const uint8_t* __restrict__ text, 
     return m;
 }
 
-// PHI[SA[r]] = SA[r-1]; PHI[SA[0]] = none
-__global__ __launch_bounds__(kBlock) void k_phi(const uint32_t* __restrict__ sa, uint64_t n,
-                                                uint32_t* __restrict__ phi) {
-    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x; r < n; r += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t x = sa[r];
-        if (x < n) phi[x] = r ? sa[r - 1] : kPhiNone;   // guard: never scatter out of bounds
-    }
-}
-
 // v[i] = PLCP[i] + i for irreducible i, 0 for reducible i; pairs still equal
 // after kDirect bytes go to the first cooperative list with mm = ~0.
+// phi1 = PHI + 1 (the permutation's placement, sa_check.h PhiSrc): 0 = none,
+// so phi1 - 1 wraps to kPhiNone
 __global__ __launch_bounds__(kBlock) void k_plcp_irreducible(const uint8_t* __restrict__ text, uint64_t n,
-                                                             const uint32_t* __restrict__ phi,
+                                                             const uint32_t* __restrict__ phi1,
                                                              uint32_t* __restrict__ v,
                                                              uint64_t* __restrict__ list, uint32_t* __restrict__ mm,
                                                              uint32_t* __restrict__ cnt) {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
-        const uint32_t j = phi[i];
+        const uint32_t j = phi1[i] - 1u;
         if (j == kPhiNone) {   // the smallest suffix: LCP[0] = 0 is fixed, PLCP unused
             v[i] = 0;
             continue;
         }
-        if (i > 0 && j > 0 && phi[i - 1] != kPhiNone && text[i - 1] == text[j - 1]) {
+        if (i > 0 && j > 0 && phi1[i - 1] != 0u && text[i - 1] == text[j - 1]) {
             v[i] = 0;   // reducible: PLCP[i] = PLCP[i-1] - 1
             continue;
         }

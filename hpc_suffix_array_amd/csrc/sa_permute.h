@@ -203,7 +203,7 @@ __global__ __launch_bounds__(BLOCK) void k_perm_rank(const uint64_t* __restrict_
 // byte between it and the value, sa_check.h).  CLAMP: a slot past its
 // sub-bin (a non-permutation; the checker's cursor test flags it) is dropped
 // instead of written into the next sub-bin.
-template <int BLOCK, int ITEMS, int DSH = 32, bool CLAMP = false>
+template <int BLOCK, int ITEMS, int DSH = 32, bool CLAMP = false, int TAG = 0>
 __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
                                                        uint32_t s2, uint32_t tpb, uint32_t* __restrict__ cur,
                                                        uint64_t* __restrict__ out) {
@@ -291,7 +291,8 @@ struct NextHist {
 // sub-bins (spb of them), whose positions lie in at most two queues of the
 // next round, counted in LDS (2 x 1024 words: two workgroups per CU still)
 // and added to the global counts once.
-// TAG: 1 for the checker's pass A (sa_check.h), so profiles tell it apart
+// TAG: 1 for the checker's pass A (sa_check.h), 2 for LCP's PHI (sa_lcp.h),
+// so profiles tell them apart
 template <int BLOCK, bool HIST = false, int TAG = 0>
 __global__ __launch_bounds__(BLOCK) void k_perm_place(const uint64_t* __restrict__ in, uint64_t n,
                                                        uint32_t* __restrict__ rank, uint32_t* __restrict__ err,

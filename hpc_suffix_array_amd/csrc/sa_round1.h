@@ -64,6 +64,16 @@ constexpr uint32_t kKeySample = SA_KEY_SAMPLE;
 // bucketed round's one-GPU maximum; their starts live in the onesweep base
 // scratch after the second pass's 2^hb (<= 1024) digit bases
 constexpr uint64_t kPadMinN = 1ull << 26;
+// the fixed-span local sort's variant (k_bucket_sort LSV; sa_opts.tune bits
+// 16-19 + 1 select one for A/B runs, 0 = the default)
+#ifndef SA_LS_VARIANT
+#define SA_LS_VARIANT 0
+#endif
+static int ls_variant(const sa_context* c) {
+    const uint32_t t = ((uint32_t)c->tune >> 16) & 0xFu;
+    return t ? (int)(t - 1u) : SA_LS_VARIANT;
+}
+
 // first-pass cursor stripes with padded segments (sa_opts.tune bits 8-15
 // override: 1 = one cursor per digit shared by every tile, ticketed tiles)
 static uint32_t text_stripes(const sa_context* c) {
@@ -668,9 +678,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                 XqWin xw;
                 xw.hx = hx;
                 xw.rows = xrows;
-                hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, true>), dim3(kBsWpc * (uint32_t)c->cus),
-                                   dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb,
-                                   br.bits1, bp.ib, c->words, c->keys[0], d_sa, retry, o, xw);
+#define SA_LS_XQ(V)                                                                                              \
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, true, V>), dim3(kBsWpc * (uint32_t)c->cus),   \
+                       dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1,  \
+                       bp.ib, c->words, c->keys[0], d_sa, retry, o, xw)
+                switch (ls_variant(c)) {
+                case 1: SA_LS_XQ(1); break;
+                case 2: SA_LS_XQ(2); break;
+                case 3: SA_LS_XQ(3); break;
+                default: SA_LS_XQ(0); break;
+                }
+#undef SA_LS_XQ
                 // the windows for the measured-span kernel (several buckets, or
                 // clustered keys), from their chunks to their SA positions
                 hipLaunchKernelGGL(k_window_gather, dim3(1024), dim3(kBlock), 0, s, (const uint32_t*)retry,
@@ -678,9 +696,17 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                                    (const uint32_t*)xq_pc, (const uint32_t*)xq_pn, nb_tab, (const uint64_t*)c->keys_u,
                                    c->keys[1]);
             } else {
-                hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems>), dim3(kBsWpc * (uint32_t)c->cus), dim3(kBsBlock),
-                                   0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1, bp.ib,
-                                   c->words, c->keys[0], d_sa, retry, o);
+#define SA_LS(V)                                                                                                 \
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, false, V>), dim3(kBsWpc * (uint32_t)c->cus),  \
+                       dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1,  \
+                       bp.ib, c->words, c->keys[0], d_sa, retry, o)
+                switch (ls_variant(c)) {
+                case 1: SA_LS(1); break;
+                case 2: SA_LS(2); break;
+                case 3: SA_LS(3); break;
+                default: SA_LS(0); break;
+                }
+#undef SA_LS
             }
         } else {
             hipLaunchKernelGGL((k_bucket_sort_wide<kBsBlock, kBsItems>), dim3(g), dim3(kBsBlock), 0, s,

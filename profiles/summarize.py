@@ -22,10 +22,13 @@ import sys
 from collections import defaultdict
 
 KINDS = [("k_chk_bin<1024, 8, sa::ChkSrcA", "check_bin_a"), ("k_chk_bin<1024, 8, sa::ChkSrcB", "check_bin_b"),
+         ("k_chk_bin<1024, 8, sa::PhiSrc", "lcp_phi_bin"), ("k_chk_split<1024, 8, 32, 2", "lcp_phi_split"),
+         ("k_perm_split<1024, 8, 32, true, 2", "lcp_phi_split"), ("k_perm_place<1024, false, 2", "lcp_phi_place"),
          ("k_perm_split<1024, 8, 32, true", "check_split_a"), ("k_perm_split<1024, 8, 40, true", "check_split_b"),
+         ("k_chk_split<1024, 8, 32", "check_split_a"), ("k_chk_split<1024, 8, 40", "check_split_b"),
          ("k_perm_place<1024, false, 1", "check_place_a"), ("k_chk_place", "check_place_b"),
          ("k_chk_cursors", "check_small"), ("k_chk_tiles", "check_small"),
-         ("k_phi", "lcp_phi"), ("k_plcp_irreducible", "lcp_irreducible"), ("k_plcp_long", "lcp_long"),
+         ("k_plcp_irreducible", "lcp_irreducible"), ("k_plcp_long", "lcp_long"),
          ("k_plcp_settle", "lcp_long"), ("k_chunk_max", "lcp_scan"), ("k_scan_chunk_max", "lcp_scan"),
          ("k_plcp_apply", "lcp_scan"), ("k_lcp_gather", "lcp_gather"),
          ("k_pivot_keys", "pivot_keys"), ("k_pivot_pass<0", "pivot_count"), ("k_pivot_pass<1", "pivot_count"), ("k_pivot_pass<2", "pivot_write"),

@@ -5,7 +5,8 @@ built `reps` times per variant, interleaved, with per-kernel HIP events;
 prints the median ms per kernel kind.
 
     python scripts/ab_debug.py [--n N] [--kind dna] [--reps 6] default no_xq ...
-(variant "default" = no debug flags; "a+b" = several flags)"""
+(variant "default" = no debug flags; "a+b" = several flags; a part
+"t:<int>" sets sa_opts.tune instead, e.g. t:0x20000 = local-sort variant 1)"""
 import argparse
 import os
 import statistics
@@ -34,17 +35,24 @@ def main():
     else:
         b.generate_text(t, a.n, ALPHABETS[a.kind], seed=1)
     sa = torch.empty(a.n, dtype=torch.int32, device="cuda")
+    def opts(v):
+        parts = [] if v == "default" else v.split("+")
+        tune = sum(int(p[2:], 0) for p in parts if p.startswith("t:"))
+        return tuple(p for p in parts if not p.startswith("t:")), tune
+
     res = {v: [] for v in a.variants}
-    for v in a.variants:   # warm-up
-        b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=() if v == "default" else tuple(v.split("+")))
+    ok = {}
+    for v in a.variants:   # warm-up, and every variant's SA checked
+        dbg, tune = opts(v)
+        b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=dbg, tune=tune)
+        ok[v] = b.check(t, a.n, sa)
     for _ in range(a.reps):
         for v in a.variants:
-            dbg = () if v == "default" else tuple(v.split("+"))
+            dbg, tune = opts(v)
             torch.cuda.synchronize()
-            st = b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=dbg)
+            st = b.build(t, a.n, sa, profile=True, schedule=a.schedule, debug=dbg, tune=tune)
             torch.cuda.synchronize()
             res[v].append(st)
-    ok = {v: b.check(t, a.n, sa) for v in a.variants[-1:]}
     for v, sts in res.items():
         kinds = [k for k, x in sts[0]["kernels"].items() if x["launches"]]
         med = {k: statistics.median(s["kernels"][k]["ms"] for s in sts) for k in kinds}

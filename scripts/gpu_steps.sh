@@ -16,6 +16,7 @@
 #   collect      rocprof summaries: DNA, degenerate, reference schedule
 #   collect_dna  rocprof summary of the headline only
 #   mb_bucket    microbench_bucket (the local sort alone, 2^30 items)
+#   abcheck      scripts/ab_check.py 0 1 2 (checker level-1 bins 256 / 1024 / 512, and the LCP)
 #   ab:<v1,v2>   scripts/ab_debug.py default v1 v2 (in-process interleaved A/B)
 set -o pipefail
 tag=${1:?tag}; shift
@@ -47,6 +48,7 @@ for s in "$@"; do
              run 900 collect_ref.log bash profiles/collect.sh ${tag}_refsched --schedule reference ;;
     collect_dna) run 900 collect_dna.log bash profiles/collect.sh ${tag} ;;
     mb_bucket) run 120 mb_bucket.log hpc_suffix_array_amd/csrc/build/microbench_bucket 30 5 ;;
+    abcheck) run 300 ab_check.txt python -u scripts/ab_check.py 0 1 2 ;;
     ab:*) v=${s#ab:}; run 300 ab_${v//[,+]/_}.txt python -u scripts/ab_debug.py --reps 6 default ${v//,/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac

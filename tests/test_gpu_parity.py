@@ -874,6 +874,39 @@ def test_compact_layout_text_tails(gpu, oracle, tail):
     assert (got == oracle.sa_c(t)).all()
 
 
+def test_local_sort_variants(gpu):
+    """The fixed-span local sort's variants (sa_bucket.h k_bucket_sort LSV,
+    sa_opts.tune bits 16-19): unconditional network reads, suffix indices
+    written back by the sorting threads (the U walk converting the
+    sub-buckets with groups), both -- each with per-XCD chunks (XQ) and with
+    one region (no_xq), on random DNA and on DNA with a planted repeat (groups
+    left by round 1 in many windows); same SA as the default, O(n)-checked."""
+    import torch
+    from hpc_suffix_array_amd import DeviceBuilder
+    n = (1 << 28) + 4097
+    b = DeviceBuilder(n)
+    t = torch.empty(n, dtype=torch.uint8, device="cuda")
+    want = torch.empty(n, dtype=torch.int32, device="cuda")
+    got = torch.empty(n, dtype=torch.int32, device="cuda")
+    try:
+        for kind in ("dna", "repeats"):
+            b.generate_text(t, n, b"ACGT", seed=11)
+            if kind == "repeats":   # ~4 K 64-symbol blocks each copied once: pairs of equal 20-symbol keys
+                ar = torch.arange(64, device="cuda")[None, :]
+                src = torch.arange(0, n - 70_000, 65_536, device="cuda")[:, None] + ar
+                t[(src + 32_768).reshape(-1)] = t[src.reshape(-1)]
+            t[-1] = ord("T")
+            for dbg in ((), ("no_xq",)):
+                st0 = b.build(t, n, want, debug=dbg)
+                assert st0["round1"] == "bucketed", st0
+                assert b.check(t, n, want), (kind, dbg)
+                for v in (1, 2, 3, 4):
+                    b.build(t, n, got, debug=dbg, tune=v << 16)
+                    assert bool((got == want).all().item()), (kind, dbg, v)
+    finally:
+        b.close()
+
+
 def test_round1_xq_second_pass(gpu):
     """The second bucket pass by per-XCD queues and regions (sa_split.h
     k_split_seg<.., XQ>, k_bucket_starts_xq; sa_bucket.h load_items_xq,
