@@ -606,6 +606,8 @@ static PermPlan plan_perm(uint64_t n) {
 constexpr uint64_t kPermTile = (uint64_t)kPermBlock * kPermItems;
 static_assert((kPermTile & (kPermTile - 1)) == 0, "power-of-two first-level tiles");
 static uint32_t* perm_tile_off(sa_context* c) { return c->hist + ((uint64_t)kRadix * kMaxChunks) / 2; }
+// tickets of the persistent permutation kernels: below the re-rank's tile offsets in hist
+static uint32_t* perm_tickets(sa_context* c) { return c->hist + ((uint64_t)kRadix * kMaxChunks) / 2 - 64; }
 
 static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa, const Chunking& ch,
                           hipStream_t s, Timer& tm, sa_stats* st, uint32_t kshift = 0, NextHist nh = NextHist{}) {
@@ -630,8 +632,16 @@ static int rerank_permute(sa_context* c, uint64_t* sorted, const uint32_t* d_sa,
                            (const uint64_t*)sorted, d_sa, n, toff, p.s1, 0u, cur1, other);
     const uint64_t* placed = other;
     if (p.s1 > p.s2) {
-        hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3((p.nb1 + 7) / 8 * 8 * p.tpb), dim3(kPermBlock), 0, s,
-                           (const uint64_t*)other, n, p.s1, p.s2, p.tpb, cur2, sorted);
+        if ((((uint32_t)c->tune >> 24) & 0xFu) == 1u) {   // A/B: the persistent prefetching split
+            uint32_t* tk = perm_tickets(c);
+            SA_HIP(hipMemsetAsync(tk, 0, 8 * 4, s));
+            hipLaunchKernelGGL((k_split_p<kPermBlock, kPermItems>), dim3(2 * (uint32_t)c->cus), dim3(kPermBlock), 0, s,
+                               (const uint64_t*)other, n, p.s1, p.s2, p.nb1, 1u, (uint64_t)0, p.tpb,
+                               (const uint32_t*)nullptr, 0u, cur2, sorted, tk);
+        } else {
+            hipLaunchKernelGGL((k_perm_split<kPermBlock, kPermItems>), dim3((p.nb1 + 7) / 8 * 8 * p.tpb),
+                               dim3(kPermBlock), 0, s, (const uint64_t*)other, n, p.s1, p.s2, p.tpb, cur2, sorted);
+        }
         placed = sorted;
     }
     if (nh.out) {   // the next round's first-digit counts too (persistent: one count flush per workgroup)
@@ -1058,21 +1068,26 @@ static uint32_t key_bits(uint64_t base, uint32_t K) {   // bit width of B^K - 1
     return w;
 }
 
-// auto K: enough symbols that a random text of this alphabet leaves few
-// unsorted suffixes (sigma^K >= 512 n), rounded up to fill the radix passes.
+// the fewest symbols K with sigma^K >= 512 n: a random text of this
+// alphabet then leaves few suffixes unsorted by round 1
+static uint32_t min_chars(uint32_t sigma, uint64_t n) {
+    const uint32_t kmax = max_chars((uint64_t)sigma + 1);
+    uint32_t kmin = 1;
+    unsigned __int128 p = sigma, target = (unsigned __int128)n * 512u;
+    while (p < target && kmin < kmax) {
+        p *= sigma;
+        ++kmin;
+    }
+    return kmin;
+}
+
+// auto K: min_chars, rounded up to fill the radix passes (the LSD round 1).
 static uint32_t choose_chars(uint32_t sigma, uint64_t n, int32_t req) {
     const uint64_t base = (uint64_t)sigma + 1;
     const uint32_t kmax = max_chars(base);
     if (req > 0) return std::min<uint32_t>((uint32_t)req, kmax);
     if (sigma <= 1) return kmax;
-    uint32_t kmin = 1;
-    {
-        unsigned __int128 p = sigma, target = (unsigned __int128)n * 512u;
-        while (p < target && kmin < kmax) {
-            p *= sigma;
-            ++kmin;
-        }
-    }
+    const uint32_t kmin = min_chars(sigma, n);
     const uint32_t P = (key_bits(base, kmin) + 7) / 8;
     uint32_t K = kmin;
     while (K + 1 <= kmax && key_bits(base, K + 1) <= 8 * P) ++K;
@@ -1429,9 +1444,15 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // LSD sort of the packed key
     BucketPlan bp;
     const int r1 = opts ? opts->round1 : SA_ROUND1_AUTO;
-    bool bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, !(c->dbg & SA_DEBUG_NO_CMP));
+    // the bucketed round sorts by min_chars symbols (an explicit K as given):
+    // rounding K up to fill radix passes only serves the LSD round, and a
+    // shorter key1 keeps its low bits narrow enough for the fixed-span local
+    // sort and the per-XCD second pass (1 GiB alnum: K 8 -> 7, 16.05 -> 13.59
+    // ms, profiles/r06_h_bench_alnum_k*.log; DNA, ascii127, byte256: the same K)
+    const uint32_t Kb = (opts && opts->init_chars > 0) || sigma <= 1 ? K : min_chars(sigma, n);
+    bool bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, !(c->dbg & SA_DEBUG_NO_CMP));
     if (bucketed && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
-        bucketed = plan_bucketed(sigma, n, K, r1, c->radix, &bp, 1, false);
+        bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, false);
     bool fused = false;
     bool r1_pivot = false;   // round 1 by the pivot split (pivot_round1)
     uint64_t D = 0, m = 0, G = 0;
@@ -1736,6 +1757,10 @@ constexpr uint32_t kCur2 = 1024 * kChkStripes;   // hist: level-1 cursors [strip
 
 // the checker's level-1 bin bits (sa_check.h k_chk_bin NB): 8 by default;
 // sa_context_set_debug's tune bits 20-23 = 1 / 2 select 10 / 9 (A/B runs)
+// the checker's level-2 kernel: tune bits 20-23 = 3 take the persistent
+// prefetching k_split_p (A/B runs)
+static bool chk_split_persistent(const sa_context* c) { return (((uint32_t)c->tune >> 20) & 0xFu) == 3u; }
+
 static uint32_t chk_stride(const PermPlan& p) { return p.nb1 <= 256 ? 256u : p.nb1 <= 512 ? 512u : 1024u; }
 
 static uint32_t chk_bin_bits(const sa_context* c) {
@@ -1770,6 +1795,19 @@ static const uint64_t* permute_levels(sa_context* c, const Src& src, uint64_t n,
                            0, s, src, n, p.s1, c->hist, c->keys[0], err, bs);
     }
     if (p.s1 == p.s2 && bs.st == 1) return c->keys[0];
+    if (chk_split_persistent(c)) {
+        uint32_t* tk = perm_tickets(c);
+        if (hipMemsetAsync(tk, 0, 8 * 4, s) != hipSuccess) {
+            *rc = set_err(SA_E_HIP, "hipMemsetAsync failed");
+            return nullptr;
+        }
+        const uint32_t tpr = bs.st > 1 ? (uint32_t)((bs.scap + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems))
+                                       : p.tpb;
+        hipLaunchKernelGGL((k_split_p<kPermBlock, kPermItems, DSH, true, TAG>), dim3(2 * (uint32_t)c->cus),
+                           dim3(kPermBlock), 0, s, (const uint64_t*)c->keys[0], n, p.s1, p.s2, p.nb1, bs.st, bs.scap,
+                           tpr, (const uint32_t*)c->hist, fstride, c->hist + kCur2, c->keys[1], tk);
+        return c->keys[1];
+    }
     if (bs.st > 1) {
         const uint32_t tps = (uint32_t)((bs.scap + kPermBlock * kPermItems - 1) / (kPermBlock * kPermItems));
         hipLaunchKernelGGL((k_chk_split<kPermBlock, kPermItems, DSH, TAG>), dim3((p.nb1 + 7) / 8 * 8 * bs.st * tps),

@@ -268,6 +268,127 @@ __global__ __launch_bounds__(BLOCK) void k_perm_split(const uint64_t* __restrict
     }
 }
 
+// Level 2 as persistent workgroups (k_perm_split's work, one tile of
+// BLOCK x ITEMS pairs at a time): the one-tile-per-workgroup kernels run their
+// load -> rank -> claim -> stage -> write chain with nothing in flight but the
+// other workgroup of the CU (a permutation level ran at ~3-5 TB/s); here the
+// next tile's pairs are loaded while the current one is staged and written.
+// XCD q (workgroup w mod 8) takes the tiles of the bins b = q mod 8 from its
+// own ticket tickets[q] (all tiles of a bin on one XCD, whose L2 merges the
+// partial lines where consecutive tiles' runs of a sub-bin meet).  A bin's
+// pairs: [b 2^s1, + its size) (st == 1), or its st stripe regions of level 1
+// (sa_check.h BinStripes: region (b, q') at (b st + q') scap, filled to
+// fill[q' fstride + b]), tpr tiles per region.  CLAMP: a slot past its
+// sub-bin is dropped.  grid: a multiple of 8.
+template <int BLOCK, int ITEMS, int DSH = 32, bool CLAMP = false, int TAG = 0>
+__global__ __launch_bounds__(BLOCK) void k_split_p(const uint64_t* __restrict__ in, uint64_t n, uint32_t s1,
+                                                    uint32_t s2, uint32_t nb1, uint32_t st, uint64_t scap,
+                                                    uint32_t tpr, const uint32_t* __restrict__ fill, uint32_t fstride,
+                                                    uint32_t* __restrict__ cur, uint64_t* __restrict__ out,
+                                                    uint32_t* __restrict__ tickets) {
+    constexpr int T = BLOCK * ITEMS;
+    constexpr int NB = kPermMaxSub;
+    static_assert(BLOCK >= NB, "one thread per sub-bin");
+    __shared__ uint64_t s_pair[T];
+    __shared__ uint32_t s_cnt[NB];
+    __shared__ uint32_t s_start[NB];
+    __shared__ uint32_t s_gofs[NB];
+    __shared__ uint32_t s_tmp[NB / kWave];
+    __shared__ uint32_t s_q[2];
+    const uint32_t tid = threadIdx.x;
+    const uint32_t q = blockIdx.x & 7u;
+    const uint32_t nbq = nb1 > q ? (nb1 - q + 7u) / 8u : 0u;
+    const uint32_t ntiles = nbq * st * tpr;
+    const uint32_t nsub = 1u << (s1 - s2);
+    // ticket x of queue q -> its bin and the tile's pairs [src0, src0 + valid)
+    auto decode = [&](uint32_t x, uint32_t& b, uint64_t& src0, uint32_t& valid) {
+        const uint32_t tt = x % tpr, r = x / tpr, sq = r % st;
+        b = q + 8u * (r / st);
+        const uint64_t b0 = (uint64_t)b << s1;
+        uint64_t f, base;
+        if (st == 1) {
+            f = (n - b0) < (1ull << s1) ? n - b0 : (1ull << s1);
+            base = b0;
+        } else {
+            f = fill[sq * fstride + b];
+            f = f < scap ? f : scap;
+            base = ((uint64_t)b * st + sq) * scap;
+        }
+        const uint64_t t0 = (uint64_t)tt * T;
+        valid = t0 < f ? (uint32_t)((f - t0) < (uint64_t)T ? (f - t0) : (uint64_t)T) : 0u;
+        src0 = base + t0;
+    };
+    uint64_t p[ITEMS];
+    auto load = [&](uint64_t src0, uint32_t valid) {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t x = j * BLOCK + tid;
+            p[j] = valid ? in[src0 + (x < valid ? x : valid - 1)] : 0ull;
+        }
+    };
+    if (tid < (uint32_t)NB) s_cnt[tid] = 0;
+    if (tid == 0) s_q[0] = atomicAdd(&tickets[q], 1u);
+    __syncthreads();
+    uint32_t x = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[0]);
+    uint32_t b = 0, valid = 0;
+    uint64_t src0 = 0;
+    if (x < ntiles) {
+        decode(x, b, src0, valid);
+        load(src0, valid);
+    }
+    uint32_t par = 0;
+    while (x < ntiles) {
+        if (tid == 0) s_q[par ^ 1u] = atomicAdd(&tickets[q], 1u);   // the next tile's ticket
+        const uint64_t bin0 = (uint64_t)b << s1;
+        uint32_t sub[ITEMS], slot[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t xx = j * BLOCK + tid;
+            sub[j] = xx < valid ? ((uint32_t)(p[j] >> DSH) >> s2) & (nsub - 1u) : NB;
+            slot[j] = sub[j] < (uint32_t)NB ? atomicAdd(&s_cnt[sub[j]], 1u) : 0u;
+        }
+        __syncthreads();
+        const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;
+        const uint32_t stt = perm_scan<NB>(cnt, s_tmp);
+        if (tid < (uint32_t)NB) {
+            s_start[tid] = stt;
+            s_gofs[tid] = cnt ? (uint32_t)bin0 + (tid << s2) + atomicAdd(&cur[(uint64_t)b * nsub + tid], cnt) : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j)
+            if (sub[j] < (uint32_t)NB) s_pair[s_start[sub[j]] + slot[j]] = p[j];
+        // the tile is in LDS: the next tile's pairs go out now
+        const uint32_t xn = (uint32_t)__builtin_amdgcn_readfirstlane((int)s_q[par ^ 1u]);
+        const uint32_t vcur = valid, bcur = b;
+        if (xn < ntiles) {
+            decode(xn, b, src0, valid);
+            __builtin_amdgcn_sched_barrier(0);
+            load(src0, valid);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint32_t xx = j * BLOCK + tid;
+            if (xx < vcur) {
+                const uint64_t v = s_pair[xx];
+                const uint32_t sb = ((uint32_t)(v >> DSH) >> s2) & (nsub - 1u);
+                const uint64_t g = (uint64_t)s_gofs[sb] + (xx - s_start[sb]);
+                if (CLAMP) {
+                    const uint64_t s0 = ((uint64_t)bcur << s1) + ((uint64_t)sb << s2);
+                    if (g < n && g < s0 + (1ull << s2)) out[g] = v;
+                } else if (g < n) {
+                    out[g] = v;
+                }
+            }
+        }
+        if (tid < (uint32_t)NB) s_cnt[tid] = 0;
+        __syncthreads();   // s_pair / s_start / s_gofs reused by the next tile
+        x = xn;
+        par ^= 1u;
+    }
+}
+
 // The next reference round's first-digit counts, taken while the ranks are
 // written (the LSD sort's histogram kernel then skips its 8-byte-per-suffix
 // read): its key of position i is (rank[i] << w | rank[i + h]) with the

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B of the O(n) checker's variants (sa_check.h; sa_context_set_debug tune
-bits 20-23: 0 = 256 level-1 bins, 1 = 1024, 2 = 512) and the LCP, in ONE
+bits 20-23: 0 = 256 level-1 bins, 1 = 1024, 2 = 512, 3 = the persistent
+prefetching level 2, k_split_p) and the LCP, in ONE
 process on one 1 GiB build: interleaved, median ms per variant.
 
     python scripts/ab_check.py [--n N] [--kind dna] [--reps 5] 0 1 2"""

@@ -48,7 +48,11 @@ for s in "$@"; do
              run 900 collect_ref.log bash profiles/collect.sh ${tag}_refsched --schedule reference ;;
     collect_dna) run 900 collect_dna.log bash profiles/collect.sh ${tag} ;;
     mb_bucket) run 120 mb_bucket.log hpc_suffix_array_amd/csrc/build/microbench_bucket 30 5 ;;
-    abcheck) run 300 ab_check.txt python -u scripts/ab_check.py 0 1 2 ;;
+    alnumk) for kk in 8 7; do
+                run 200 bench_alnum_k$kk.log python -u bench.py --kind alnum --init-chars $kk --no-cpu-baseline --no-reference-schedule --no-lcp
+            done ;;
+    abcheck) run 300 ab_check.txt python -u scripts/ab_check.py 0 3 ;;
+    abref:*) v=${s#abref:}; run 600 abref_${v//[,+]/_}.txt python -u scripts/ab_debug.py --schedule reference --reps 3 default ${v//,/ } ;;
     ab:*) v=${s#ab:}; run 300 ab_${v//[,+]/_}.txt python -u scripts/ab_debug.py --reps 6 default ${v//,/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac
