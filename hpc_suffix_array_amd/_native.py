@@ -49,7 +49,8 @@ class SAError(RuntimeError):
 # tests force; every combination gives the same suffix array
 DEBUG_FLAGS = {"no_cmp": 0x1, "no_pk8": 0x2, "no_pad": 0x4, "pad_overflow": 0x8, "no_fast32": 0x10,
                "no_pivot": 0x20, "perm_always": 0x40, "no_xq": 0x80, "xq_overflow": 0x100,
-               "no_tied": 0x200, "no_key1_round": 0x400}
+               "no_tied": 0x200, "no_key1_round": 0x400, "no_eonly": 0x800,
+               "eonly": 0x1000}
 
 
 def debug_bits(names) -> int:
@@ -115,7 +116,7 @@ class SaStats(ctypes.Structure):
             "round1_segments": {0: "exact", 1: "padded", 2: "padded-overflow", 3: "striped-records",
                                 4: "striped-records-overflow"}.get(self.round1_segments, "exact"),
             "round1_layout": {"compact": bool(self.round1_layout & 1), "pk8": bool(self.round1_layout & 2),
-                              "xq": bool(self.round1_layout & 4)},
+                              "xq": bool(self.round1_layout & 4), "eonly": bool(self.round1_layout & 8)},
             "reference_model_bytes": int(self.model_bytes),
             "round_bytes": [int(x) for x in self.round_bytes[:r]],
             "kernels": {k: {"ms": self.kern_ms[i], "launches": int(self.kern_launches[i]),

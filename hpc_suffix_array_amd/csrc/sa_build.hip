@@ -1450,9 +1450,21 @@ static int build_packed(sa_context* c, const uint8_t* d_text, uint64_t n, uint32
     // sort and the per-XCD second pass (1 GiB alnum: K 8 -> 7, 16.05 -> 13.59
     // ms, profiles/r06_h_bench_alnum_k*.log; DNA, ascii127, byte256: the same K)
     const uint32_t Kb = (opts && opts->init_chars > 0) || sigma <= 1 ? K : min_chars(sigma, n);
-    bool bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, !(c->dbg & SA_DEBUG_NO_CMP));
+    bool bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, (c->dbg & SA_DEBUG_NO_CMP) ? 0 : 1);
     if (bucketed && bp.bs.cmp && short_suffix_ties(h_tail, n, tail_n, h_code, sigma, bp.bs.s, bp.bs.R))
-        bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, false);
+        bucketed = plan_bucketed(sigma, n, Kb, r1, c->radix, &bp, 1, 0);
+    // a non-power-of-two alphabet one bit short of packed first-pass items
+    // (1 GiB alnum / ascii127: 65 bits) takes the E-only layout when the
+    // text's last K suffixes pad apart (BucketSpec, sa_kernels.h)
+    const bool force_eonly = (c->dbg & SA_DEBUG_EONLY) != 0;
+    if (bucketed && bp.bs.cmp == 1 && ((sigma & (sigma - 1)) != 0 || force_eonly) && !(c->dbg & SA_DEBUG_NO_EONLY)) {
+        const uint32_t hb = bp.bs.bb - kLoBits;
+        BucketPlan b2;
+        if ((force_eonly || !plan_pk8(bp, hb, c->dbg, true)) && plan_bucketed(sigma, n, Kb, r1, c->radix, &b2, 1, 2) &&
+            (force_eonly || plan_pk8(b2, hb, c->dbg, true)) &&
+            !short_suffix_ties(h_tail, n, tail_n, h_code, sigma, b2.bs.s, b2.bs.R, b2.K))
+            bp = b2;
+    }
     bool fused = false;
     bool r1_pivot = false;   // round 1 by the pivot split (pivot_round1)
     uint64_t D = 0, m = 0, G = 0;

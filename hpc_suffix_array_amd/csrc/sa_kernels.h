@@ -105,17 +105,25 @@ struct SrcText {
 // suffix then differs from every other short one in (D, r), and from the
 // longer suffixes continuing it with the smallest symbol -- equal (D, r), it
 // is their prefix -- in the bit.
+// E-only variant (cmp = 2): low = r, no end bit -- one bit less, which lets
+// a non-power-of-two alphabet's first pass write packed 8-byte items (1 GiB
+// alnum / ascii127: 65 -> 64 bits).  A short suffix S then shares its key
+// with the suffixes continuing it with the smallest symbol; round 2 orders
+// them (S + K is past the end: rank 0).  Exact when the text's last K
+// suffixes have distinct (D, r) (short_suffix_ties over K, host-checked;
+// tests/test_key1_layout.py runs the packed doubling on it).
 struct BucketSpec {
     uint64_t pow_s1;   // sigma^(s-1)
     uint64_t powR1;    // sigma^(R-1)
     uint64_t cmul;     // floor(2^48 / sigma^s): bucket = (D * cmul) >> bsh
     uint32_t sigma, s, R, rb;
     uint32_t bb, bsh;  // bucket bits (16..18), bsh = 48 - bb
-    uint32_t cmp;      // 1: compact low
+    uint32_t cmp;      // 1: compact low, 2: E-only low
 };
 
 // low of a suffix of length L with next-R-symbols value r (see BucketSpec)
 __host__ __device__ __forceinline__ uint64_t bucket_low(const BucketSpec& b, uint64_t r, uint64_t L) {
+    if (b.cmp == 2) return r;
     if (b.cmp) return 2 * r + (L >= b.s + b.R ? 1u : 0u);
     if (L < b.s) return L - 1;
     const uint64_t tl = L - b.s < b.R ? L - b.s : b.R;

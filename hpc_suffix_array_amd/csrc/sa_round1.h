@@ -106,7 +106,7 @@ struct BucketPlan {
 // cmp: the compact low of BucketSpec (only when short_suffix_ties is false
 // for the text)
 static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, int radix, BucketPlan* p,
-                          int world = 1, bool cmp = false) {
+                          int world = 1, int cmp = 0) {
     if (round1 == SA_ROUND1_LSD || radix != 0 || sigma < 2 || n < 2) return false;
     if (round1 == SA_ROUND1_AUTO && n < kBucketMinN) return false;
     // bucket bits: windows of about n / 2^bb suffixes must fit the
@@ -141,7 +141,7 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
     for (uint32_t R = K - s; R >= 1; --R) {
         unsigned __int128 pr = 1;   // sigma^R
         for (uint32_t t = 0; t < R; ++t) pr *= sigma;
-        unsigned __int128 lowmax = cmp ? 2 * pr - 1 : s + (pr - 1) * (R + 1) + R;
+        unsigned __int128 lowmax = cmp == 2 ? pr - 1 : cmp ? 2 * pr - 1 : s + (pr - 1) * (R + 1) + R;
         uint32_t rb = 0;
         while (lowmax) {
             ++rb;
@@ -157,7 +157,7 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
         p->bs.s = s;
         p->bs.R = R;
         p->bs.rb = rb;
-        p->bs.cmp = cmp ? 1u : 0u;
+        p->bs.cmp = (uint32_t)cmp;
         p->ib = ib;
         p->K = s + R;
         return true;
@@ -169,14 +169,17 @@ static bool plan_bucketed(uint32_t sigma, uint64_t n, uint32_t K, int round1, in
 // suffixes share (D, r) with digit 0 past the end (the text ends in a run of
 // its smallest symbol, e.g. ...AA for DNA: "A" and "AA" pad alike).  tail:
 // the text's last t = min(n, kMaxK) >= K - 1 bytes; code: dense codes.
+// last: how many of the last suffixes must differ (K - 1 for the compact
+// layout, K for the E-only one); t >= last.
 static bool short_suffix_ties(const uint8_t* tail, uint64_t n, uint32_t t, const uint16_t* code, uint32_t sigma,
-                              uint32_t s, uint32_t R) {
+                              uint32_t s, uint32_t R, uint32_t last = 0) {
     auto dig = [&](uint8_t x) -> uint32_t { return code[x] ? code[x] - 1u : 0u; };
     const uint32_t K = s + R;
-    uint64_t Ds[kMaxK];
-    unsigned __int128 rs[kMaxK];
+    if (last == 0) last = K - 1;
+    uint64_t Ds[kMaxK + 1];
+    unsigned __int128 rs[kMaxK + 1];
     uint32_t cnt = 0;
-    for (uint32_t L = 1; L < K && L <= n && L <= t; ++L) {
+    for (uint32_t L = 1; L <= last && L <= n && L <= t; ++L) {
         const uint8_t* x = tail + (t - L);
         uint64_t D = 0;
         unsigned __int128 r = 0;
@@ -195,9 +198,19 @@ static bool short_suffix_ties(const uint8_t* tail, uint64_t n, uint32_t t, const
 // (k_split_text / k_split_list <.., PK8>, SrcPk8): a power-of-two alphabet,
 // and the second pass's digit (of the local bucket), key1 below its bucket and
 // the index fitting 64 bits
-static bool plan_pk8(const BucketPlan& bp, uint32_t hb, uint32_t dbg) {
+// np2 (one GPU): a non-power-of-two alphabet too -- key1 below its bucket =
+// key1 - (Dmin(b) << rb) < (D values per bucket) 2^rb, D - Dmin(b) from the
+// bucket's fraction of D cmul (k_split_text); the buckets of (D cmul) >> bsh hold at most
+// ceil(sigma^s / 2^bb) + 1 values of D
+static bool plan_pk8(const BucketPlan& bp, uint32_t hb, uint32_t dbg, bool np2 = false) {
     const uint32_t sg = bp.bs.sigma;
-    if (sg < 2 || (sg & (sg - 1)) != 0 || (dbg & SA_DEBUG_NO_PK8)) return false;
+    if (sg < 2 || (dbg & SA_DEBUG_NO_PK8)) return false;
+    if ((sg & (sg - 1)) != 0) {
+        if (!np2) return false;
+        const uint64_t ps = bp.bs.pow_s1 * sg;
+        const uint64_t per = ((ps + (1ull << bp.bs.bb) - 1) >> bp.bs.bb) + 1;
+        return hb + bit_width(per - 1) + bp.bs.rb + bp.ib <= 64;
+    }
     const uint32_t lg = (uint32_t)__builtin_ctz(sg);
     if (lg * bp.bs.s < bp.bs.bb) return false;
     return hb + (lg * bp.bs.s - bp.bs.bb) + bp.bs.rb + bp.ib <= 64;
@@ -374,13 +387,18 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     const uint32_t hb = (blo == 0 && bhi == (1u << bp.bs.bb)) ? bp.bs.bb - kLoBits : range_hb(bhi - blo);
     if (hb < 7 || hb > 10) return set_err(SA_E_INTERNAL, "second bucket pass of %u bits", hb);
     const uint32_t nb_tab = 1u << (hb + kLoBits);   // local buckets in the start table
-    const bool pk8 = plan_pk8(bp, hb, c->dbg);
+    const bool np2 = (bp.bs.sigma & (bp.bs.sigma - 1)) != 0;
+    const bool pk8 = plan_pk8(bp, hb, c->dbg, !br_.always_u);   // (non-power-of-two alphabets: one GPU)
     // the local sort's key span: a one-bucket window's keys fill bits1 bits
     // (compact layout); 0 = measured per window
     uint32_t bits1 = 0;
     if (bp.bs.cmp) {
         const uint64_t ps = bp.bs.pow_s1 * bp.bs.sigma, per = (ps + (1ull << bp.bs.bb) - 1) >> bp.bs.bb;
-        bits1 = bit_width(per - 1) + bp.bs.rb;
+        // (a power-of-two alphabet's buckets hold exactly per values of D;
+        // (D cmul) >> bsh buckets up to per + 1, so key1 - Dmin(b) << rb
+        // reaches per << rb)
+        const bool exact = (ps & ((1ull << bp.bs.bb) - 1)) == 0;
+        bits1 = bit_width(exact ? per - 1 : per) + bp.bs.rb;
         // tests: a span wider than the keys' (they cluster in the low
         // sub-buckets), so every window takes the measured-span recount
         if (c->span_extra > 0) bits1 = std::min<uint32_t>(bits1 + (uint32_t)c->span_extra, 64u - bp.ib);
@@ -401,7 +419,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     static_assert(kXqQueues == kXq && kXqRegionSlack == kXqSlack, "sa_limits.h mirrors sa_split.h");
     const bool xq = SA_SEG_XQ && allow_xq && fast32 && c->cus % (int)kXq == 0 && !(c->dbg & SA_DEBUG_NO_XQ) &&
                     c->kucap >= xq_region_space(m) && xq_offsets_fit(m);
-    if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0);
+    if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0) | (bp.bs.cmp == 2 ? 8 : 0);
     // XQ workspace: queue cursors / bases / claim counts / tickets, the digit
     // sub-region starts, the per-region chunk starts and counts per bucket
     const uint64_t xqw = xq_words(1u << hb);
@@ -483,6 +501,18 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
                                    (const uint64_t*)lkeys, (const uint32_t*)lpos, m, blo, (const uint32_t*)os_base(c),
                                    os_tickets(c), c->keys[0], c->vals_alt, g_hi, cursor, 0u, 0u,
                                    striped ? (const uint32_t*)rcur : nullptr, rcap);
+        } else if (pk8 && np2) {
+#define SA_TEXT_NP2(R32)                                                                                         \
+    hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, false, true, false, false, R32>), dim3(text_grid(kSpBlock)), \
+                       dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code, bp.bs,                           \
+                       (const uint32_t*)(padded ? pstart : os_base(c)), os_tickets(c), c->keys[0], c->vals_alt, g_hi, \
+                       cursor, m, blo, bhi, padded ? (const uint32_t*)pstart + 1 : nullptr,                        \
+                       padded ? c->words + 11 : nullptr, hb, bp.ib, stripes)
+            if (bp.bs.powR1 * (uint64_t)bp.bs.sigma <= 0xFFFFFFFFull && !(((uint32_t)c->tune >> 28) & 1u))
+                SA_TEXT_NP2(true);
+            else
+                SA_TEXT_NP2(false);
+#undef SA_TEXT_NP2
         } else if (pk8 && dna) {
             SA_TEXT_PASS(true, true, kTextBlock, true, false);
         } else if (pk8 && ident) {
@@ -493,6 +523,13 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
             SA_TEXT_PASS(true, false, kTextBlock, false, true);
         } else if (pow2) {
             SA_TEXT_PASS(true, false, kTextBlock, false, false);
+        } else if (bp.bs.powR1 * (uint64_t)bp.bs.sigma <= 0xFFFFFFFFull && !(((uint32_t)c->tune >> 28) & 1u)) {
+            // sigma^R < 2^32: the remainder in 32 bits (tune bit 28: off, for A/B runs)
+            hipLaunchKernelGGL((k_split_text<kItemsA, kSpBlock, false, false, false, false, true>),
+                               dim3(text_grid(kSpBlock)), dim3(kSpBlock), 0, s, d_text, n, (const uint16_t*)c->code,
+                               bp.bs, (const uint32_t*)(padded ? pstart : os_base(c)), os_tickets(c), c->keys[0],
+                               c->vals_alt, g_hi, cursor, m, blo, bhi, padded ? (const uint32_t*)pstart + 1 : nullptr,
+                               padded ? c->words + 11 : nullptr, hb, bp.ib, stripes);
         } else {
             SA_TEXT_PASS(false, false, kSpBlock, false, false);
         }

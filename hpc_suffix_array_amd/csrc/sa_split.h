@@ -20,6 +20,7 @@
 // its current one, hence the smallest unfinished tile is always being
 // processed and the look-back cannot deadlock.
 #pragma once
+#include <type_traits>
 #include "sa_bucket.h"
 #include "sa_onesweep.h"
 
@@ -368,7 +369,10 @@ __global__ __launch_bounds__(kSpBlock) void k_split(Src src, uint64_t n, uint32_
 // byte itself -- staged without the byte map, and each position's D and
 // remainder are bit fields of the big-endian 8-byte window at it (two
 // alignbyte + bswap of the lane's staged words) instead of a roll by bytes
-template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false, bool DNA = false, bool IDENT = false>
+// R32 (!POW2, sigma^R < 2^32: alnum, ascii127): the remainder rolls in 32
+// bits (one v_mul_lo_u32 per step instead of a 64-bit multiply)
+template <int ITEMS, int BLOCK = kSpBlock, bool POW2 = false, bool PK8 = false, bool DNA = false, bool IDENT = false,
+          bool R32 = false>
 __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_t* __restrict__ text, uint64_t n,
                                                          const uint16_t* __restrict__ code, BucketSpec b,
                                                          const uint32_t* __restrict__ digit_base,
@@ -387,7 +391,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
     // claim per tile and digit.  1 GiB DNA, interleaved A/B: 1 stripe 4.01 /
     // 4.02 ms, 8 stripes 3.70 / 3.70 (tiles assigned statically instead of
     // by the ticket: 3.80 / 3.91; 2 or 4 stripes static 4.16 / 4.22).
-    static_assert(!PK8 || POW2, "packed items need a power-of-two alphabet (Dmin(bucket) by a shift)");
+    // PK8 over a non-power-of-two alphabet (NP2): key1 below its bucket is
+    // key1 - (Dmin(b) << rb), D - Dmin(b) from the bucket's fraction of D cmul
+    // (a per-item gather of a table of Dmin(b) made the pass 4.4 ->
+    // 7.4 ms at 1 GiB alnum: profiles/r06_k_ab_alnum_no_eonly_no_pk8.txt)
+    constexpr bool NP2 = PK8 && !POW2;
     constexpr int RADIX = kLoRadix;
     constexpr int RWAVES = RADIX / kWave;
     constexpr int TILE = BLOCK * ITEMS;
@@ -524,14 +532,15 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         {
             const uint32_t l0 = ITEMS * dg;
             uint32_t D = 0;
-            uint64_t r = 0;
+            using RT = typename std::conditional<R32 && !POW2, uint32_t, uint64_t>::type;
+            RT r = 0;
             // POW2: lg = log2 sigma; D < 2^(lg s) <= 2^32, r < 2^(lg R)
             const uint32_t lg = POW2 ? (uint32_t)__builtin_ctz(b.sigma) : 0u;
             const uint32_t dmask = POW2 ? (lg * b.s >= 32 ? ~0u : (1u << (lg * b.s)) - 1u) : 0u;
             const uint64_t rmask = POW2 ? ((1ull << (lg * b.R)) - 1ull) : 0ull;
             const uint32_t bksh = POW2 ? lg * b.s - b.bb : 0u;   // bucket = D >> (lg s - bb)
             // interior low = r mulR + addR (BucketSpec: compact or not)
-            const uint64_t mulR = b.cmp ? 2u : b.R + 1u, addR = b.cmp ? 1u : b.s + b.R;
+            const uint64_t mulR = b.cmp == 2 ? 1u : b.cmp ? 2u : b.R + 1u, addR = b.cmp == 2 ? 0u : b.cmp ? 1u : b.s + b.R;
             uint64_t win = 0;   // DNA: symbols l0 .. l0 + 31, the first on top
             uint32_t wid[IDENT ? ITEMS / 4 + 2 : 1];   // IDENT: the lane's staged words from l0
             if constexpr (IDENT) {
@@ -547,7 +556,7 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 for (uint32_t q = 0; q < b.R; ++q) r = (r << lg) | s_dc[l0 + b.s + q];
             } else {
                 for (uint32_t q = 0; q < b.s; ++q) D = D * b.sigma + s_dc[l0 + q];
-                for (uint32_t q = 0; q < b.R; ++q) r = r * b.sigma + s_dc[l0 + b.s + q];
+                for (uint32_t q = 0; q < b.R; ++q) r = r * (RT)b.sigma + s_dc[l0 + b.s + q];
             }
             const bool interior = (uint32_t)t < t_int;   // every suffix of the tile has >= K symbols
             const bool full = full0 && interior;        // uniform
@@ -583,11 +592,11 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                         r = ((r << lg) | byte_at<ITEMS>(xn, j - 1)) & rmask;
                     } else {
                         D = (D - byte_at<ITEMS>(xo, j - 1) * (uint32_t)b.pow_s1) * b.sigma + xi;
-                        r = (r - (uint64_t)xi * b.powR1) * b.sigma + byte_at<ITEMS>(xn, j - 1);
+                        r = (r - (RT)xi * (RT)b.powR1) * (RT)b.sigma + byte_at<ITEMS>(xn, j - 1);
                     }
                 }
                 // (past the end L wraps: never ranked; FULL tiles are interior)
-                const uint64_t low = (FULL || interior) ? r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
+                const uint64_t low = (FULL || interior) ? (uint64_t)r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
                 k[j] = ((uint64_t)D << b.rb) | low;
                 const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
                 const uint32_t lb = bk - blo;
@@ -648,14 +657,30 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
         // values there spilled 19 VGPRs): the second pass's digit (the
         // bucket's high bits; one GPU: local = global bucket), key1 below its
         // bucket, the position
-        const uint32_t kbsh = b.rb + (PK8 ? (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb : 0u);
-        const uint64_t remmask = PK8 ? (1ull << kbsh) - 1ull : 0ull;
+        const uint32_t kbsh = b.rb + ((PK8 && POW2) ? (uint32_t)__builtin_ctz(b.sigma) * b.s - b.bb : 0u);
+        const uint64_t remmask = (PK8 && POW2) ? (1ull << kbsh) - 1ull : 0ull;
+        // NP2: D - Dmin(bucket) = the values of D below D in its bucket =
+        // floor(f / cmul), f = D cmul mod 2^bsh (the bucket's fraction; f <
+        // 2^31): by a double reciprocal, corrected by one integer step
+        const double icm = NP2 ? 1.0 / (double)b.cmul : 0.0;
+        const uint64_t fmask = (1ull << b.bsh) - 1ull;
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                if constexpr (PK8) {
+                if constexpr (NP2) {
+                    const uint64_t prod = (k[j] >> b.rb) * b.cmul;
+                    const uint32_t bk = (uint32_t)(prod >> b.bsh);
+                    const uint32_t f = (uint32_t)(prod & fmask);
+                    uint32_t rd = (uint32_t)((double)f * icm);
+                    rd = ((uint64_t)rd * b.cmul > f) ? rd - 1u : rd;
+                    rd = ((uint64_t)(rd + 1u) * b.cmul <= f) ? rd + 1u : rd;
+                    const uint32_t hi = (bk - blo) >> kLoBits;   // local bucket
+                    const uint64_t rel = ((uint64_t)rd << b.rb) | (k[j] & ((1ull << b.rb) - 1ull));
+                    s_keys[pos] = ((uint64_t)hi << (64u - pk_hb)) | (rel << pk_ib) | (tb + ITEMS * dg + j);
+                    s_idx[pos] = (uint16_t)d;
+                } else if constexpr (PK8) {
                     const uint32_t hi = ((uint32_t)(k[j] >> kbsh) - blo) >> kLoBits;   // local bucket
                     s_keys[pos] = ((uint64_t)hi << (64u - pk_hb)) | ((k[j] & remmask) << pk_ib) |
                                   (tb + ITEMS * dg + j);

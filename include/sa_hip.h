@@ -95,6 +95,10 @@ enum sa_kernel_kind {
                                            the sample search (RankLookup), not as key1 rebuilt from the text */
 #define SA_DEBUG_NO_TIED 0x200u         /* pivot rounds: tied blocks through the sorted output and segments(), not
                                            written straight to the next unsorted set (sa_pivot.h) */
+#define SA_DEBUG_NO_EONLY 0x800u        /* non-power-of-two alphabets: keep the compact key1 layout (and 12-byte
+                                           first-pass items) instead of the E-only layout that packs them */
+#define SA_DEBUG_EONLY 0x1000u          /* bucketed round 1: the E-only key1 layout whenever the text's tail allows
+                                           it (tests; production takes it only for packed non-power-of-two items) */
 
 typedef struct {
     int32_t profile;        /* 1: time every launch with HIP events */
@@ -139,7 +143,8 @@ typedef struct {
                                             stripe overflowed and the round ran again with the counting scan */
     int32_t round1_layout;               /* bucketed round 1: bit 0 compact key1 low (BucketSpec.cmp),
                                             bit 1 packed 8-byte first-pass items (PK8), bit 2 the second
-                                            pass by per-XCD queues and regions (XQ) */
+                                            pass by per-XCD queues and regions (XQ), bit 3 the E-only
+                                            key1 low (no end bit; non-power-of-two alphabets' PK8) */
     uint64_t round_bytes[SA_MAX_ROUNDS]; /* algorithmic bytes of the kernels launched in round j (the kern_bytes
                                             added between its boundaries; the schedule actually run) */
 } sa_stats;

@@ -17,6 +17,7 @@
 #   collect_dna  rocprof summary of the headline only
 #   mb_bucket    microbench_bucket (the local sort alone, 2^30 items)
 #   abcheck      scripts/ab_check.py 0 1 2 (checker level-1 bins 256 / 1024 / 512, and the LCP)
+#   abk:<kind>:<v1,v2>  the same A/B on another alphabet
 #   ab:<v1,v2>   scripts/ab_debug.py default v1 v2 (in-process interleaved A/B)
 set -o pipefail
 tag=${1:?tag}; shift
@@ -53,6 +54,7 @@ for s in "$@"; do
             done ;;
     abcheck) run 300 ab_check.txt python -u scripts/ab_check.py 0 3 ;;
     abref:*) v=${s#abref:}; run 600 abref_${v//[,+]/_}.txt python -u scripts/ab_debug.py --schedule reference --reps 3 default ${v//,/ } ;;
+    abk:*) v=${s#abk:}; kk=${v%%:*}; v=${v#*:}; run 300 ab_${kk}_${v//[,+]/_}.txt python -u scripts/ab_debug.py --kind $kk --reps 6 default ${v//,/ } ;;
     ab:*) v=${s#ab:}; run 300 ab_${v//[,+]/_}.txt python -u scripts/ab_debug.py --reps 6 default ${v//,/ } ;;
     *) echo "unknown step $s"; exit 2 ;;
     esac

@@ -714,7 +714,9 @@ def test_round1_variants_agree(gpu, oracle, round1):
     for kind, n in (("dna", 3_000_017), ("alnum", 1_500_007), ("byte256", 1 << 21)):
         t = oracle.gen_text(kind, n, seed=n)
         got, st = build_suffix_array(t, return_stats=True, round1=round1)
-        ref, st_ref = build_suffix_array(t, return_stats=True, round1="lsd")
+        # the same K for both (auto K: the bucketed round takes the fewest
+        # symbols, the LSD round rounds K up to whole radix passes)
+        ref, st_ref = build_suffix_array(t, return_stats=True, round1="lsd", init_chars=st["init_chars"])
         assert (got == ref).all() and (got == oracle.sa_c(t)).all(), (kind, round1)
         assert st["round1"] == round1
         assert st["distinct"] == st_ref["distinct"], (kind, st["distinct"], st_ref["distinct"])
@@ -872,6 +874,41 @@ def test_compact_layout_text_tails(gpu, oracle, tail):
     smallest_run = tail.endswith(b"AA")   # "A" and "AA" pad alike
     assert st["round1_layout"]["compact"] == (not smallest_run), (tail, st["round1_layout"])
     assert (got == oracle.sa_c(t)).all()
+
+
+@pytest.mark.parametrize("kind", ["alnum", "ascii127", "dna", "binary"])
+def test_eonly_layout(gpu, oracle, kind):
+    """The E-only key1 layout (BucketSpec.cmp = 2, no end bit: what lets 1 GiB
+    alnum / ascii127 pack their first-pass items) forced at every size: short
+    suffixes share keys with the suffixes continuing them with the smallest
+    symbol and round 2 orders them.  Texts whose last K suffixes pad alike
+    (a tail run of the smallest symbol) must keep the compact layout.  Also
+    the packed non-power-of-two items (np2 PK8, k_bucket_dmin) on their own."""
+    from hpc_suffix_array_amd import build_suffix_array
+    for n in (70_001, 1 << 20, 3_000_017):
+        t = oracle.gen_text(kind, n, seed=n + 5)
+        want = oracle.sa_c(t)
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed", debug=("eonly",))
+        assert (got == want).all(), (kind, n)
+        assert st["round1"] == "bucketed", (kind, n)
+        if kind != "binary":   # (a random binary tail often pads alike: compact / original layout, still exact)
+            assert st["round1_layout"]["eonly"], (kind, n, st["round1_layout"])
+        got, st = build_suffix_array(t, return_stats=True, round1="bucketed")
+        assert (got == want).all(), (kind, n)
+        if kind in ("alnum", "ascii127"):   # non-power-of-two items packed at these sizes (compact layout fits)
+            assert st["round1_layout"]["pk8"], (kind, n, st["round1_layout"])
+        # tails that defeat the E-only precondition: the smallest symbol repeated
+        tt = t.copy()
+        tt[-(st["init_chars"] + 3):] = tt.min()
+        got, st = build_suffix_array(tt, return_stats=True, round1="bucketed", debug=("eonly",))
+        assert (got == oracle.sa_c(tt)).all(), (kind, n, "tail")
+        assert not st["round1_layout"]["eonly"], (kind, n)
+        # one short suffix equal to the smallest symbol only (passes the check
+        # when the rest of the tail differs): "...x" + smallest
+        tt = t.copy()
+        tt[-1] = t.min()
+        got, st = build_suffix_array(tt, return_stats=True, round1="bucketed", debug=("eonly",))
+        assert (got == oracle.sa_c(tt)).all(), (kind, n, "one")
 
 
 def test_local_sort_variants(gpu):
