@@ -835,8 +835,8 @@ def test_round1_padded_segments_skewed(gpu, oracle):
 def test_round1_layouts(gpu, oracle, golden, layout):
     """Key layouts of the bucketed first round (sa_kernels.h BucketSpec,
     sa_split.h k_split_text<.., PK8>): the compact low (cmp) with packed
-    8-byte first-pass items (pk8, power-of-two alphabets with the bits to
-    spare), the compact low alone, and the original layout -- same SA."""
+    8-byte first-pass items (pk8, wherever the bits fit: sa_round1.h
+    plan_pk8), the compact low alone, and the original layout -- same SA."""
     from hpc_suffix_array_amd import build_suffix_array
     dbg = () if layout == "default" else (layout,)
     for kind, n in (("dna", 3_000_017), ("byte256", 1 << 21), ("alnum", 1_500_007), ("binary", 1 << 20)):
@@ -846,8 +846,10 @@ def test_round1_layouts(gpu, oracle, golden, layout):
         assert st["round1"] == "bucketed", (kind, st)
         lay = st["round1_layout"]
         assert lay["compact"] == (layout != "no_cmp"), (kind, lay)
-        if layout == "no_pk8" or kind == "alnum":   # alnum: sigma 62, not a power of two
+        if layout == "no_pk8":
             assert not lay["pk8"], (kind, lay)
+        elif kind != "binary":   # alnum (sigma 62) through the fraction form of D - Dmin(bucket)
+            assert lay["pk8"], (kind, lay)
         assert (got == oracle.sa_c(t)).all(), (kind, layout)
     if layout == "default":   # config 2 through the packed items (1 GiB: the bench)
         k = golden["known"]["dna_64MiB"]
@@ -855,7 +857,7 @@ def test_round1_layouts(gpu, oracle, golden, layout):
         got, st = build_suffix_array(t, return_stats=True)
         # 2^26 suffixes: 16-bit buckets of ~1024 suffixes, below the fixed-span
         # local sort's 4 window strides, so the second pass takes one region
-        assert st["round1_layout"] == {"compact": True, "pk8": True, "xq": False}, st["round1_layout"]
+        assert st["round1_layout"] == {"compact": True, "pk8": True, "xq": False, "eonly": False}, st["round1_layout"]
         assert oracle.sha256(got.astype(np.int32)) == k["sa_sha256_i32"]
 
 
