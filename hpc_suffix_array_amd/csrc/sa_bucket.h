@@ -1555,7 +1555,7 @@ __global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restr
                                                          uint32_t* __restrict__ retry, uint32_t fast,
                                                          const uint32_t* __restrict__ pc = nullptr,
                                                          const uint32_t* __restrict__ pn = nullptr, uint32_t nb = 0,
-                                                         uint32_t* __restrict__ hx = nullptr) {
+                                                         uint32_t* __restrict__ hx = nullptr, uint32_t crows = 0) {
     const uint32_t nlist = words[7];
     const uint32_t lane = lane_id();
     for (uint64_t q0 = (uint64_t)blockIdx.x * kBlock; q0 < nlist; q0 += (uint64_t)gridDim.x * kBlock) {
@@ -1568,12 +1568,18 @@ __global__ __launch_bounds__(kBlock) void k_window_split(const uint32_t* __restr
             b0 = br.wb[j];
             one = fast && br.wb[j + 1] - b0 == 1u;
             // XQ: a chunk under 64 items could put two boundaries in one row
-            // of 64 slots (k_window_rows): such windows take the wide kernel
-            if (one && hx)
+            // of 64 slots (k_window_rows): such windows take the wide kernel;
+            // chunk rows (crows > 0: one chunk per row) need sum ceil(c / 64)
+            // <= crows rows instead
+            if (one && hx) {
+                uint32_t nr = 0;
                 for (uint32_t k = 0; k < kXq; ++k) {
                     const uint32_t c = pn[(uint64_t)k * nb + b0];
-                    if (c && c < kWave) one = false;
+                    if (!crows && c && c < kWave) one = false;
+                    nr += (c + kWave - 1) / kWave;
                 }
+                if (crows && nr > crows) one = false;
+            }
         }
         const uint64_t m1 = __ballot(ok && one), m2 = __ballot(ok && !one);
         uint32_t base1 = 0, base2 = 0;
@@ -1746,8 +1752,31 @@ __device__ __forceinline__ uint32_t xq_offset(const uint32_t* __restrict__ hx, u
     return off;
 }
 
+// Chunk rows (CR, k_window_rows<true>): every row of 64 load slots reads ONE
+// chunk -- the chunks' full rows first, in chunk order, then one partial row
+// per chunk whose length is not a multiple of 64, then empty rows; the table
+// holds per row its w_in index of lane 0 (t = 0) and its lanes holding items
+// (t = 1: 64, the partial count or 0).  A load is then one uniform base and
+// the lane (one readlane, no per-lane select or clamp: ~10 VALU per item
+// fewer), at the price of up to 8 partial rows (k_window_split admits a
+// window when sum ceil(chunk / 64) <= ROWS) whose idle lanes read up to 63
+// items past their chunk, inside keys_u's slack, and are masked where the
+// items are used.  The slots are no longer in window order; the sort does not
+// need them to be.
+template <int ITEMS>
+__device__ __forceinline__ void load_items_cr(const uint64_t* __restrict__ w_in, const uint32_t (&rv)[3],
+                                              uint64_t (&x)[ITEMS]) {
+    const uint32_t lane = lane_id();
+#pragma unroll
+    for (int i = 0; i < ITEMS; ++i) {
+        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane((int)rv[0], i);
+        x[i] = (w_in + base)[lane];
+    }
+}
+
 // this wave's row words of a window: lane i < ITEMS holds word i of row
-// (wave ITEMS + i) of table t (0: d_a, 1: d_b, 2: split)
+// (wave ITEMS + i) of table t (0: d_a, 1: d_b, 2: split; chunk rows: 0 base,
+// 1 count)
 template <int ITEMS, int ROWS>
 __device__ __forceinline__ void load_rows_xq(const uint32_t* __restrict__ rows, uint32_t (&rv)[3]) {
     const uint32_t lane = lane_id();
@@ -1778,6 +1807,8 @@ __device__ __forceinline__ void load_items_xq(const uint64_t* __restrict__ w_in,
 // words[kHdrWord], hx), one wave per window: row r covers slots [64 r,
 // min(64 r + 63, m - 1)] (slots past m re-read item m - 1); at most one
 // chunk boundary lies inside a row (k_window_split).
+// CR: the chunk rows of load_items_cr instead.
+template <bool CR>
 __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restrict__ words, const uint4* __restrict__ hdr,
                                                         const uint32_t* __restrict__ hx, uint32_t nrows,
                                                         uint32_t* __restrict__ rows) {
@@ -1788,6 +1819,38 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
         uint32_t hv[16];
 #pragma unroll
         for (int k = 0; k < 16; ++k) hv[k] = hx[q * 16 + k];
+        if constexpr (CR) {
+            // chunk k: items [P_k, P_k+1) of the window at w_in[hv[k] + P_k ...]
+            uint32_t st[kXq], cn[kXq], nfull = 0;
+#pragma unroll
+            for (int k = 0; k < (int)kXq; ++k) {
+                const uint32_t p0 = k ? hv[kXq - 1 + k] : 0u, p1 = k + 1 < (int)kXq ? hv[kXq + k] : m;
+                st[k] = hv[k] + p0;
+                cn[k] = p1 - p0;
+                nfull += cn[k] / kWave;
+            }
+            for (uint32_t r = lane; r < nrows; r += kWave) {
+                uint32_t base = st[0], cnt = 0, rf = 0, rp = nfull;
+#pragma unroll
+                for (int k = 0; k < (int)kXq; ++k) {
+                    const uint32_t nf = cn[k] / kWave, rem = cn[k] % kWave;
+                    if (r >= rf && r < rf + nf) {
+                        base = st[k] + kWave * (r - rf);
+                        cnt = kWave;
+                    }
+                    if (rem && r == rp) {
+                        base = st[k] + kWave * nf;
+                        cnt = rem;
+                    }
+                    rf += nf;
+                    rp += rem ? 1u : 0u;
+                }
+                uint32_t* const e = rows + q * 3 * nrows + r;
+                e[0] = base;
+                e[nrows] = cnt;
+            }
+            continue;
+        }
         for (uint32_t r = lane; r < nrows; r += kWave) {
             const uint32_t lo = std::min(r * kWave, m - 1), hi = std::min(r * kWave + (kWave - 1), m - 1);
             uint32_t split = kWave;   // the first boundary inside (lo, hi]
@@ -1810,7 +1873,7 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
 #ifndef SA_LS_WFULL
 #define SA_LS_WFULL 1
 #endif
-template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false, int LSV = 0>
+template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false, int LSV = 0, bool CR = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
                                                        uint32_t ib, uint32_t* __restrict__ words,
@@ -1851,10 +1914,13 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     if (q >= nwin) return;   // uniform
     uint4 h = hdr[q];
     uint64_t w[ITEMS];
+    // XQ: this window's row words (CR: its row counts mark the load slots
+    // holding items)
+    uint32_t rv[3] = {0u, 0u, 0u};
     if constexpr (XQ) {
-        uint32_t rv[3];
         load_rows_xq<ITEMS, ROWS>(xw.rows + (uint64_t)q * 3 * ROWS, rv);
-        load_items_xq<ITEMS>(keys_in, rv, h.z, w);
+        if constexpr (CR) load_items_cr<ITEMS>(keys_in, rv, w);
+        else load_items_xq<ITEMS>(keys_in, rv, h.z, w);
     } else {
         load_items<ITEMS>(keys_in, h.y, h.z, w);
     }
@@ -1882,8 +1948,18 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         probe.mark(0);
         const uint32_t l0 = slot0<ITEMS>();
         // 1. sub-bucket histogram (counts < 2^16: no carry between the halves)
+        // wfull: this wave's SA positions all lie inside the window (the
+        // store); sfull: its load slots all hold items (CR: its rows are all
+        // full, else = wfull); slot_ok(i): item i of this lane holds one
         const bool wfull = SA_LS_WFULL && (wave + 1) * (uint32_t)(kWave * ITEMS) <= m;   // uniform per wave
-        if (wfull) {
+        bool sfull = wfull;
+        if constexpr (XQ && CR)
+            sfull = SA_LS_WFULL && __ballot(lane < (uint32_t)ITEMS && rv[1] == kWave) == (1ull << ITEMS) - 1ull;
+        auto slot_ok = [&](int i) -> bool {
+            if constexpr (XQ && CR) return lane < (uint32_t)__builtin_amdgcn_readlane((int)rv[1], i);
+            else return l0 + i * kWave < m;
+        };
+        if (sfull) {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
                 const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
@@ -1892,7 +1968,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         } else {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
-                if (l0 + i * kWave < m) {
+                if (slot_ok(i)) {
                     const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
                     atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
                 }
@@ -1945,7 +2021,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // positions for it; storing the items here made this kernel spill)
             if (threadIdx.x == 0) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
+            if constexpr (XQ && CR) load_items_cr<ITEMS>(keys_in, rwn, w);
+            else if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
             else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
         } else {
@@ -1957,21 +2034,22 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 s_k[(old >> (16 * (sb & 1))) & 0xFFFFu] = (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
                 s_x[le] = (uint32_t)(w[i] & imask);
             };
-            if (wfull) {
+            if (sfull) {
 #pragma unroll
                 for (int i = 0; i < ITEMS; ++i) scatter1(i, l0 + i * kWave);
             } else {
 #pragma unroll
                 for (int i = 0; i < ITEMS; ++i) {
                     const uint32_t le = l0 + i * kWave;
-                    if (le < m) scatter1(i, le);
+                    if (slot_ok(i)) scatter1(i, le);
                 }
             }
             // ... the window is in LDS: the next window's loads go out now (a
             // scheduling barrier: hoisted above the scatter, they would hold
             // a second window of registers)
             __builtin_amdgcn_sched_barrier(0);
-            if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
+            if constexpr (XQ && CR) load_items_cr<ITEMS>(keys_in, rwn, w);
+            else if constexpr (XQ) load_items_xq<ITEMS>(keys_in, rwn, hn.z, w);
             else load_items<ITEMS>(keys_in, hn.y, hn.z, w);
             __syncthreads();
             probe.mark(3);
@@ -2127,6 +2205,10 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         if (!more) break;
         q = qn;
         h = hn;
+        if constexpr (XQ && CR) {
+            rv[0] = rwn[0];
+            rv[1] = rwn[1];
+        }
         par ^= 1u;
     }
     probe.flush(words);

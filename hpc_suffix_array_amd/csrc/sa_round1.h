@@ -418,7 +418,7 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
     // load_items_xq): the whole region space must stay below 2^32
     static_assert(kXqQueues == kXq && kXqRegionSlack == kXqSlack, "sa_limits.h mirrors sa_split.h");
     const bool xq = SA_SEG_XQ && allow_xq && fast32 && c->cus % (int)kXq == 0 && !(c->dbg & SA_DEBUG_NO_XQ) &&
-                    c->kucap >= xq_region_space(m) && xq_offsets_fit(m);
+                    c->kucap >= xq_region_space(m) + kWave && xq_offsets_fit(m);   // (+ a row: load_items_cr)
     if (st) st->round1_layout = (bp.bs.cmp ? 1 : 0) | (pk8 ? 2 : 0) | (xq ? 4 : 0) | (bp.bs.cmp == 2 ? 8 : 0);
     // XQ workspace: queue cursors / bases / claim counts / tickets, the digit
     // sub-region starts, the per-region chunk starts and counts per bucket
@@ -707,23 +707,35 @@ static int round1_bucketed(sa_context* c, const uint8_t* d_text, uint64_t n, uin
         (void)hipMemsetAsync(c->words + kRetryWord, 0, 12, s);   // retry count, one-bucket windows, ticket
         if (fast32) {
             const uint32_t gs = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>((nw + kBlock - 1) / kBlock, 1024));
+            // XQ chunk rows (sa_bucket.h load_items_cr; tune bit 29: the
+            // window-order rows with a per-lane chunk select)
+            const bool cr = xq && !(((uint32_t)c->tune >> 29) & 1u);
             hipLaunchKernelGGL(k_window_split, dim3(gs), dim3(kBlock), 0, s, (const uint32_t*)list, (const uint32_t*)ws,
-                               br, c->words, hdr, retry, 1u, (const uint32_t*)xq_pc, (const uint32_t*)xq_pn, nb_tab, hx);
+                               br, c->words, hdr, retry, 1u, (const uint32_t*)xq_pc, (const uint32_t*)xq_pn, nb_tab, hx,
+                               cr ? kBsRows : 0u);
             if (xq) {
-                hipLaunchKernelGGL(k_window_rows, dim3(2048), dim3(kBlock), 0, s, (const uint32_t*)c->words,
-                                   (const uint4*)hdr, (const uint32_t*)hx, kBsRows, xrows);
+                if (cr)
+                    hipLaunchKernelGGL(k_window_rows<true>, dim3(2048), dim3(kBlock), 0, s, (const uint32_t*)c->words,
+                                       (const uint4*)hdr, (const uint32_t*)hx, kBsRows, xrows);
+                else
+                    hipLaunchKernelGGL(k_window_rows<false>, dim3(2048), dim3(kBlock), 0, s, (const uint32_t*)c->words,
+                                       (const uint4*)hdr, (const uint32_t*)hx, kBsRows, xrows);
                 XqWin xw;
                 xw.hx = hx;
                 xw.rows = xrows;
-#define SA_LS_XQ(V)                                                                                              \
-    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, true, V>), dim3(kBsWpc * (uint32_t)c->cus),   \
+#define SA_LS_XQ(V, CR)                                                                                          \
+    hipLaunchKernelGGL((k_bucket_sort<kBsBlock, kBsItems, NoProbe, true, V, CR>), dim3(kBsWpc * (uint32_t)c->cus), \
                        dim3(kBsBlock), 0, s, (const uint64_t*)c->keys_u, (const uint4*)hdr, bp.bs.rb, br.bits1,  \
                        bp.ib, c->words, c->keys[0], d_sa, retry, o, xw)
-                switch (ls_variant(c)) {
-                case 1: SA_LS_XQ(1); break;
-                case 2: SA_LS_XQ(2); break;
-                case 3: SA_LS_XQ(3); break;
-                default: SA_LS_XQ(0); break;
+                switch (ls_variant(c) | (cr ? 4 : 0)) {
+                case 1: SA_LS_XQ(1, false); break;
+                case 2: SA_LS_XQ(2, false); break;
+                case 3: SA_LS_XQ(3, false); break;
+                case 4: SA_LS_XQ(0, true); break;
+                case 5: SA_LS_XQ(1, true); break;
+                case 6: SA_LS_XQ(2, true); break;
+                case 7: SA_LS_XQ(3, true); break;
+                default: SA_LS_XQ(0, false); break;
                 }
 #undef SA_LS_XQ
                 // the windows for the measured-span kernel (several buckets, or
