@@ -1873,6 +1873,9 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
 #ifndef SA_LS_WFULL
 #define SA_LS_WFULL 1
 #endif
+#ifndef SA_LS_CLAIMS
+#define SA_LS_CLAIMS 3   // (must divide ITEMS)
+#endif
 template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false, int LSV = 0, bool CR = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
                                                        const uint4* __restrict__ hdr, uint32_t rb, uint32_t bits,
@@ -1882,10 +1885,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     constexpr int WAVES = BLOCK / kWave;
     constexpr int CAP = BLOCK * ITEMS;
     static_assert(CAP <= (1 << kSlotBits), "load slots");
-    // LSV bit 0: kNet words of padding (unconditional network reads)
-    __shared__ uint32_t s_k[CAP + ((LSV & 1) ? kNet : 0)];   // (key bits below the sub-bucket) << kSlotBits | load slot
-    __shared__ uint32_t s_x[CAP];                 // index of each load slot
-    __shared__ uint32_t s_cnt[kSubBuckets / 2];   // 16-bit counts, cursors, then ends; two per word
+    // s_cnt first (LDS address 0: its byte addresses need no base); its
+    // 16-bit counts, cursors and ends count BYTES of s_k (4 per word, at most
+    // 4 CAP < 2^16), so a claimed cursor is the word's address
+    // (one array: the compiler places separate __shared__ arrays largest first)
+    // LSV bit 0: kNet words of padding after s_k (unconditional network reads)
+    __shared__ uint32_t s_lds[kSubBuckets / 2 + CAP + ((LSV & 1) ? kNet : 0) + CAP];
+    uint32_t* const s_cnt = s_lds;                    // two 16-bit halves per word: sub-buckets 2 t, 2 t + 1
+    uint32_t* const s_k = s_lds + kSubBuckets / 2;   // (key bits below the sub-bucket) << kSlotBits | load slot
+    uint32_t* const s_x = s_k + CAP + ((LSV & 1) ? kNet : 0);   // index of each load slot
     __shared__ uint32_t s_tmp[WAVES];
     __shared__ uint32_t s_cm[WAVES];
     __shared__ uint32_t s_ug[WAVES];
@@ -1902,7 +1910,19 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
     const uint32_t dsh = ib + low_bits;
     const uint32_t lmask = (1u << low_bits) - 1u;
     const uint64_t imask = (1ull << ib) - 1ull;
-    auto end_of = [&](uint32_t sb) -> uint32_t { return (s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu; };
+    auto end_of = [&](uint32_t sb) -> uint32_t { return ((s_cnt[sb >> 1] >> (16 * (sb & 1))) & 0xFFFFu) >> 2; };
+    static_assert(4 * CAP < (1 << 16), "byte counts in 16-bit halves");
+    // sub-bucket sb = (w >> dsh) & 2047 of an item: y = w >> dsh, its counter
+    // word's byte address (y << 1) & 0xFFC, the half's shift y << 4 (shifts
+    // and bit-field extracts use the low 5 bits: (sb & 1) * 16)
+    auto cnt_word = [&](uint32_t y) -> uint32_t* {
+        return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_cnt) + ((y << 1) & 0xFFCu));
+    };
+    auto half_inc = [](uint32_t y) -> uint32_t {   // 4 << ((sb & 1) * 16)
+        uint32_t r;
+        asm("v_lshlrev_b32_e64 %0, %1, 4" : "=v"(r) : "v"(y << 4));
+        return r;
+    };
     Probe probe;
     if (threadIdx.x == 0) {
         s_q[0] = atomicAdd(&words[kTicketWord], 1u);
@@ -1962,15 +1982,15 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         if (sfull) {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
-                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                const uint32_t y = (uint32_t)(w[i] >> dsh);
+                atomicAdd(cnt_word(y), half_inc(y));
             }
         } else {
 #pragma unroll
             for (int i = 0; i < ITEMS; ++i) {
                 if (slot_ok(i)) {
-                    const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                    atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
+                    const uint32_t y = (uint32_t)(w[i] >> dsh);
+                    atomicAdd(cnt_word(y), half_inc(y));
                 }
             }
         }
@@ -2016,7 +2036,7 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
         }
         __syncthreads();
         probe.mark(2);
-        if (big > kMaxSub) {   // uniform: clustered keys -> the measured-span kernel
+        if ((big >> 2) > kMaxSub) {   // uniform: clustered keys -> the measured-span kernel
             // (XQ: k_window_gather copies the retried windows to their SA
             // positions for it; storing the items here made this kernel spill)
             if (threadIdx.x == 0) retry[atomicAdd(&words[kRetryWord], 1u)] = j;
@@ -2029,14 +2049,34 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
             // 2. scatter the 32-bit words into sub-buckets (any order inside
             // one); the indices stay by load slot
             auto scatter1 = [&](int i, uint32_t le) {
-                const uint32_t sb = (uint32_t)(w[i] >> dsh) & (kSubBuckets - 1);
-                const uint32_t old = atomicAdd(&s_cnt[sb >> 1], 1u << (16 * (sb & 1)));
-                s_k[(old >> (16 * (sb & 1))) & 0xFFFFu] = (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
+                const uint32_t y = (uint32_t)(w[i] >> dsh);
+                const uint32_t old = atomicAdd(cnt_word(y), half_inc(y));
+                const uint32_t at = __builtin_amdgcn_ubfe(old, y << 4, 16u);   // byte address in s_k
+                *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_k) + at) =
+                    (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
                 s_x[le] = (uint32_t)(w[i] & imask);
             };
             if (sfull) {
+                // claims in groups of SA_LS_CLAIMS (the atomics' round trips
+                // overlap; one at a time, each item waited for its own)
 #pragma unroll
-                for (int i = 0; i < ITEMS; ++i) scatter1(i, l0 + i * kWave);
+                for (int g = 0; g < ITEMS; g += SA_LS_CLAIMS) {
+                    uint32_t y[SA_LS_CLAIMS], old[SA_LS_CLAIMS];
+#pragma unroll
+                    for (int t = 0; t < SA_LS_CLAIMS; ++t) {
+                        y[t] = (uint32_t)(w[g + t] >> dsh);
+                        old[t] = atomicAdd(cnt_word(y[t]), half_inc(y[t]));
+                    }
+#pragma unroll
+                    for (int t = 0; t < SA_LS_CLAIMS; ++t) {
+                        const int i = g + t;
+                        const uint32_t le = l0 + i * kWave;
+                        const uint32_t at = __builtin_amdgcn_ubfe(old[t], y[t] << 4, 16u);
+                        *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(s_k) + at) =
+                            (((uint32_t)(w[i] >> ib) & lmask) << kSlotBits) | le;
+                        s_x[le] = (uint32_t)(w[i] & imask);
+                    }
+                }
             } else {
 #pragma unroll
                 for (int i = 0; i < ITEMS; ++i) {

@@ -7,9 +7,9 @@ rev=${1:-HEAD}; name=${2:-head}
 tmp=$(mktemp -d)
 git archive "$rev" hpc_suffix_array_amd/csrc include | tar -x -C "$tmp"
 C=$tmp/hpc_suffix_array_amd/csrc
-mkdir -p ab/$name
-/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c -x hip $C/sa_build.hip -o ab/$name/sa_build.o
-g++ -O3 -std=c++17 -fPIC -c $C/sa_dropin.cpp -o ab/$name/sa_dropin.o
-g++ -O3 -std=c++17 -fPIC -c $C/sa_debug.cpp -o ab/$name/sa_debug.o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -rdynamic ab/$name/sa_build.o ab/$name/sa_dropin.o ab/$name/sa_debug.o -o ab/$name/libsa_hip.so
+AB=${AB_DIR:-ab}; mkdir -p $AB/$name
+/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -c -x hip $C/sa_build.hip -o $AB/$name/sa_build.o
+g++ -O3 -std=c++17 -fPIC -c $C/sa_dropin.cpp -o $AB/$name/sa_dropin.o
+g++ -O3 -std=c++17 -fPIC -c $C/sa_debug.cpp -o $AB/$name/sa_debug.o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -rdynamic $AB/$name/sa_build.o $AB/$name/sa_dropin.o $AB/$name/sa_debug.o -o $AB/$name/libsa_hip.so
 rm -rf "$tmp"

@@ -3,7 +3,7 @@
 set -e
 mkdir -p gpurun_out/ab
 for v in default "$@" default "$@"; do
-  if [ "$v" = default ]; then unset SA_LIB_PATH; else export SA_LIB_PATH=$PWD/ab/$v/libsa_hip.so; fi
+  if [ "$v" = default ]; then unset SA_LIB_PATH; else export SA_LIB_PATH=$PWD/${AB_DIR:-ab}/$v/libsa_hip.so; fi
   timeout -k 10 120 python -u bench.py --no-cpu-baseline --no-reference-schedule --steps 10 --warmup 2 > gpurun_out/ab/$v.log 2>&1
   python - "$v" gpurun_out/ab/$v.log <<'PY'
 import json,sys
