@@ -8,11 +8,11 @@ cd "$(dirname "$0")/.."
 C=hpc_suffix_array_amd/csrc
 make -s -C $C
 for v in "$@"; do
-  mkdir -p ab/$v
+  AB=${AB_DIR:-ab}; mkdir -p $AB/$v
   defs=$(echo "$v" | tr '+' '\n' | sed 's/^/-D/' | tr '\n' ' ')
-  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $defs -c -x hip $C/sa_build.hip -o ab/$v/sa_build.o &
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 $defs -c -x hip $C/sa_build.hip -o $AB/$v/sa_build.o &
 done
 wait
 for v in "$@"; do
-  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -rdynamic ab/$v/sa_build.o $C/build/sa_dropin.o $C/build/sa_debug.o -o ab/$v/libsa_hip.so
+  /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -rdynamic $AB/$v/sa_build.o $C/build/sa_dropin.o $C/build/sa_debug.o -o $AB/$v/libsa_hip.so
 done
