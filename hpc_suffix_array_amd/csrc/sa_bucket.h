@@ -1874,7 +1874,7 @@ __global__ __launch_bounds__(kBlock) void k_window_rows(const uint32_t* __restri
 #define SA_LS_WFULL 1
 #endif
 #ifndef SA_LS_CLAIMS
-#define SA_LS_CLAIMS 3   // (must divide ITEMS)
+#define SA_LS_CLAIMS 1   // (must divide ITEMS; 3 / 6 / 9 at a time measured no faster: profiles/r06_t_ab_local_sort_claims.txt)
 #endif
 template <int BLOCK, int ITEMS, class Probe = NoProbe, bool XQ = false, int LSV = 0, bool CR = false>
 __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __restrict__ keys_in,
@@ -2057,8 +2057,8 @@ __global__ __launch_bounds__(BLOCK, 4) void k_bucket_sort(const uint64_t* __rest
                 s_x[le] = (uint32_t)(w[i] & imask);
             };
             if (sfull) {
-                // claims in groups of SA_LS_CLAIMS (the atomics' round trips
-                // overlap; one at a time, each item waited for its own)
+                // claims in groups of SA_LS_CLAIMS (> 1: the atomics' round
+                // trips overlap, at more live registers)
 #pragma unroll
                 for (int g = 0; g < ITEMS; g += SA_LS_CLAIMS) {
                     uint32_t y[SA_LS_CLAIMS], old[SA_LS_CLAIMS];
