@@ -52,6 +52,7 @@ constexpr int kChkItems = 8;
 struct ChkSrcA {
     const uint32_t* __restrict__ sa;
     static constexpr int DSH = 32;
+    static constexpr int kNb = 0;   // pair() reads no neighbour word (see ChkSrcB)
     __device__ __forceinline__ uint64_t dest(uint64_t r, uint64_t n, uint32_t& bad) const {
         const uint32_t x = sa[r];
         if (x >= n) {
@@ -71,6 +72,20 @@ struct ChkSrcB {
     const uint32_t* __restrict__ isa;
     const uint8_t* __restrict__ text;
     static constexpr int DSH = 40;
+    // kNb = +1: pair(i) needs word(i + 1), the next lane's word (k_chk_bin
+    // passes it by a lane shuffle; only a wave's last lane loads it)
+    static constexpr int kNb = 1;
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return isa[i]; }
+    __device__ __forceinline__ uint64_t dest_w(uint32_t x, uint64_t n, uint32_t& bad) const {
+        if (x == 0u || x > n) {
+            bad |= 8u;
+            return ~0ull;
+        }
+        return x - 1u;
+    }
+    __device__ __forceinline__ uint64_t pair_w(uint64_t i, uint64_t d, uint64_t n, uint32_t s1, uint32_t nx) const {
+        return ((d & ((1ull << s1) - 1ull)) << 40) | ((uint64_t)text[i] << 32) | (i + 1 < n ? nx : 0u);
+    }
     __device__ __forceinline__ uint64_t dest(uint64_t i, uint64_t n, uint32_t& bad) const {
         const uint32_t x = isa[i];
         if (x == 0u || x > n) {   // (only after pass A failed)
@@ -91,6 +106,15 @@ struct ChkSrcB {
 struct PhiSrc {
     const uint32_t* __restrict__ sa;
     static constexpr int DSH = 32;
+    // kNb = -1: pair(r) needs word(r - 1), the previous lane's word
+    static constexpr int kNb = -1;
+    __device__ __forceinline__ uint32_t word(uint64_t r) const { return sa[r]; }
+    __device__ __forceinline__ uint64_t dest_w(uint32_t x, uint64_t n, uint32_t&) const {
+        return x < n ? (uint64_t)x : ~0ull;
+    }
+    __device__ __forceinline__ uint64_t pair_w(uint64_t r, uint64_t d, uint64_t n, uint32_t, uint32_t p) const {
+        return (d << 32) | (r && p < n ? p + 1u : 0u);
+    }
     __device__ __forceinline__ uint64_t dest(uint64_t r, uint64_t n, uint32_t&) const {
         const uint32_t x = sa[r];
         return x < n ? (uint64_t)x : ~0ull;
@@ -141,18 +165,49 @@ __global__ __launch_bounds__(BLOCK) void k_chk_bin(Src src, uint64_t n, uint32_t
     __syncthreads();
     uint32_t bad = 0;
     uint64_t d[ITEMS];
-#pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
-        d[j] = e < n ? src.dest(e, n, bad) : ~0ull;
-    }
     uint64_t p[ITEMS];
     uint32_t slot[ITEMS];
+    if constexpr (Src::kNb != 0) {
+        // element e's neighbour word (e + kNb) is the adjacent lane's word:
+        // a lane shuffle, and one load by the wave's edge lane
+        const uint32_t lane = lane_id();
+        uint32_t x[ITEMS];
 #pragma unroll
-    for (int j = 0; j < ITEMS; ++j) {
-        const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
-        p[j] = d[j] != ~0ull ? src.pair(e, d[j], n, s1) : 0ull;
-        slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+            x[j] = e < n ? src.word(e) : 0u;
+        }
+        uint32_t nb[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+            if constexpr (Src::kNb > 0) {
+                nb[j] = (uint32_t)__shfl_down((int)x[j], 1, kWave);
+                if (lane == kWave - 1) nb[j] = e + 1 < n ? src.word(e + 1) : 0u;
+            } else {
+                nb[j] = (uint32_t)__shfl_up((int)x[j], 1, kWave);
+                if (lane == 0) nb[j] = e > 0 && e - 1 < n ? src.word(e - 1) : 0u;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+            d[j] = e < n ? src.dest_w(x[j], n, bad) : ~0ull;
+            p[j] = d[j] != ~0ull ? src.pair_w(e, d[j], n, s1, nb[j]) : 0ull;
+            slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+            d[j] = e < n ? src.dest(e, n, bad) : ~0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
+            p[j] = d[j] != ~0ull ? src.pair(e, d[j], n, s1) : 0ull;
+            slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
+        }
     }
     __syncthreads();
     const uint32_t cnt = tid < (uint32_t)NB ? s_cnt[tid] : 0u;

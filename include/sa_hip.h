@@ -112,7 +112,12 @@ typedef struct {
                                (its windows all take the measured-span retry) */
     int32_t tune;           /* A/B shapes, 0 = defaults: bits 0-7 the reference
                                schedule's widest LSD digit (8..10), bits 8-15 the
-                               first bucket pass's cursor stripes (1, 2, 4, 8) */
+                               first bucket pass's cursor stripes (1, 2, 4, 8),
+                               16-19 local-sort variants, 20-23 checker level-1
+                               bins / persistent split, 24-27 = 1 the persistent
+                               re-rank split, 28 no 32-bit rolling (12-byte
+                               first-pass items), 29 window-order local-sort
+                               rows (no chunk rows) */
 } sa_opts;
 
 typedef struct {
