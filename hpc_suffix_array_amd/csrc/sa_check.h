@@ -52,16 +52,16 @@ constexpr int kChkItems = 8;
 struct ChkSrcA {
     const uint32_t* __restrict__ sa;
     static constexpr int DSH = 32;
-    static constexpr int kNb = 0;   // pair() reads no neighbour word (see ChkSrcB)
-    __device__ __forceinline__ uint64_t dest(uint64_t r, uint64_t n, uint32_t& bad) const {
-        const uint32_t x = sa[r];
+    static constexpr int kNb = 0;   // pair_w needs no neighbour word (see ChkSrcB)
+    __device__ __forceinline__ uint32_t word(uint64_t r) const { return sa[r]; }
+    __device__ __forceinline__ uint64_t dest_w(uint32_t x, uint64_t n, uint32_t& bad) const {
         if (x >= n) {
             bad |= 1u;
             return ~0ull;
         }
         return x;
     }
-    __device__ __forceinline__ uint64_t pair(uint64_t r, uint64_t d, uint64_t, uint32_t) const {
+    __device__ __forceinline__ uint64_t pair_w(uint64_t r, uint64_t d, uint64_t, uint32_t, uint32_t) const {
         return (d << 32) | (uint32_t)(r + 1);
     }
 };
@@ -72,7 +72,7 @@ struct ChkSrcB {
     const uint32_t* __restrict__ isa;
     const uint8_t* __restrict__ text;
     static constexpr int DSH = 40;
-    // kNb = +1: pair(i) needs word(i + 1), the next lane's word (k_chk_bin
+    // kNb = +1: pair_w(i) needs word(i + 1), the next lane's word (k_chk_bin
     // passes it by a lane shuffle; only a wave's last lane loads it)
     static constexpr int kNb = 1;
     __device__ __forceinline__ uint32_t word(uint64_t i) const { return isa[i]; }
@@ -86,18 +86,6 @@ struct ChkSrcB {
     __device__ __forceinline__ uint64_t pair_w(uint64_t i, uint64_t d, uint64_t n, uint32_t s1, uint32_t nx) const {
         return ((d & ((1ull << s1) - 1ull)) << 40) | ((uint64_t)text[i] << 32) | (i + 1 < n ? nx : 0u);
     }
-    __device__ __forceinline__ uint64_t dest(uint64_t i, uint64_t n, uint32_t& bad) const {
-        const uint32_t x = isa[i];
-        if (x == 0u || x > n) {   // (only after pass A failed)
-            bad |= 8u;
-            return ~0ull;
-        }
-        return x - 1u;
-    }
-    __device__ __forceinline__ uint64_t pair(uint64_t i, uint64_t d, uint64_t n, uint32_t s1) const {
-        const uint32_t nx = i + 1 < n ? isa[i + 1] : 0u;
-        return ((d & ((1ull << s1) - 1ull)) << 40) | ((uint64_t)text[i] << 32) | nx;
-    }
 };
 
 // LCP's PHI (sa_lcp.h) by the same permutation: element r -> destination
@@ -106,21 +94,13 @@ struct ChkSrcB {
 struct PhiSrc {
     const uint32_t* __restrict__ sa;
     static constexpr int DSH = 32;
-    // kNb = -1: pair(r) needs word(r - 1), the previous lane's word
+    // kNb = -1: pair_w(r) needs word(r - 1), the previous lane's word
     static constexpr int kNb = -1;
     __device__ __forceinline__ uint32_t word(uint64_t r) const { return sa[r]; }
     __device__ __forceinline__ uint64_t dest_w(uint32_t x, uint64_t n, uint32_t&) const {
         return x < n ? (uint64_t)x : ~0ull;
     }
     __device__ __forceinline__ uint64_t pair_w(uint64_t r, uint64_t d, uint64_t n, uint32_t, uint32_t p) const {
-        return (d << 32) | (r && p < n ? p + 1u : 0u);
-    }
-    __device__ __forceinline__ uint64_t dest(uint64_t r, uint64_t n, uint32_t&) const {
-        const uint32_t x = sa[r];
-        return x < n ? (uint64_t)x : ~0ull;
-    }
-    __device__ __forceinline__ uint64_t pair(uint64_t r, uint64_t d, uint64_t n, uint32_t) const {
-        const uint32_t p = r ? sa[r - 1] : 0u;
         return (d << 32) | (r && p < n ? p + 1u : 0u);
     }
 };
@@ -167,9 +147,12 @@ __global__ __launch_bounds__(BLOCK) void k_chk_bin(Src src, uint64_t n, uint32_t
     uint64_t d[ITEMS];
     uint64_t p[ITEMS];
     uint32_t slot[ITEMS];
-    if constexpr (Src::kNb != 0) {
-        // element e's neighbour word (e + kNb) is the adjacent lane's word:
-        // a lane shuffle, and one load by the wave's edge lane
+    {   // (a source: word(e), dest_w(word), pair_w(e, dest, n, s1, neighbour word))
+        // every element's word loaded first, all loads in flight before the
+        // first use (separate dest / pair loops ran pass A's level 1 at 4.26
+        // ms, this 3.4); an element's neighbour word (e + kNb) is the
+        // adjacent lane's: a lane shuffle, and one load by the wave's edge
+        // lane (ChkSrcB 5.41 -> 4.69 ms, PhiSrc 4.60 -> 3.37)
         const uint32_t lane = lane_id();
         uint32_t x[ITEMS];
 #pragma unroll
@@ -181,7 +164,9 @@ __global__ __launch_bounds__(BLOCK) void k_chk_bin(Src src, uint64_t n, uint32_t
 #pragma unroll
         for (int j = 0; j < ITEMS; ++j) {
             const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
-            if constexpr (Src::kNb > 0) {
+            if constexpr (Src::kNb == 0) {
+                nb[j] = 0u;
+            } else if constexpr (Src::kNb > 0) {
                 nb[j] = (uint32_t)__shfl_down((int)x[j], 1, kWave);
                 if (lane == kWave - 1) nb[j] = e + 1 < n ? src.word(e + 1) : 0u;
             } else {
@@ -194,18 +179,6 @@ __global__ __launch_bounds__(BLOCK) void k_chk_bin(Src src, uint64_t n, uint32_t
             const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
             d[j] = e < n ? src.dest_w(x[j], n, bad) : ~0ull;
             p[j] = d[j] != ~0ull ? src.pair_w(e, d[j], n, s1, nb[j]) : 0ull;
-            slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
-        }
-    } else {
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
-            d[j] = e < n ? src.dest(e, n, bad) : ~0ull;
-        }
-#pragma unroll
-        for (int j = 0; j < ITEMS; ++j) {
-            const uint64_t e = tb + (uint64_t)j * BLOCK + tid;
-            p[j] = d[j] != ~0ull ? src.pair(e, d[j], n, s1) : 0ull;
             slot[j] = d[j] != ~0ull ? atomicAdd(&s_cnt[(uint32_t)(d[j] >> s1)], 1u) : 0u;
         }
     }
