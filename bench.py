@@ -132,10 +132,22 @@ def cpu_baseline(kind: str, n_sample: int, seed: int, reps: int = 3) -> dict:
                     break
     except OSError:
         pass
-    return {"value": n_sample / med, "unit": "suffixes/s", "cores": 1, "kind": "port",
-            "sample": f"{kind} n={n_sample} seed={seed}, oracle/mm_oracle.c single thread pinned to core {core}, "
-                      f"median of {reps} ({med:.2f} s, {rounds} rounds), cpu '{model}', "
-                      f"host cpus {os.cpu_count()}"}
+    out = {"value": n_sample / med, "unit": "suffixes/s", "cores": 1, "kind": "port",
+           "sample": f"{kind} n={n_sample} seed={seed}, oracle/mm_oracle.c single thread pinned to core {core}, "
+                     f"median of {reps} ({med:.2f} s, {rounds} rounds), cpu '{model}', "
+                     f"host cpus {os.cpu_count()}"}
+    # the same restatement at configs[2]'s full size, timed once on a GPU box
+    # host (scripts/cpu_baseline_1g.py; ~150 s, so not inside every bench run)
+    full = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "r06_cpu_baseline_1g.txt")
+    if kind == "dna" and os.path.exists(full):
+        for line in open(full):
+            if line.startswith("{"):
+                f = json.loads(line)
+                out["full_size"] = {"n": f["n"], "value": f["suffixes_per_s"], "seconds": f["seconds"],
+                                    "cores": f["cores"], "cpu": f["cpu"],
+                                    "sa_matches_known_answer": f["sa_sha256_matches_known_answer"],
+                                    "source": "profiles/r06_cpu_baseline_1g.txt"}
+    return out
 
 
 def tag_order(tag: str) -> tuple:
