@@ -598,7 +598,9 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
                 // (past the end L wraps: never ranked; FULL tiles are interior)
                 const uint64_t low = (FULL || interior) ? (uint64_t)r * mulR + addR : bucket_low(b, r, n - (tb + l0 + j));
                 k[j] = ((uint64_t)D << b.rb) | low;
-                const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * b.cmul) >> b.bsh);
+                // (a non-power-of-two sigma has sigma^s > 2^16 = 2^bb at least,
+                // so cmul = 2^48 / sigma^s < 2^32: one 32 x 32 multiply)
+                const uint32_t bk = POW2 ? (D >> bksh) : (uint32_t)(((uint64_t)D * (uint32_t)b.cmul) >> b.bsh);
                 const uint32_t lb = bk - blo;
                 if constexpr (FULL) {
                     const uint32_t d = lb & (RADIX - 1);
@@ -669,13 +671,14 @@ __global__ __launch_bounds__(BLOCK, 2048 / BLOCK) void k_split_text(const uint8_
             const uint32_t d = dr[j] >> 16;
             if (d < (uint32_t)RADIX) {
                 const uint32_t pos = s_start[d] + (dr[j] & 0xFFFFu);
-                if constexpr (NP2) {
-                    const uint64_t prod = (k[j] >> b.rb) * b.cmul;
+                if constexpr (NP2) {   // (D < 2^32, cmul < 2^32: 32 x 32 multiplies)
+                    const uint32_t cm32 = (uint32_t)b.cmul;
+                    const uint64_t prod = (uint64_t)(uint32_t)(k[j] >> b.rb) * cm32;
                     const uint32_t bk = (uint32_t)(prod >> b.bsh);
                     const uint32_t f = (uint32_t)(prod & fmask);
                     uint32_t rd = (uint32_t)((double)f * icm);
-                    rd = ((uint64_t)rd * b.cmul > f) ? rd - 1u : rd;
-                    rd = ((uint64_t)(rd + 1u) * b.cmul <= f) ? rd + 1u : rd;
+                    rd = ((uint64_t)rd * cm32 > f) ? rd - 1u : rd;
+                    rd = ((uint64_t)(rd + 1u) * cm32 <= f) ? rd + 1u : rd;
                     const uint32_t hi = (bk - blo) >> kLoBits;   // local bucket
                     const uint64_t rel = ((uint64_t)rd << b.rb) | (k[j] & ((1ull << b.rb) - 1ull));
                     s_keys[pos] = ((uint64_t)hi << (64u - pk_hb)) | (rel << pk_ib) | (tb + ITEMS * dg + j);
