@@ -1961,7 +1961,30 @@ static int lcp_device(sa_context* c, const uint8_t* d_text, uint64_t n, const ui
     hipLaunchKernelGGL(k_chunk_max, dim3(ch.chunks), dim3(kBlock), 0, s, (const uint32_t*)v, ch, c->hist);
     hipLaunchKernelGGL(k_scan_chunk_max, dim3(1), dim3(kBlock), 0, s, c->hist, ch.chunks);
     hipLaunchKernelGGL(k_plcp_apply, dim3(ch.chunks), dim3(kBlock), 0, s, v, ch, (const uint32_t*)c->hist);
-    hipLaunchKernelGGL(k_lcp_gather, dim3(grid), dim3(kBlock), 0, s, d_sa, n, (const uint32_t*)v, d_lcp, best);
+    // LCP[r] = PLCP[SA[r]] (:147-155): ISA + 1 by the coalesced permutation
+    // (into vals_alt, free after the long rounds), then PLCP placed at ISA
+    // -- 2 x ~8.6 ms of streamed traffic at 1 GiB against a 24.7 ms random
+    // 4-byte gather (146 GB moved); tune bit 30: the gather (A/B runs)
+    if ((((uint32_t)c->tune >> 30) & 1u) || n < 2) {
+        hipLaunchKernelGGL(k_lcp_gather, dim3(grid), dim3(kBlock), 0, s, d_sa, n, (const uint32_t*)v, d_lcp, best);
+    } else {
+        uint32_t* isa1 = c->vals_alt;
+        for (int pass = 0; pass < 2; ++pass) {
+            for (uint32_t stripes : {kChkStripes, 1u}) {
+                SA_HIP(hipMemsetAsync(c->words + 12, 0, 4, s));
+                if (pass == 0)
+                    SA_TRY(place_by_permutation<IsaSrc, 3>(c, IsaSrc{{d_sa}}, n, isa1, c->words + 12, s, stripes));
+                else
+                    SA_TRY(place_by_permutation<PlcpSrc, 4>(c, PlcpSrc{isa1, v}, n, d_lcp, c->words + 12, s,
+                                                            stripes));
+                if (stripes == 1) break;
+                SA_HIP(hipMemcpyAsync(c->host_words + 12, c->words + 12, 4, hipMemcpyDeviceToHost, s));
+                SA_HIP(host_sync(s));
+                if (!(c->host_words[12] & 128u)) break;
+            }
+        }
+        hipLaunchKernelGGL(k_lcp_best, dim3(grid), dim3(kBlock), 0, s, (const uint32_t*)d_lcp, n, best);
+    }
     SA_HIP(hipGetLastError());
     SA_HIP(hipMemcpyAsync(c->host_words + 8, best, 8, hipMemcpyDeviceToHost, s));
     SA_HIP(hipMemcpyAsync(c->host_words + 16, cnt, (kLongRounds + 1) * 4, hipMemcpyDeviceToHost, s));

@@ -88,6 +88,31 @@ struct ChkSrcB {
     }
 };
 
+// LCP's ISA + 1 (sa_lcp.h: LCP[r] = PLCP[SA[r]] by two permutations instead
+// of a random gather): pass A's source under its own name, so profiles keep
+// the two apart
+struct IsaSrc : ChkSrcA {};
+
+// LCP[r] = PLCP[i] placed at r = ISA[i] (isa1 = ISA + 1, from IsaSrc); LCP[0]
+// = 0 (PLCP at SA[0] is unused, :147)
+struct PlcpSrc {
+    const uint32_t* __restrict__ isa1;
+    const uint32_t* __restrict__ plcp;
+    static constexpr int DSH = 32;
+    static constexpr int kNb = 0;
+    __device__ __forceinline__ uint32_t word(uint64_t i) const { return isa1[i]; }
+    __device__ __forceinline__ uint64_t dest_w(uint32_t x, uint64_t n, uint32_t& bad) const {
+        if (x == 0u || x > n) {   // (an invalid SA only)
+            bad |= 8u;
+            return ~0ull;
+        }
+        return x - 1u;
+    }
+    __device__ __forceinline__ uint64_t pair_w(uint64_t i, uint64_t d, uint64_t, uint32_t, uint32_t) const {
+        return (d << 32) | (d ? plcp[i] : 0u);
+    }
+};
+
 // LCP's PHI (sa_lcp.h) by the same permutation: element r -> destination
 // SA[r], value PHI'[SA[r]] = SA[r - 1] + 1 (0 for r = 0: no predecessor;
 // a hole of an invalid SA reads as 0 too, so PHI' - 1 never indexes past n)

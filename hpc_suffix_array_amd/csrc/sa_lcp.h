@@ -242,4 +242,21 @@ __global__ __launch_bounds__(kBlock) void k_lcp_gather(const uint32_t* __restric
     if (lane_id() == 0 && (b >> 32)) atomicMax(best, b);
 }
 
+// the LRS over the finished LCP array: max over r >= 1 of (LCP[r] << 32 | ~r)
+// (first r with the strictly largest value, as :165-171)
+__global__ __launch_bounds__(kBlock) void k_lcp_best(const uint32_t* __restrict__ lcp, uint64_t n,
+                                                     unsigned long long* __restrict__ best) {
+    unsigned long long b = 0;
+    for (uint64_t r = (uint64_t)blockIdx.x * kBlock + threadIdx.x + 1; r < n; r += (uint64_t)gridDim.x * kBlock) {
+        const unsigned long long k = ((unsigned long long)lcp[r] << 32) | (0xFFFFFFFFull - r);
+        b = b > k ? b : k;
+    }
+#pragma unroll
+    for (int o = kWave / 2; o > 0; o >>= 1) {
+        const unsigned long long y = __shfl_xor(b, o, kWave);
+        b = b > y ? b : y;
+    }
+    if (lane_id() == 0 && (b >> 32)) atomicMax(best, b);
+}
+
 }  // namespace sa

@@ -21,7 +21,7 @@ import shutil
 import sys
 from collections import defaultdict
 
-KINDS = [("k_chk_bin<1024, 8, sa::ChkSrcA", "check_bin_a"), ("k_chk_bin<1024, 8, sa::ChkSrcB", "check_bin_b"),
+KINDS = [("k_chk_bin<1024, 8, sa::IsaSrc", "lcp_isa_bin"), ("k_chk_split<1024, 8, 32, 3", "lcp_isa_split"), ("k_perm_split<1024, 8, 32, true, 3", "lcp_isa_split"), ("k_perm_place<1024, false, 3", "lcp_isa_place"), ("k_chk_bin<1024, 8, sa::PlcpSrc", "lcp_place_bin"), ("k_chk_split<1024, 8, 32, 4", "lcp_place_split"), ("k_perm_split<1024, 8, 32, true, 4", "lcp_place_split"), ("k_perm_place<1024, false, 4", "lcp_place_place"), ("k_lcp_best", "lcp_best"), ("k_chk_bin<1024, 8, sa::ChkSrcA", "check_bin_a"), ("k_chk_bin<1024, 8, sa::ChkSrcB", "check_bin_b"),
          ("k_chk_bin<1024, 8, sa::PhiSrc", "lcp_phi_bin"), ("k_chk_split<1024, 8, 32, 2", "lcp_phi_split"),
          ("k_perm_split<1024, 8, 32, true, 2", "lcp_phi_split"), ("k_perm_place<1024, false, 2", "lcp_phi_place"),
          ("k_perm_split<1024, 8, 32, true", "check_split_a"), ("k_perm_split<1024, 8, 40, true", "check_split_b"),
