@@ -117,7 +117,8 @@ typedef struct {
                                bins / persistent split, 24-27 = 1 the persistent
                                re-rank split, 28 no 32-bit rolling (12-byte
                                first-pass items), 29 window-order local-sort
-                               rows (no chunk rows) */
+                               rows (no chunk rows), 30 LCP by the random gather
+                               (no permutations) */
 } sa_opts;
 
 typedef struct {
